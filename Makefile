@@ -1,0 +1,28 @@
+# Build the product library (librein48.so: gfx950 kernels + C-ABI) and the test-only oracle.
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+HIPFLAGS ?= -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -Wall -Wno-unused-function
+LIBDIR := rein48_amd/lib
+SRC := rein48_amd/csrc/r48_env.hip
+DEPS := rein48_amd/csrc/r48_board.h include/rein48.h
+
+all: $(LIBDIR)/librein48.so oracle
+
+$(LIBDIR)/librein48.so: $(SRC) $(DEPS)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(SRC)
+
+# assembly + register report for the hot kernels (not needed for the build)
+asm: $(SRC) $(DEPS)
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) --cuda-device-only -S -o build/r48_env.s $(SRC)
+	$(HIPCC) $(HIPFLAGS) --cuda-device-only -c -o /dev/null -Rpass-analysis=kernel-resource-usage $(SRC) 2> build/resource_usage.txt
+
+oracle:
+	$(MAKE) -s -C oracle
+
+clean:
+	rm -rf $(LIBDIR) build
+	$(MAKE) -s -C oracle clean
+
+.PHONY: all asm oracle clean

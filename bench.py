@@ -1,0 +1,261 @@
+#!/usr/bin/env python3
+"""bench.py -- env steps/sec on 4x4 boards (BASELINE.json metric), MI355X.
+
+Workload (BASELINE.json configs[1], "1M parallel 4x4 int8 boards, random policy, env-only
+throughput on 1 MI355X"): 2^20 boards per GPU, every step = one gfx950 k_step launch over
+all of them (move + spawn + game-over + auto-reset, in-kernel uniform random policy,
+actions and done flags written back). Boards start from the reference reset rule (one
+tile) and are resident in HBM before the timed region. Steps are issued in hipGraph
+chunks (r48_env_step_n) so the host never gates the GPU.
+
+Multi-GPU: one process per GPU (torchrun), each rank owns boards [rank*N, (rank+1)*N)
+(Philox keyed by global board id); no data-path collective. Timing: barrier + sync on
+both sides of exactly K steps, max over ranks; value = all boards x K / that time.
+
+Extra objects on the JSON line:
+  roofline      HBM roofline of k_step: 34 algorithmic bytes per board-step (16 B board in,
+                16 B out, 1 B action out, 1 B done out) per launch / the kernel's average
+                duration from HIP events over the timed region; peak 8 TB/s (MI355X spec).
+                `traffic` = per-launch HBM bytes from rocprofv3 PMC passes when
+                profiles/pmc_k_step.json exists (tools/pmc_traffic.py), else null.
+  cpu_baseline  oracle/game_port.py (faithful pure-Python restatement of the reference
+                Game + Rand, calibrated against the reference in BASELINE.md) on one host
+                core for a bounded sample, rank 0, N=1 only.
+  extras        HBM-honest point (2^26 boards/GPU, past the 256 MiB Infinity Cache), the
+                fused random-policy rollout kernel, and the C oracle as a strong CPU line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "env steps/sec (whole node), 4×4 boards, at 1/2/4/8 MI355X"
+ALGO_BYTES = 34            # per board-step, see module docstring
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
+HBM_MEASURED_GBS = 6290.0  # float4 copy measured on MI355X (same guide)
+
+
+def chunks(total, size):
+    out = [size] * (total // size)
+    if total % size:
+        out.append(total % size)
+    return out
+
+
+def warm_plan(warmup, chunk, timed_plan):
+    """Warm-up steps that also instantiate every graph size the timed plan uses."""
+    plan, left = [], warmup
+    for c in sorted(set(timed_plan), reverse=True):
+        if left >= c:
+            plan.append(c)
+            left -= c
+    plan += [1] * left
+    return plan
+
+
+def cpu_baseline(seconds):
+    """oracle/game_port.py on one core for ~`seconds` (bounded sample)."""
+    from oracle import game_port
+    import platform
+    steps, t0 = 0, time.perf_counter()
+    seed = 0
+    while time.perf_counter() - t0 < seconds:
+        game_port.run_steps(20_000, seed=seed)
+        steps += 20_000
+        seed += 1
+    dt = time.perf_counter() - t0
+    cpu = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": steps / dt, "unit": "env steps/s", "cores": 1, "kind": "port",
+            "sample": "%d random-policy steps of oracle/game_port.py (list-of-lists, deepcopy per move, "
+                      "global random; auto-restart on game over) in %.1f s on 1 core of %s (%s)"
+                      % (steps, dt, cpu, platform.python_version())}
+
+
+def strong_cpu_line(seconds=2.0):
+    from oracle import native as O
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        O.bench_pyrand(n + 1, 1_000_000)
+        n += 1_000_000
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "env steps/s", "cores": 1, "kind": "oracle C restatement",
+            "sample": "%d steps, one board, CPython-compatible MT19937 draws" % n}
+
+
+def kernel_events(env, launches, chunk=None):
+    """Per-launch duration of k_step (ms) from HIP events on the env's stream."""
+    s = torch.cuda.current_stream(env.device)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(launches)]
+    for a, b in ev:
+        a.record(s)
+        env.step(None, auto_reset=True)
+        b.record(s)
+    torch.cuda.synchronize(env.device)
+    return [a.elapsed_time(b) for a, b in ev]
+
+
+def extras(dev, seed, n_small):
+    from rein48_amd import VecGame
+    out = {}
+    # HBM-honest: 2^26 boards (1 GiB of boards) -- far beyond the 256 MiB Infinity Cache
+    big = 1 << 26
+    env = VecGame(big, device=dev, seed=seed)
+    env.reset()
+    for _ in range(3):
+        env.step(None, auto_reset=True)
+    ms = kernel_events(env, 20)
+    avg = sum(ms) / len(ms)
+    out["hbm_honest"] = {"boards": big, "launches": len(ms), "kernel_ms": avg,
+                         "env_steps_per_s": big / (avg * 1e-3),
+                         "achieved_GBs": big * ALGO_BYTES / (avg * 1e-3) / 1e9,
+                         "frac_of_peak": big * ALGO_BYTES / (avg * 1e-3) / 1e9 / HBM_PEAK_GBS}
+    del env
+    torch.cuda.empty_cache()
+    # fused rollout: K steps per launch with the per-step trajectory (action, done) written
+    env = VecGame(n_small, device=dev, seed=seed)
+    env.reset()
+    K = 64
+    acts = torch.empty((K, n_small), dtype=torch.int8, device=dev)
+    dn = torch.empty((K, n_small), dtype=torch.uint8, device=dev)
+    env.rollout(K, actions=acts, done=dn)
+    s = torch.cuda.current_stream(dev)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = 10
+    a.record(s)
+    for _ in range(reps):
+        env.rollout(K, actions=acts, done=dn)
+    b.record(s)
+    torch.cuda.synchronize(dev)
+    ms = a.elapsed_time(b) / reps
+    out["rollout_fused"] = {"boards": n_small, "steps_per_launch": K, "kernel_ms": ms,
+                            "env_steps_per_s": n_small * K / (ms * 1e-3),
+                            "note": "k_rollout: boards stay in VGPRs for K steps; writes action+done per "
+                                    "step (2 B) and the board once per launch"}
+    return out
+
+
+def traffic_from_profile(n_boards):
+    p = os.path.join(ROOT, "profiles", "pmc_k_step.json")
+    if not os.path.exists(p):
+        return None
+    d = json.load(open(p))
+    if int(d.get("boards", -1)) != n_boards:
+        return None
+    return d.get("hbm_bytes_per_launch")
+
+
+def main():
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--warmup", type=int, default=200)
+    ap.add_argument("--boards", type=int, default=1 << 20, help="boards per GPU")
+    ap.add_argument("--chunk", type=int, default=100, help="steps per hipGraph replay")
+    ap.add_argument("--seed", type=int, default=0x20485EED)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    if world != args.gpus and not (world == 1 and args.gpus == 1):
+        print("warning: --gpus %d but WORLD_SIZE=%d; using WORLD_SIZE" % (args.gpus, world), file=sys.stderr)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from rein48_amd import VecGame
+
+    n, K, W = args.boards, args.steps, args.warmup
+    env = VecGame(n, device=dev, seed=args.seed, board_offset=rank * n)
+    env.reset()
+    chunk = max(1, min(args.chunk, K))
+    plan = chunks(K, chunk)
+    for c in warm_plan(W, chunk, plan):
+        env.step_n(c, auto_reset=True)
+
+    s = torch.cuda.current_stream(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in plan]
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for (a, b), c in zip(ev, plan):
+        a.record(s)
+        env.step_n(c, auto_reset=True)
+        b.record(s)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    elapsed = float(elapsed.item())
+    gpu_ms = sum(a.elapsed_time(b) for a, b in ev)       # device time of the K steps (events)
+    step_ms_dev = gpu_ms / K                              # per launch, incl. launch boundaries
+
+    # per-launch kernel duration (eager launches of the same kernel, HIP events per launch)
+    ms = kernel_events(env, 50)
+    kern_ms = sorted(ms)[len(ms) // 2]
+
+    value = world * n * K / elapsed
+    bytes_per_launch = n * ALGO_BYTES
+    achieved = bytes_per_launch / (step_ms_dev * 1e-3) / 1e9
+    line = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "env steps/s",
+        "n_gpus": world,
+        "steps": K,
+        "warmup": W,
+        "ms_per_step": elapsed * 1e3 / K,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int8",
+        "data": "synthetic: boards from the reference reset rule (one 2/4 tile), in-kernel uniform random "
+                "policy and spawns from Philox4x32-10, auto-reset on game over",
+        "config": {"workload": "BASELINE configs[1]: 2^20 4x4 int8 boards per GPU, random policy, env-only",
+                   "boards_per_gpu": n, "global_boards": n * world, "parallelism": "env shards x%d, no collective"
+                   % world, "graph_chunk": chunk},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic_from_profile(n),
+                     "kernel": "k_step<RANDOM=1,AUTO_RESET=1,REWARD=0>",
+                     "algorithmic_bytes_per_launch": bytes_per_launch,
+                     "launch_ms_events_in_timed_region": step_ms_dev,
+                     "launch_ms_events_eager_median": kern_ms,
+                     "frac_of_measured_copy_ceiling": achieved / HBM_MEASURED_GBS},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+    if rank == 0 and world == 1 and not args.no_extras:
+        ex = extras(dev, args.seed, n)
+        if not args.no_cpu_baseline:
+            ex["cpu_strong_line"] = strong_cpu_line()
+        line["extras"] = ex
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,144 @@
+/*
+ * rein48.h -- C-ABI of the MI355X-native 2048 environment (librein48.so).
+ *
+ * The reference (nevertiree/Rein48) has no FFI: its environment is the Python class
+ * game/GameClient.py:Game, consumed duck-typed by main.py:39-48, algorithm/a3c/a3c.py:182-204
+ * and algorithm/ddpg/ddpg.py:22-29. Each entry point below names the reference member it
+ * replaces. The Python side binds them with ctypes (rein48_amd/_lib.py; INTEGRATION.md shows
+ * the stub a reference maintainer would add).
+ *
+ * Conventions
+ *   - A board is int8[16], row-major (cell (r,c) at 4*r+c). Cell value e: 0 = empty,
+ *     e > 0 = tile 2^e (the reference stores the raw value 2^e in list[list[int]]).
+ *   - Every array argument is a DEVICE pointer on the env's GPU, owned by the caller;
+ *     nothing is allocated inside step/reset. Boards are bound with r48_env_bind_boards.
+ *   - `stream` is a hipStream_t (NULL = default stream); calls are asynchronous on it.
+ *   - Every function returns R48_OK (0) or a negative R48_E* status; the message for the
+ *     calling thread is in r48_last_error(). The reference raises ValueError for a bad
+ *     action (GameClient.py:254); batched kernels cannot raise, so a bad action byte
+ *     leaves that board unchanged and is counted in the env's device error counter
+ *     (r48_env_error_count).
+ *   - Action codes: 0 UP, 1 DOWN, 2 LEFT, 3 RIGHT (GameClient.py:140,182,206,230).
+ */
+#ifndef REIN48_H
+#define REIN48_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define R48_OK 0
+#define R48_EINVAL (-1)   /* bad argument (null pointer, size, unbound boards, ...) */
+#define R48_EHIP (-2)     /* a HIP runtime call failed */
+#define R48_ENOMEM (-3)
+
+/* step / create flags */
+#define R48_AUTO_RESET 1u      /* a board that is done after the step is reset (reset rule) */
+#define R48_RANDOM_POLICY 2u   /* actions drawn in-kernel (control/rand.py:9-11) and written back */
+#define R48_MERGE_REWARD 4u    /* reward = merged tile values (opt-in; reference reward is 0) */
+
+typedef struct r48_env r48_env;
+
+/* Game.__init__ (GameClient.py:19-29) for a batch: an env of n_boards boards on `device`.
+ * `board_offset` is the global id of board 0 (shard offset); Philox draws are keyed by
+ * (seed, global board id), so a sharded run is identical to an unsharded one. */
+int r48_env_create(r48_env **out, int device, int64_t n_boards, uint64_t seed, int64_t board_offset);
+int r48_env_destroy(r48_env *env);
+
+/* Game.state_matrix (GameClient.py:17,34,45): bind the caller's int8[n_boards][16] device
+ * buffer (16-byte aligned) as the boards the env steps in place. */
+int r48_env_bind_boards(r48_env *env, int8_t *boards);
+int8_t *r48_env_boards(const r48_env *env);
+int64_t r48_env_size(const r48_env *env);
+
+/* Philox counters: the step counter advances once per r48_env_step, the reset counter once
+ * per r48_env_reset. Exposed for checkpoint/resume and parity tests. */
+int r48_env_get_counters(const r48_env *env, uint32_t *step, uint32_t *reset);
+int r48_env_set_counters(r48_env *env, uint32_t step, uint32_t reset);
+
+/* Game.reset (GameClient.py:33-38): zero the board, then ONE spawn (random_fill_grid,
+ * :102-127). mask (uint8[n], nullable = all boards) selects the boards to reset. */
+int r48_env_reset(r48_env *env, const uint8_t *mask, void *stream);
+
+/* Game.reset with injected draws: rank[i] picks the blank (row-major, modulo the blank
+ * count), four[i] != 0 spawns a 4 instead of a 2. */
+int r48_env_reset_with_draws(r48_env *env, const uint8_t *mask, const uint8_t *rank,
+                             const uint8_t *four, void *stream);
+
+/* Game.step (GameClient.py:40-51) for every board: update_matrix (:129-254), spawn only if
+ * the board changed (:48-49), then has_game_over on the spawned board (:51, :65-100).
+ *   actions  int8[n]: read; with R48_RANDOM_POLICY drawn in-kernel (uniform over 0..3,
+ *            control/rand.py:9-11) and written back when non-NULL.
+ *   done     uint8[n] (nullable): has_game_over after the step (before any auto-reset).
+ *   changed  uint8[n] (nullable): the reference's has_changed.
+ *   reward   int32[n] (nullable): 0 (GameClient.py:138), or merged values with R48_MERGE_REWARD.
+ *   score    int32[n] (nullable): tile-value sum after the step (main.py:48), before auto-reset.
+ * flags: R48_AUTO_RESET | R48_RANDOM_POLICY | R48_MERGE_REWARD. Spawn draws come from
+ * Philox4x32-10 keyed by (seed, board id) with the step counter, which then advances. */
+int r48_env_step(r48_env *env, int8_t *actions, uint32_t flags, uint8_t *done, uint8_t *changed,
+                 int32_t *reward, int32_t *score, void *stream);
+
+/* n_steps consecutive r48_env_step calls with the same arguments (outputs hold the last
+ * step's values), replayed from a hipGraph of n_steps step kernels that is captured on the
+ * first call and cached per (n_steps, flags, buffers). The step counter is read from device
+ * memory, so replays advance it exactly like eager calls. n_steps <= 4096. One stream per env. */
+int r48_env_step_n(r48_env *env, int32_t n_steps, int8_t *actions, uint32_t flags, uint8_t *done,
+                   uint8_t *changed, int32_t *reward, int32_t *score, void *stream);
+
+/* Game.step with the spawn draws injected (parity mode, reproduces a reference trajectory
+ * given the reference's randint/uniform draws): rank[i] modulo the post-move blank count,
+ * four[i] != 0 -> 4. No auto-reset, no step-counter advance. */
+int r48_env_step_with_draws(r48_env *env, const int8_t *actions, const uint8_t *rank,
+                            const uint8_t *four, uint32_t flags, uint8_t *done, uint8_t *changed,
+                            int32_t *reward, void *stream);
+
+/* The two halves of Game.step for callers that draw the spawn on the host after seeing
+ * the move (the drop-in single-board Game uses the global Python `random`, exactly like
+ * GameClient.py:121,125):
+ *   r48_env_move : update_matrix only (:129-254) -> changed, n_blank (blank count after move)
+ *   r48_env_spawn: random_fill_grid with injected draws where mask[i] != 0, then
+ *                  has_game_over for every board -> done. */
+int r48_env_move(r48_env *env, const int8_t *actions, uint32_t flags, uint8_t *changed,
+                 uint8_t *n_blank, int32_t *reward, void *stream);
+int r48_env_spawn(r48_env *env, const uint8_t *mask, const uint8_t *rank, const uint8_t *four,
+                  uint8_t *done, void *stream);
+
+/* Random-policy rollout (README.md:19 "random-policy data generation on GPU"; the
+ * main.py:36-42 loop batched): n_steps Philox-mode steps with R48_RANDOM_POLICY |
+ * R48_AUTO_RESET, boards held in registers across steps. Per step t it writes
+ * actions[t*n + i] and done[t*n + i] (both nullable); equal to n_steps calls of
+ * r48_env_step with those flags. */
+int r48_env_rollout(r48_env *env, int32_t n_steps, int8_t *actions, uint8_t *done, void *stream);
+
+/* main.py:48 score = np.sum(state_matrix): tile-value sum per board into int32[n]. */
+int r48_env_score(r48_env *env, int32_t *out, void *stream);
+
+/* Number of bad action bytes seen since the last clear (synchronises the stream). */
+int r48_env_error_count(r48_env *env, int64_t *out, void *stream);
+int r48_env_clear_errors(r48_env *env, void *stream);
+
+/* ---- stateless value-domain helpers: the reference's @staticmethods on arbitrary integer
+ * tiles (GameClientTest.py uses values such as 1 and non-square 4x1 / 1x4 matrices) ----
+ * boards int32[n][16] of raw tile values (row-major 4x4; a smaller matrix is zero-padded on
+ * the side AWAY from the move, which leaves its lines unchanged by construction).        */
+
+/* Game.update_matrix (GameClient.py:129-254): in place; changed uint8[n]; actions int8[n]. */
+int r48_values_move(int32_t *boards, const int8_t *actions, int64_t n, uint8_t *changed,
+                    int64_t *reward, void *stream);
+/* Game.has_table_filled (:96-100) / Game.has_game_over (:65-94) over rows x cols
+ * (1..4 each) top-left sub-matrices; outputs uint8[n], each nullable. */
+int r48_values_check(const int32_t *boards, int64_t n, int32_t rows, int32_t cols,
+                     uint8_t *filled, uint8_t *over, void *stream);
+
+/* Thread-local message of the last failed call on this thread ("" if none). */
+const char *r48_last_error(void);
+/* "rein48 <version> gfx950" */
+const char *r48_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* REIN48_H */

@@ -1,0 +1,97 @@
+"""ctypes binding of librein48.so (C-ABI in include/rein48.h).
+
+The library is the product: gfx950 HIP kernels behind an extern "C" boundary. There is
+no CPU fallback. If the shared object is missing or cannot be loaded, importing any
+compute entry point raises Rein48LibraryError with the build command.
+
+torch is imported first on purpose: the torch ROCm wheel ships its own
+libamdhip64.so.7, and loading it before librein48.so makes the library bind to that same
+HIP runtime (one runtime per process, so torch streams and pointers are valid here).
+"""
+import ctypes as C
+import os
+import threading
+
+import torch  # noqa: F401  (see module docstring: HIP runtime load order)
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "librein48.so")
+
+R48_OK, R48_EINVAL, R48_EHIP, R48_ENOMEM = 0, -1, -2, -3
+AUTO_RESET, RANDOM_POLICY, MERGE_REWARD = 1, 2, 4
+
+# name -> (restype, argtypes); mirrors include/rein48.h one to one
+_P, _I32, _I64, _U32, _U64 = C.c_void_p, C.c_int32, C.c_int64, C.c_uint32, C.c_uint64
+SIGNATURES = {
+    "r48_env_create": (C.c_int, [C.POINTER(_P), C.c_int, _I64, _U64, _I64]),
+    "r48_env_destroy": (C.c_int, [_P]),
+    "r48_env_bind_boards": (C.c_int, [_P, _P]),
+    "r48_env_boards": (_P, [_P]),
+    "r48_env_size": (_I64, [_P]),
+    "r48_env_get_counters": (C.c_int, [_P, C.POINTER(_U32), C.POINTER(_U32)]),
+    "r48_env_set_counters": (C.c_int, [_P, _U32, _U32]),
+    "r48_env_reset": (C.c_int, [_P, _P, _P]),
+    "r48_env_reset_with_draws": (C.c_int, [_P, _P, _P, _P, _P]),
+    "r48_env_step": (C.c_int, [_P, _P, _U32, _P, _P, _P, _P, _P]),
+    "r48_env_step_n": (C.c_int, [_P, _I32, _P, _U32, _P, _P, _P, _P, _P]),
+    "r48_env_step_with_draws": (C.c_int, [_P, _P, _P, _P, _U32, _P, _P, _P, _P]),
+    "r48_env_move": (C.c_int, [_P, _P, _U32, _P, _P, _P, _P]),
+    "r48_env_spawn": (C.c_int, [_P, _P, _P, _P, _P, _P]),
+    "r48_env_rollout": (C.c_int, [_P, _I32, _P, _P, _P]),
+    "r48_env_score": (C.c_int, [_P, _P, _P]),
+    "r48_env_error_count": (C.c_int, [_P, C.POINTER(_I64), _P]),
+    "r48_env_clear_errors": (C.c_int, [_P, _P]),
+    "r48_values_move": (C.c_int, [_P, _P, _I64, _P, _P, _P]),
+    "r48_values_check": (C.c_int, [_P, _I64, _I32, _I32, _P, _P, _P]),
+    "r48_last_error": (C.c_char_p, []),
+    "r48_version": (C.c_char_p, []),
+}
+
+
+class Rein48LibraryError(ImportError):
+    """librein48.so (the HIP extension) is missing or failed to load."""
+
+
+class Rein48Error(RuntimeError):
+    """A C-ABI call returned a negative status."""
+
+    def __init__(self, status, msg):
+        super().__init__("rein48 error %d: %s" % (status, msg))
+        self.status = status
+
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load():
+    """Load librein48.so once; raise Rein48LibraryError loudly if it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise Rein48LibraryError(
+                    "librein48.so not found at %s -- build it with `make` (hipcc --offload-arch=gfx950) "
+                    "or `python -c 'import __graft_entry__ as g; g.build()'`" % LIB_PATH)
+            try:
+                lib = C.CDLL(LIB_PATH)
+            except OSError as e:
+                raise Rein48LibraryError("cannot load %s: %s" % (LIB_PATH, e)) from e
+            for name, (res, args) in SIGNATURES.items():
+                f = getattr(lib, name)
+                f.restype = res
+                f.argtypes = args
+            _lib = lib
+    return _lib
+
+
+def check(status):
+    if status != R48_OK:
+        raise Rein48Error(status, load().r48_last_error().decode())
+    return status
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL)."""
+    return None if t is None else C.c_void_p(t.data_ptr())

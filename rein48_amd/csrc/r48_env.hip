@@ -1,0 +1,740 @@
+// r48_env.hip -- gfx950 kernels + C-ABI (include/rein48.h) of the vectorized 2048 env.
+//
+// Hot path: Game.step (nevertiree/Rein48 game/GameClient.py:40-51) over millions of
+// int8[16] boards in lockstep. One board per lane: a 16-B global_load_dwordx4 per lane
+// (1 KiB contiguous per wave), the step on four VGPRs (r48_board.h), a 16-B store back.
+// Spawn draws come from a per-lane Philox4x32-10 keyed by (seed, global board id) with
+// the step counter -- no RNG state lives in HBM. HBM traffic per board-step (random policy):
+// 16 B board in + 16 B board out + 1 B action out + 1 B done out = 34 B.
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <map>
+#include <cstdint>
+#include <cstdio>
+#include <string>
+
+#include "../../include/rein48.h"
+#include "r48_board.h"
+
+using r48::Board;
+
+namespace {
+
+constexpr int kBlock = 256;
+
+__device__ __forceinline__ Board load_board(const int8_t *boards, int64_t i)
+{
+    const uint4 v = *reinterpret_cast<const uint4 *>(boards + 16 * i);
+    return Board{v.x, v.y, v.z, v.w};
+}
+
+__device__ __forceinline__ void store_board(int8_t *boards, int64_t i, const Board &b)
+{
+    *reinterpret_cast<uint4 *>(boards + 16 * i) = make_uint4(b.w0, b.w1, b.w2, b.w3);
+}
+
+__device__ __forceinline__ void philox_words(uint32_t w[4], uint64_t gid, uint32_t ctr, uint32_t tag,
+                                             uint32_t k0, uint32_t k1)
+{
+    w[0] = (uint32_t)gid;
+    w[1] = (uint32_t)(gid >> 32);
+    w[2] = ctr;
+    w[3] = tag;
+    r48::philox4x32_10(w, k0, k1);
+}
+
+// one wave-level atomic per wave that saw a bad action byte
+__device__ __forceinline__ void count_bad(bool bad, unsigned long long *err)
+{
+    const unsigned long long m = __ballot(bad);
+    if (m && (threadIdx.x & 63) == __builtin_ctzll(m))
+        atomicAdd(err, (unsigned long long)__builtin_popcountll(m));
+}
+
+// ---------------------------------------------------------------- Philox-mode step
+// The Philox step counter is `step_arg` (eager launches) or `*d_ctr + step_arg` (graph
+// replays: node k of a captured chunk carries step_arg = k and the launch function sets
+// *d_ctr to the env's counter with a memset node's value before each replay).
+template <bool RANDOM, bool AUTO_RESET, bool REWARD>
+__global__ __launch_bounds__(kBlock) void k_step(int8_t *__restrict__ boards, int64_t n, int64_t gid0,
+                                                 uint32_t k0, uint32_t k1, const uint32_t *__restrict__ d_ctr,
+                                                 uint32_t step_arg, int8_t *__restrict__ actions,
+                                                 uint8_t *__restrict__ done, uint8_t *__restrict__ changed,
+                                                 int32_t *__restrict__ reward, int32_t *__restrict__ score,
+                                                 unsigned long long *err)
+{
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n)
+        return;
+    const uint32_t step = (d_ctr ? *d_ctr : 0u) + step_arg;
+    Board b = load_board(boards, i);
+    uint32_t w[4];
+    philox_words(w, (uint64_t)(gid0 + i), step, r48::kStepTag, k0, k1);
+    uint32_t a;
+    if (RANDOM) {
+        a = w[0] >> 30;  // uniform over {UP, DOWN, LEFT, RIGHT} (control/rand.py:9-11)
+    } else {
+        a = (uint32_t)(uint8_t)actions[i];
+        count_bad(a > 3u, err);
+    }
+    const r48::StepOut o = r48::step_board<REWARD, false>(b, a, w[1], w[2] < r48::kFourThresh);
+    if (score)
+        score[i] = (int32_t)r48::tile_sum(b);
+    if (AUTO_RESET && o.done)
+        r48::reset_board(b, w[3] >> 28, (w[3] & 0x0FFFFFFFu) < r48::kFourThresh28);
+    store_board(boards, i, b);
+    if (RANDOM && actions)
+        actions[i] = (int8_t)a;
+    if (done)
+        done[i] = (uint8_t)o.done;
+    if (changed)
+        changed[i] = (uint8_t)o.changed;
+    if (reward)
+        reward[i] = REWARD ? (int32_t)o.reward : 0;
+}
+
+// ---------------------------------------------------------------- injected-draw step
+template <bool REWARD>
+__global__ __launch_bounds__(kBlock) void k_step_draws(int8_t *__restrict__ boards, int64_t n,
+                                                       const int8_t *__restrict__ actions,
+                                                       const uint8_t *__restrict__ rank,
+                                                       const uint8_t *__restrict__ four,
+                                                       uint8_t *__restrict__ done, uint8_t *__restrict__ changed,
+                                                       int32_t *__restrict__ reward, unsigned long long *err)
+{
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n)
+        return;
+    Board b = load_board(boards, i);
+    const uint32_t a = (uint32_t)(uint8_t)actions[i];
+    count_bad(a > 3u, err);
+    const r48::StepOut o = r48::step_board<REWARD, true>(b, a, rank[i], four[i] != 0);
+    store_board(boards, i, b);
+    if (done)
+        done[i] = (uint8_t)o.done;
+    if (changed)
+        changed[i] = (uint8_t)o.changed;
+    if (reward)
+        reward[i] = REWARD ? (int32_t)o.reward : 0;
+}
+
+// ---------------------------------------------------------------- move / spawn halves
+template <bool REWARD>
+__global__ __launch_bounds__(kBlock) void k_move(int8_t *__restrict__ boards, int64_t n,
+                                                 const int8_t *__restrict__ actions,
+                                                 uint8_t *__restrict__ changed, uint8_t *__restrict__ n_blank,
+                                                 int32_t *__restrict__ reward, unsigned long long *err)
+{
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n)
+        return;
+    Board b = load_board(boards, i);
+    const uint32_t a = (uint32_t)(uint8_t)actions[i];
+    const bool valid = a < 4u;
+    count_bad(!valid, err);
+    Board L = r48::to_lines(b, a & 3u);
+    const Board L0 = L;
+    uint32_t rw = r48::move_lines<REWARD>(L);
+    const uint32_t diff = (L.w0 ^ L0.w0) | (L.w1 ^ L0.w1) | (L.w2 ^ L0.w2) | (L.w3 ^ L0.w3);
+    const bool c = valid && diff != 0u;
+    const Board m = r48::from_lines(L, a & 3u);
+    b = Board{r48::sel(c, m.w0, b.w0), r48::sel(c, m.w1, b.w1), r48::sel(c, m.w2, b.w2), r48::sel(c, m.w3, b.w3)};
+    store_board(boards, i, b);
+    if (changed)
+        changed[i] = (uint8_t)c;
+    if (n_blank)
+        n_blank[i] = (uint8_t)r48::blanks(b).n;
+    if (reward)
+        reward[i] = (REWARD && c) ? (int32_t)rw : 0;
+}
+
+__global__ __launch_bounds__(kBlock) void k_spawn(int8_t *__restrict__ boards, int64_t n,
+                                                  const uint8_t *__restrict__ mask, const uint8_t *__restrict__ rank,
+                                                  const uint8_t *__restrict__ four, uint8_t *__restrict__ done)
+{
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n)
+        return;
+    Board b = load_board(boards, i);
+    const r48::Blanks bl = r48::blanks(b);
+    const bool on = (mask == nullptr || mask[i] != 0) && bl.n != 0u;
+    const uint32_t cell = r48::select_blank(bl, on ? rank[i] % bl.n : 0u);
+    r48::place(b, cell, (on && four[i]) ? 2u : 1u, on);
+    if (on)
+        store_board(boards, i, b);
+    if (done)
+        done[i] = (uint8_t)r48::game_over(b, bl.n - (on ? 1u : 0u));
+}
+
+// ---------------------------------------------------------------- reset
+__global__ __launch_bounds__(kBlock) void k_reset(int8_t *__restrict__ boards, int64_t n, int64_t gid0,
+                                                  uint32_t k0, uint32_t k1, uint32_t ctr,
+                                                  const uint8_t *__restrict__ mask)
+{
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n || (mask && !mask[i]))
+        return;
+    uint32_t w[4];
+    philox_words(w, (uint64_t)(gid0 + i), ctr, r48::kResetTag, k0, k1);
+    Board b;
+    r48::reset_board(b, w[0] >> 28, w[1] < r48::kFourThresh);
+    store_board(boards, i, b);
+}
+
+__global__ __launch_bounds__(kBlock) void k_reset_draws(int8_t *__restrict__ boards, int64_t n,
+                                                        const uint8_t *__restrict__ mask,
+                                                        const uint8_t *__restrict__ rank,
+                                                        const uint8_t *__restrict__ four)
+{
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n || (mask && !mask[i]))
+        return;
+    Board b;
+    r48::reset_board(b, rank[i] & 15u, four[i] != 0);
+    store_board(boards, i, b);
+}
+
+// ---------------------------------------------------------------- rollout (K steps in registers)
+__global__ __launch_bounds__(kBlock) void k_rollout(int8_t *__restrict__ boards, int64_t n, int64_t gid0,
+                                                    uint32_t k0, uint32_t k1, uint32_t step0, int32_t n_steps,
+                                                    int8_t *__restrict__ actions, uint8_t *__restrict__ done)
+{
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n)
+        return;
+    Board b = load_board(boards, i);
+    const uint64_t gid = (uint64_t)(gid0 + i);
+    for (int32_t t = 0; t < n_steps; t++) {
+        uint32_t w[4];
+        philox_words(w, gid, step0 + (uint32_t)t, r48::kStepTag, k0, k1);
+        const uint32_t a = w[0] >> 30;
+        const r48::StepOut o = r48::step_board<false, false>(b, a, w[1], w[2] < r48::kFourThresh);
+        if (o.done)
+            r48::reset_board(b, w[3] >> 28, (w[3] & 0x0FFFFFFFu) < r48::kFourThresh28);
+        if (actions)
+            actions[(int64_t)t * n + i] = (int8_t)a;
+        if (done)
+            done[(int64_t)t * n + i] = (uint8_t)o.done;
+    }
+    store_board(boards, i, b);
+}
+
+// ---------------------------------------------------------------- score
+__global__ __launch_bounds__(kBlock) void k_score(const int8_t *__restrict__ boards, int64_t n,
+                                                  int32_t *__restrict__ out)
+{
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n)
+        return;
+    out[i] = (int32_t)r48::tile_sum(load_board(boards, i));
+}
+
+// ---------------------------------------------------------------- value-domain helpers
+// Raw integer tiles (the reference's static methods accept any ints, GameClientTest.py
+// uses 1s): the reference's two-pointer line walk (GameClient.py:141-179), equal tiles sum.
+__device__ int64_t value_line(int32_t *c[4])
+{
+    int64_t rw = 0;
+    int i = 0, j = 1;
+    while (j < 4) {
+        while (j < 4 && *c[j] == 0)
+            j++;
+        if (j == 4)
+            break;
+        if (*c[i] == 0) {
+            *c[i] = *c[j];
+            *c[j] = 0;
+        } else if (*c[i] == *c[j]) {
+            *c[i] += *c[j];
+            *c[j] = 0;
+            rw += *c[i];
+            i++;
+        } else {
+            if (i + 1 != j) {
+                *c[i + 1] = *c[j];
+                *c[j] = 0;
+            }
+            i++;
+        }
+        j++;
+    }
+    return rw;
+}
+
+__global__ __launch_bounds__(kBlock) void k_values_move(int32_t *__restrict__ boards,
+                                                        const int8_t *__restrict__ actions, int64_t n,
+                                                        uint8_t *__restrict__ changed, int64_t *__restrict__ reward)
+{
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n)
+        return;
+    int32_t v[16], o[16];
+    for (int k = 0; k < 16; k++)
+        o[k] = v[k] = boards[16 * i + k];
+    const int a = actions[i];
+    int64_t rw = 0;
+    if (a >= 0 && a <= 3) {
+        for (int line = 0; line < 4; line++) {
+            int32_t *p[4];
+            for (int k = 0; k < 4; k++) {
+                const int r = a == 0 ? k : a == 1 ? 3 - k : line;
+                const int cc = a == 0 || a == 1 ? line : a == 2 ? k : 3 - k;
+                p[k] = &v[4 * r + cc];
+            }
+            rw += value_line(p);
+        }
+    }
+    bool c = false;
+    for (int k = 0; k < 16; k++) {
+        c |= v[k] != o[k];
+        boards[16 * i + k] = v[k];
+    }
+    if (changed)
+        changed[i] = (uint8_t)c;
+    if (reward)
+        reward[i] = rw;
+}
+
+__global__ __launch_bounds__(kBlock) void k_values_check(const int32_t *__restrict__ boards, int64_t n,
+                                                         int32_t rows, int32_t cols, uint8_t *__restrict__ filled,
+                                                         uint8_t *__restrict__ over)
+{
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n)
+        return;
+    const int32_t *m = boards + 16 * i;
+    bool full = true, eq = false;
+    for (int r = 0; r < rows; r++)
+        for (int c = 0; c < cols; c++) {
+            const int32_t v = m[4 * r + c];
+            full &= v != 0;
+            if (r + 1 < rows)
+                eq |= v == m[4 * (r + 1) + c];
+            if (c + 1 < cols)
+                eq |= v == m[4 * r + c + 1];
+        }
+    if (filled)
+        filled[i] = (uint8_t)full;
+    if (over)
+        over[i] = (uint8_t)(full && !eq);
+}
+
+}  // namespace
+
+// =============================================================================== C-ABI
+struct GraphKey {
+    int32_t n_steps;
+    uint32_t flags;
+    const void *p[6];
+    bool operator<(const GraphKey &o) const
+    {
+        if (n_steps != o.n_steps)
+            return n_steps < o.n_steps;
+        if (flags != o.flags)
+            return flags < o.flags;
+        for (int k = 0; k < 6; k++)
+            if (p[k] != o.p[k])
+                return p[k] < o.p[k];
+        return false;
+    }
+};
+
+struct r48_env {
+    int device;
+    int64_t n;
+    uint64_t seed;
+    int64_t gid0;
+    uint32_t step_ctr;
+    uint32_t reset_ctr;
+    int8_t *boards;
+    unsigned long long *err;  // device counter of bad action bytes
+    uint32_t *d_ctr;          // step counter read by graph-replayed step kernels
+    hipStream_t cap;          // private capture stream
+    std::map<GraphKey, hipGraphExec_t> graphs;
+};
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string &msg)
+{
+    g_last_error = msg;
+    return code;
+}
+
+struct DeviceGuard {
+    int prev = -1;
+    bool ok = true;
+    explicit DeviceGuard(int dev)
+    {
+        if (hipGetDevice(&prev) != hipSuccess)
+            prev = -1;
+        if (prev != dev)
+            ok = hipSetDevice(dev) == hipSuccess;
+    }
+    ~DeviceGuard()
+    {
+        if (prev >= 0)
+            (void)hipSetDevice(prev);
+    }
+};
+
+int check_env(const r48_env *env, bool need_boards = true)
+{
+    if (!env)
+        return fail(R48_EINVAL, "env is NULL");
+    if (need_boards && !env->boards)
+        return fail(R48_EINVAL, "no boards bound (call r48_env_bind_boards)");
+    return R48_OK;
+}
+
+int launched(const char *what)
+{
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess)
+        return fail(R48_EHIP, std::string(what) + ": " + hipGetErrorString(e));
+    return R48_OK;
+}
+
+inline dim3 grid_for(int64_t n) { return dim3((unsigned)((n + kBlock - 1) / kBlock)); }
+
+}  // namespace
+
+extern "C" {
+
+const char *r48_last_error(void) { return g_last_error.c_str(); }
+
+const char *r48_version(void) { return "rein48 0.1.0 gfx950"; }
+
+int r48_env_create(r48_env **out, int device, int64_t n_boards, uint64_t seed, int64_t board_offset)
+{
+    if (!out)
+        return fail(R48_EINVAL, "out is NULL");
+    *out = nullptr;
+    if (n_boards <= 0 || n_boards > ((int64_t)1 << 40))
+        return fail(R48_EINVAL, "n_boards out of range");
+    if (board_offset < 0)
+        return fail(R48_EINVAL, "board_offset < 0");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev)
+        return fail(R48_EINVAL, "no such HIP device " + std::to_string(device));
+    DeviceGuard g(device);
+    if (!g.ok)
+        return fail(R48_EHIP, "hipSetDevice failed");
+    r48_env *env = new r48_env{device, n_boards, seed, board_offset, 0u, 0u, nullptr, nullptr, nullptr, nullptr, {}};
+    if (hipMalloc(&env->err, sizeof(unsigned long long)) != hipSuccess) {
+        delete env;
+        return fail(R48_ENOMEM, "hipMalloc(error counter) failed");
+    }
+    if (hipMalloc(&env->d_ctr, sizeof(uint32_t)) != hipSuccess) {
+        (void)hipFree(env->err);
+        delete env;
+        return fail(R48_ENOMEM, "hipMalloc(step counter) failed");
+    }
+    if (hipMemset(env->err, 0, sizeof(unsigned long long)) != hipSuccess) {
+        (void)hipFree(env->err);
+        delete env;
+        return fail(R48_EHIP, "hipMemset failed");
+    }
+    *out = env;
+    return R48_OK;
+}
+
+int r48_env_destroy(r48_env *env)
+{
+    if (!env)
+        return R48_OK;
+    DeviceGuard g(env->device);
+    for (auto &kv : env->graphs)
+        (void)hipGraphExecDestroy(kv.second);
+    if (env->cap)
+        (void)hipStreamDestroy(env->cap);
+    (void)hipFree(env->d_ctr);
+    (void)hipFree(env->err);
+    delete env;
+    return R48_OK;
+}
+
+int r48_env_bind_boards(r48_env *env, int8_t *boards)
+{
+    if (int s = check_env(env, false))
+        return s;
+    if (!boards || (reinterpret_cast<uintptr_t>(boards) & 15u))
+        return fail(R48_EINVAL, "boards must be a non-NULL 16-byte aligned device pointer");
+    if (env->boards != boards) {
+        for (auto &kv : env->graphs)
+            (void)hipGraphExecDestroy(kv.second);
+        env->graphs.clear();
+    }
+    env->boards = boards;
+    return R48_OK;
+}
+
+int8_t *r48_env_boards(const r48_env *env) { return env ? env->boards : nullptr; }
+
+int64_t r48_env_size(const r48_env *env) { return env ? env->n : 0; }
+
+int r48_env_get_counters(const r48_env *env, uint32_t *step, uint32_t *reset)
+{
+    if (int s = check_env(env, false))
+        return s;
+    if (step)
+        *step = env->step_ctr;
+    if (reset)
+        *reset = env->reset_ctr;
+    return R48_OK;
+}
+
+int r48_env_set_counters(r48_env *env, uint32_t step, uint32_t reset)
+{
+    if (int s = check_env(env, false))
+        return s;
+    env->step_ctr = step;
+    env->reset_ctr = reset;
+    return R48_OK;
+}
+
+int r48_env_reset(r48_env *env, const uint8_t *mask, void *stream)
+{
+    if (int s = check_env(env))
+        return s;
+    DeviceGuard g(env->device);
+    hipLaunchKernelGGL(k_reset, grid_for(env->n), dim3(kBlock), 0, (hipStream_t)stream, env->boards, env->n,
+                       env->gid0, (uint32_t)env->seed, (uint32_t)(env->seed >> 32), env->reset_ctr, mask);
+    env->reset_ctr++;
+    return launched("k_reset");
+}
+
+int r48_env_reset_with_draws(r48_env *env, const uint8_t *mask, const uint8_t *rank, const uint8_t *four,
+                             void *stream)
+{
+    if (int s = check_env(env))
+        return s;
+    if (!rank || !four)
+        return fail(R48_EINVAL, "rank and four are required");
+    DeviceGuard g(env->device);
+    hipLaunchKernelGGL(k_reset_draws, grid_for(env->n), dim3(kBlock), 0, (hipStream_t)stream, env->boards,
+                       env->n, mask, rank, four);
+    return launched("k_reset_draws");
+}
+
+}  // extern "C"
+
+namespace {
+
+int validate_step(const r48_env *env, const int8_t *actions, uint32_t flags)
+{
+    if (int s = check_env(env))
+        return s;
+    if (flags & ~(R48_AUTO_RESET | R48_RANDOM_POLICY | R48_MERGE_REWARD))
+        return fail(R48_EINVAL, "unknown flag bits");
+    if (!(flags & R48_RANDOM_POLICY) && !actions)
+        return fail(R48_EINVAL, "actions required unless R48_RANDOM_POLICY");
+    return R48_OK;
+}
+
+// one k_step launch; step counter = (d_ctr ? *d_ctr : 0) + step_arg
+void launch_step(r48_env *env, const uint32_t *d_ctr, uint32_t step_arg, int8_t *actions, uint32_t flags,
+                 uint8_t *done, uint8_t *changed, int32_t *reward, int32_t *score, hipStream_t stream)
+{
+    const bool rnd = flags & R48_RANDOM_POLICY, ar = flags & R48_AUTO_RESET, rw = flags & R48_MERGE_REWARD;
+    const uint32_t k0 = (uint32_t)env->seed, k1 = (uint32_t)(env->seed >> 32);
+    auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, grid_for(env->n), dim3(kBlock), 0, stream, env->boards, env->n, env->gid0, k0, k1,
+                           d_ctr, step_arg, actions, done, changed, reward, score, env->err);
+    };
+    // 8 instantiations: policy source x auto-reset x reward mode
+    if (rnd) {
+        if (ar) rw ? go(k_step<true, true, true>) : go(k_step<true, true, false>);
+        else rw ? go(k_step<true, false, true>) : go(k_step<true, false, false>);
+    } else {
+        if (ar) rw ? go(k_step<false, true, true>) : go(k_step<false, true, false>);
+        else rw ? go(k_step<false, false, true>) : go(k_step<false, false, false>);
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int r48_env_step(r48_env *env, int8_t *actions, uint32_t flags, uint8_t *done, uint8_t *changed, int32_t *reward,
+                 int32_t *score, void *stream)
+{
+    if (int s = validate_step(env, actions, flags))
+        return s;
+    DeviceGuard g(env->device);
+    launch_step(env, nullptr, env->step_ctr, actions, flags, done, changed, reward, score, (hipStream_t)stream);
+    env->step_ctr++;
+    return launched("k_step");
+}
+
+int r48_env_step_n(r48_env *env, int32_t n_steps, int8_t *actions, uint32_t flags, uint8_t *done, uint8_t *changed,
+                   int32_t *reward, int32_t *score, void *stream)
+{
+    if (int s = validate_step(env, actions, flags))
+        return s;
+    if (n_steps < 0 || n_steps > 4096)
+        return fail(R48_EINVAL, "n_steps must be in 0..4096");
+    if (n_steps == 0)
+        return R48_OK;
+    DeviceGuard g(env->device);
+    const GraphKey key{n_steps, flags, {env->boards, actions, done, changed, reward, score}};
+    auto it = env->graphs.find(key);
+    if (it == env->graphs.end()) {
+        // capture n_steps dependent step kernels once; replays read the counter from d_ctr
+        if (!env->cap && hipStreamCreateWithFlags(&env->cap, hipStreamNonBlocking) != hipSuccess)
+            return fail(R48_EHIP, "hipStreamCreate failed");
+        if (hipStreamBeginCapture(env->cap, hipStreamCaptureModeThreadLocal) != hipSuccess)
+            return fail(R48_EHIP, "hipStreamBeginCapture failed");
+        for (int32_t k = 0; k < n_steps; k++)
+            launch_step(env, env->d_ctr, (uint32_t)k, actions, flags, done, changed, reward, score, env->cap);
+        hipGraph_t graph = nullptr;
+        const hipError_t ce = hipStreamEndCapture(env->cap, &graph);
+        if (ce != hipSuccess || !graph)
+            return fail(R48_EHIP, std::string("stream capture failed: ") + hipGetErrorString(ce));
+        hipGraphExec_t exec = nullptr;
+        const hipError_t ie = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(graph);
+        if (ie != hipSuccess)
+            return fail(R48_EHIP, std::string("hipGraphInstantiate failed: ") + hipGetErrorString(ie));
+        it = env->graphs.emplace(key, exec).first;
+    }
+    if (hipMemsetD32Async((hipDeviceptr_t)env->d_ctr, (int)env->step_ctr, 1, (hipStream_t)stream) != hipSuccess)
+        return fail(R48_EHIP, "hipMemsetD32Async(step counter) failed");
+    const hipError_t le = hipGraphLaunch(it->second, (hipStream_t)stream);
+    if (le != hipSuccess)
+        return fail(R48_EHIP, std::string("hipGraphLaunch failed: ") + hipGetErrorString(le));
+    env->step_ctr += (uint32_t)n_steps;
+    return R48_OK;
+}
+
+int r48_env_step_with_draws(r48_env *env, const int8_t *actions, const uint8_t *rank, const uint8_t *four,
+                            uint32_t flags, uint8_t *done, uint8_t *changed, int32_t *reward, void *stream)
+{
+    if (int s = check_env(env))
+        return s;
+    if (!actions || !rank || !four)
+        return fail(R48_EINVAL, "actions, rank and four are required");
+    if (flags & ~R48_MERGE_REWARD)
+        return fail(R48_EINVAL, "only R48_MERGE_REWARD is valid with injected draws");
+    DeviceGuard g(env->device);
+    if (flags & R48_MERGE_REWARD)
+        hipLaunchKernelGGL(k_step_draws<true>, grid_for(env->n), dim3(kBlock), 0, (hipStream_t)stream,
+                           env->boards, env->n, actions, rank, four, done, changed, reward, env->err);
+    else
+        hipLaunchKernelGGL(k_step_draws<false>, grid_for(env->n), dim3(kBlock), 0, (hipStream_t)stream,
+                           env->boards, env->n, actions, rank, four, done, changed, reward, env->err);
+    return launched("k_step_draws");
+}
+
+int r48_env_move(r48_env *env, const int8_t *actions, uint32_t flags, uint8_t *changed, uint8_t *n_blank,
+                 int32_t *reward, void *stream)
+{
+    if (int s = check_env(env))
+        return s;
+    if (!actions)
+        return fail(R48_EINVAL, "actions required");
+    if (flags & ~R48_MERGE_REWARD)
+        return fail(R48_EINVAL, "only R48_MERGE_REWARD is valid for r48_env_move");
+    DeviceGuard g(env->device);
+    if (flags & R48_MERGE_REWARD)
+        hipLaunchKernelGGL(k_move<true>, grid_for(env->n), dim3(kBlock), 0, (hipStream_t)stream, env->boards,
+                           env->n, actions, changed, n_blank, reward, env->err);
+    else
+        hipLaunchKernelGGL(k_move<false>, grid_for(env->n), dim3(kBlock), 0, (hipStream_t)stream, env->boards,
+                           env->n, actions, changed, n_blank, reward, env->err);
+    return launched("k_move");
+}
+
+int r48_env_spawn(r48_env *env, const uint8_t *mask, const uint8_t *rank, const uint8_t *four, uint8_t *done,
+                  void *stream)
+{
+    if (int s = check_env(env))
+        return s;
+    if (!rank || !four)
+        return fail(R48_EINVAL, "rank and four are required");
+    DeviceGuard g(env->device);
+    hipLaunchKernelGGL(k_spawn, grid_for(env->n), dim3(kBlock), 0, (hipStream_t)stream, env->boards, env->n,
+                       mask, rank, four, done);
+    return launched("k_spawn");
+}
+
+int r48_env_rollout(r48_env *env, int32_t n_steps, int8_t *actions, uint8_t *done, void *stream)
+{
+    if (int s = check_env(env))
+        return s;
+    if (n_steps < 0)
+        return fail(R48_EINVAL, "n_steps < 0");
+    if (n_steps == 0)
+        return R48_OK;
+    DeviceGuard g(env->device);
+    hipLaunchKernelGGL(k_rollout, grid_for(env->n), dim3(kBlock), 0, (hipStream_t)stream, env->boards, env->n,
+                       env->gid0, (uint32_t)env->seed, (uint32_t)(env->seed >> 32), env->step_ctr, n_steps,
+                       actions, done);
+    env->step_ctr += (uint32_t)n_steps;
+    return launched("k_rollout");
+}
+
+int r48_env_score(r48_env *env, int32_t *out, void *stream)
+{
+    if (int s = check_env(env))
+        return s;
+    if (!out)
+        return fail(R48_EINVAL, "out is NULL");
+    DeviceGuard g(env->device);
+    hipLaunchKernelGGL(k_score, grid_for(env->n), dim3(kBlock), 0, (hipStream_t)stream, env->boards, env->n, out);
+    return launched("k_score");
+}
+
+int r48_env_error_count(r48_env *env, int64_t *out, void *stream)
+{
+    if (int s = check_env(env, false))
+        return s;
+    if (!out)
+        return fail(R48_EINVAL, "out is NULL");
+    DeviceGuard g(env->device);
+    unsigned long long v = 0;
+    if (hipMemcpyAsync(&v, env->err, sizeof v, hipMemcpyDeviceToHost, (hipStream_t)stream) != hipSuccess ||
+        hipStreamSynchronize((hipStream_t)stream) != hipSuccess)
+        return fail(R48_EHIP, "reading the error counter failed");
+    *out = (int64_t)v;
+    return R48_OK;
+}
+
+int r48_env_clear_errors(r48_env *env, void *stream)
+{
+    if (int s = check_env(env, false))
+        return s;
+    DeviceGuard g(env->device);
+    if (hipMemsetAsync(env->err, 0, sizeof(unsigned long long), (hipStream_t)stream) != hipSuccess)
+        return fail(R48_EHIP, "hipMemsetAsync failed");
+    return R48_OK;
+}
+
+int r48_values_move(int32_t *boards, const int8_t *actions, int64_t n, uint8_t *changed, int64_t *reward,
+                    void *stream)
+{
+    if (!boards || !actions || n < 0)
+        return fail(R48_EINVAL, "boards/actions NULL or n < 0");
+    if (n == 0)
+        return R48_OK;
+    hipLaunchKernelGGL(k_values_move, grid_for(n), dim3(kBlock), 0, (hipStream_t)stream, boards, actions, n,
+                       changed, reward);
+    return launched("k_values_move");
+}
+
+int r48_values_check(const int32_t *boards, int64_t n, int32_t rows, int32_t cols, uint8_t *filled, uint8_t *over,
+                     void *stream)
+{
+    if (!boards || n < 0 || rows < 1 || rows > 4 || cols < 1 || cols > 4)
+        return fail(R48_EINVAL, "boards NULL, n < 0 or rows/cols outside 1..4");
+    if (n == 0)
+        return R48_OK;
+    hipLaunchKernelGGL(k_values_check, grid_for(n), dim3(kBlock), 0, (hipStream_t)stream, boards, n, rows, cols,
+                       filled, over);
+    return launched("k_values_check");
+}
+
+}  // extern "C"

@@ -1,0 +1,198 @@
+"""Drop-in replacement for nevertiree/Rein48 game/GameClient.py (class Game).
+
+Same names, argument meaning, return shapes and errors as the reference:
+  Game(table_matrix_size=4)            GameClient.py:19-29
+  .reset(display=False) -> state       :33-38   (new list; ONE spawned tile)
+  .step(action) -> (state, 0, done)    :40-51   (state mutated in place and aliased)
+  .state_matrix / size attributes      :17, :21-27
+  static create_matrix / has_game_over / has_table_filled / random_fill_grid /
+  update_matrix / print_terminal       :55-269
+Actions: "UP"/"Up"/"U"/"up"/"u"/0, ... /3 matched by equality like the reference
+(:140, :182, :206, :230), so True means DOWN and 2.0 means LEFT; anything else raises
+ValueError (:254).
+
+Compute runs on the GPU through librein48.so: a Game owns a one-board VecGame and each step
+is the move kernel (update_matrix) + the spawn/game-over kernel. The spawn DRAWS are taken
+from Python's global `random` exactly as the reference takes them (randint over the
+row-major blank list, then uniform(0,1) > 0.1 -> 2 else 4, GameClient.py:121-125), so
+`random.seed(s)` gives the reference's trajectory bit for bit. The batched VecGame draws
+on device instead (Philox).
+
+The GPU env kernel is 4x4: Game(n) with n > 4 raises
+NotImplementedError. The static helpers accept any integer tiles on matrices up to 4x4
+(the reference's own tests use 4x1 / 1x4 matrices and the value 1).
+"""
+import copy
+import random
+
+import torch
+
+from ..env import VecGame
+from .. import _lib
+from .._lib import check, ptr
+
+_UP = ["UP", "Up", "U", "up", "u", 0]
+_DOWN = ["DOWN", "Down", "D", "down", "d", 1]
+_LEFT = ["LEFT", "Left", "L", "left", "l", 2]
+_RIGHT = ["RIGHT", "Right", "R", "right", "r", 3]
+_BAD_ACTION = "Input action signal is wrong:\n You must input valid inputs, such as  [U] [D] [L] [R]... "
+
+
+def action_code(action):
+    """The reference's direction test (GameClient.py:140,182,206,230): `action in [...]`."""
+    for code, names in enumerate((_UP, _DOWN, _LEFT, _RIGHT)):
+        if action in names:
+            return code
+    raise ValueError(_BAD_ACTION)
+
+
+def _exponent(v):
+    """raw tile value -> exponent, or None if not 0 / 2^e with 1 <= e <= 30"""
+    if v == 0:
+        return 0
+    if isinstance(v, bool) or v != int(v):
+        return None
+    v = int(v)
+    if v < 2 or v & (v - 1) or v > (1 << 30):
+        return None
+    return v.bit_length() - 1
+
+
+def _device():
+    if not torch.cuda.is_available():
+        raise RuntimeError("rein48 Game needs a ROCm GPU (torch.cuda.is_available() is False)")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def _pad(matrix, code):
+    """rows x cols (<= 4x4) -> 4x4 int32 board, anchored on the side the tiles move toward
+    (zeros on the far side cannot change any line)."""
+    rows, cols = len(matrix), len(matrix[0])
+    if rows > 4 or cols > 4 or any(len(r) != cols for r in matrix):
+        raise NotImplementedError("rein48 kernels handle rectangular matrices up to 4x4, got %dx%d"
+                                  % (rows, max(len(r) for r in matrix)))
+    r0 = 4 - rows if code == 1 else 0
+    c0 = 4 - cols if code == 3 else 0
+    board = [0] * 16
+    for i in range(rows):
+        for j in range(cols):
+            board[4 * (r0 + i) + c0 + j] = int(matrix[i][j])
+    return board, r0, c0
+
+
+class Game:
+
+    state_matrix, state_space_size = None, 0
+
+    def __init__(self, table_matrix_size=4):
+        self.reward_space_size = 1
+        self.action_space_size = 4
+        self.state_space_size = 4 if table_matrix_size < 4 else table_matrix_size
+        if self.state_space_size != 4:
+            raise NotImplementedError("the MI355X env kernel is 4x4 (got table_matrix_size=%r)"
+                                      % table_matrix_size)
+        self._vec = VecGame(1, device=_device())
+        self._one = torch.ones(1, dtype=torch.uint8, device=self._vec.device)
+        self.reset()
+
+    # ---------------------------------------------------------------- public (GameClient.py:33-51)
+    def reset(self, display=False):
+        self.state_matrix = self.create_matrix(self.state_space_size)
+        self.state_matrix = self.random_fill_grid(self.state_matrix)
+        if display:
+            Game.print_terminal(self.state_matrix)
+        return self.state_matrix
+
+    def step(self, action):
+        code = action_code(action)
+        exps = [_exponent(v) for row in self.state_matrix for v in row]
+        if any(e is None for e in exps):
+            # tiles outside 2^e: the value-domain kernels, composed like GameClient.py:45-51
+            self.state_matrix, reward, changed = self.update_matrix(self.state_matrix, code)
+            if changed:
+                self.state_matrix = Game.random_fill_grid(self.state_matrix)
+            return self.state_matrix, reward, Game.has_game_over(self.state_matrix)
+        vec = self._vec
+        dev = vec.device
+        vec.boards.copy_(torch.tensor(exps, dtype=torch.int8).view(1, 16))
+        act = torch.tensor([code], dtype=torch.int8, device=dev)
+        changed_t, n_blank_t = vec.move(act)
+        changed, n_blank = (int(x) for x in torch.stack([changed_t, n_blank_t]).view(2).cpu())
+        if changed:
+            rank = random.randint(0, n_blank - 1)                # GameClient.py:121
+            four = 0 if random.uniform(0, 1) > 0.1 else 1         # GameClient.py:125
+            done_t = vec.spawn(torch.tensor([rank], dtype=torch.uint8, device=dev),
+                               torch.tensor([four], dtype=torch.uint8, device=dev), mask=self._one)
+        else:
+            done_t = vec.spawn(self._one, self._one, mask=self._one * 0)
+        host = torch.cat([vec.boards.view(16).to(torch.int16), done_t.to(torch.int16)]).cpu().tolist()
+        for k in range(16):  # write back into the SAME lists (aliasing, GameClient.py:45)
+            e = host[k]
+            self.state_matrix[k // 4][k % 4] = (1 << e) if e else 0
+        return self.state_matrix, 0, bool(host[16])
+
+    # ---------------------------------------------------------------- static helpers (:55-269)
+    @staticmethod
+    def create_matrix(table_size=4):
+        return [[0 for _ in range(table_size)] for _ in range(table_size)]
+
+    @staticmethod
+    def _check(game_matrix):
+        rows, cols = len(game_matrix), len(game_matrix[0])
+        board, _, _ = _pad(game_matrix, 0)
+        dev = _device()
+        b = torch.tensor(board, dtype=torch.int32, device=dev)
+        out = torch.empty(2, dtype=torch.uint8, device=dev)
+        check(_lib.load().r48_values_check(ptr(b), 1, rows, cols, ptr(out[0:1]), ptr(out[1:2]),
+                                           torch.cuda.current_stream(dev).cuda_stream))
+        filled, over = out.cpu().tolist()
+        return bool(filled), bool(over)
+
+    @staticmethod
+    def has_game_over(game_matrix):
+        return Game._check(game_matrix)[1]
+
+    @staticmethod
+    def has_table_filled(game_matrix):
+        return Game._check(game_matrix)[0]
+
+    @staticmethod
+    def random_fill_grid(game_matrix):
+        """Host RNG glue (GameClient.py:102-127): enumerate the blanks row-major, draw with the
+        global `random` like the reference, write the tile in place."""
+        blank = [(i, j) for i in range(len(game_matrix)) for j in range(len(game_matrix))
+                 if game_matrix[i][j] == 0]
+        if not blank:
+            return game_matrix
+        i, j = blank[random.randint(0, len(blank) - 1)]
+        game_matrix[i][j] = 2 if (random.uniform(0, 1) > 0.1) else 4
+        return game_matrix
+
+    @staticmethod
+    def update_matrix(matrix, action):
+        """GameClient.py:129-254 on the GPU (value-domain kernel): mutates `matrix` in place,
+        returns (matrix, 0, changed)."""
+        code = action_code(action)
+        origin = copy.deepcopy(matrix)
+        board, r0, c0 = _pad(matrix, code)
+        dev = _device()
+        b = torch.tensor(board, dtype=torch.int32, device=dev)
+        a = torch.tensor([code], dtype=torch.int8, device=dev)
+        check(_lib.load().r48_values_move(ptr(b), ptr(a), 1, None, None,
+                                          torch.cuda.current_stream(dev).cuda_stream))
+        out = b.cpu().tolist()
+        for i in range(len(matrix)):
+            for j in range(len(matrix[0])):
+                matrix[i][j] = out[4 * (r0 + i) + c0 + j]
+        return matrix, 0, (origin != matrix)
+
+    @staticmethod
+    def print_terminal(matrix):
+        width, height = len(matrix[0]), len(matrix)
+        rule = "-" * (1 + 7 * width)
+        lines = [rule]
+        for i in range(height):
+            cells = [(str(matrix[i][j]).center(6) if matrix[i][j] != 0 else " " * 6) for j in range(width)]
+            lines.append("|" + "|".join(cells) + "|")
+            lines.append(rule)
+        print("\n".join(lines))

@@ -1,0 +1,62 @@
+"""C-ABI checks that need no GPU: the library loads, exports exactly what include/rein48.h
+declares, the ctypes signatures cover every export, and argument errors come back as
+R48_EINVAL with a message (no HIP call is made on these paths)."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import pytest
+
+from rein48_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "rein48.h")
+
+
+def declared():
+    text = open(HEADER).read()
+    return set(re.findall(r"^\s*(?:const\s+)?[\w]+\s*\*?\s*(r48_\w+)\s*\(", text, re.M))
+
+
+def test_header_parses():
+    names = declared()
+    assert "r48_env_step" in names and "r48_last_error" in names and len(names) >= 20
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _lib.load()
+    out = subprocess.check_output(["nm", "-D", "--defined-only", _lib.LIB_PATH], text=True)
+    exported = set(re.findall(r" T (r48_\w+)$", out, re.M))
+    assert declared() == exported
+    for name in declared():
+        assert hasattr(lib, name)
+    assert set(_lib.SIGNATURES) == declared()
+
+
+def test_library_is_gfx950_code_object():
+    data = open(_lib.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in data  # the embedded offload bundle's target triple
+
+
+def test_argument_errors_without_gpu():
+    lib = _lib.load()
+    env = C.c_void_p()
+    assert lib.r48_env_create(C.byref(env), 0, 0, 1, 0) == _lib.R48_EINVAL
+    assert b"n_boards" in lib.r48_last_error()
+    assert lib.r48_env_create(None, 0, 16, 1, 0) == _lib.R48_EINVAL
+    assert lib.r48_env_bind_boards(None, None) == _lib.R48_EINVAL
+    assert lib.r48_env_step(None, None, 0, None, None, None, None, None) == _lib.R48_EINVAL
+    assert lib.r48_values_check(None, 1, 4, 4, None, None, None) == _lib.R48_EINVAL
+    assert lib.r48_values_move(None, None, 1, None, None, None) == _lib.R48_EINVAL
+    assert lib.r48_env_destroy(None) == _lib.R48_OK
+    with pytest.raises(_lib.Rein48Error):
+        _lib.check(lib.r48_env_create(C.byref(env), 0, -5, 1, 0))
+    assert lib.r48_version().startswith(b"rein48")
+
+
+def test_missing_library_fails_loudly(monkeypatch, tmp_path):
+    monkeypatch.setattr(_lib, "_lib", None)
+    monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "nope.so"))
+    with pytest.raises(_lib.Rein48LibraryError):
+        _lib.load()

@@ -1,0 +1,416 @@
+"""GPU parity of the hot path: librein48.so's gfx950 kernels vs the oracle and the reference.
+
+Bit-exact everywhere (integer/byte work). Covers: the reference's KATs, the exhaustive
+18^4-line table, 128 seeded reference episodes replayed with the reference's own draws,
+Philox mode vs the oracle (random policy, given actions incl. bad bytes, merge reward,
+auto-reset, score), reset, move/spawn halves, rollout == repeated steps, sharding
+invariance, full-size (2^20 boards) properties, and the random-policy fingerprint.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import native as O
+from conftest import to_exp_scaled
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+def vec(n, seed=0, offset=0):
+    from rein48_amd import VecGame
+    return VecGame(n, device=DEV, seed=seed, board_offset=offset)
+
+
+def rand_boards(rng, n, emax=9, p_empty=0.5):
+    b = rng.integers(1, emax + 1, size=(n, 16)).astype(np.int8)
+    b[rng.random((n, 16)) < p_empty] = 0
+    return b
+
+
+def put(v, boards):
+    v.boards.copy_(torch.from_numpy(np.ascontiguousarray(boards, np.int8)).to(DEV))
+
+
+def host(t):
+    return t.detach().cpu().numpy()
+
+
+# ---------------------------------------------------------------- reference KATs / table
+def test_line_kats_on_gpu(golden):
+    """GameClientTest.py:49-331 through the exponent kernel (values x2) and through the
+    value-domain kernel with the KATs' raw values (1, 2, 4, ...)."""
+    from rein48_amd.game import Game
+    kats = golden["kats"]["line_moves"]
+    code = {"U": 0, "D": 1, "LEFT": 2, "R": 3}
+    boards, acts, want = [], [], []
+    for k in kats:
+        a = code[k["action"]]
+        cells = to_exp_scaled(k["input"])
+        b = np.zeros(16, np.int8)
+        exp = np.zeros(16, np.int8)
+        w = to_exp_scaled(k["expected"])
+        for i in range(4):
+            if a < 2:
+                b[4 * i + 1], exp[4 * i + 1] = cells[i], w[i]
+            else:
+                b[4 + i], exp[4 + i] = cells[i], w[i]
+        boards.append(b)
+        acts.append(a)
+        want.append(exp)
+    v = vec(len(kats))
+    put(v, np.stack(boards))
+    changed, _ = v.move(torch.tensor(acts, dtype=torch.int8, device=DEV))
+    assert np.array_equal(host(v.boards), np.stack(want))
+    assert host(changed).astype(bool).tolist() == [k["reference_changed"] for k in kats]
+    # the drop-in static method on the raw KAT matrices (value 1 and all)
+    for k in kats:
+        m = [list(r) for r in k["input"]]
+        out, reward, changed = Game.update_matrix(m, k["action"])
+        assert out == k["expected"] and out is m and reward == 0 and changed == k["reference_changed"]
+
+
+def test_filled_game_over_kats_on_gpu(golden):
+    from rein48_amd.game import Game
+    for k in golden["kats"]["filled"]:
+        assert Game.has_table_filled(k["input"]) == k["expected"]
+    for k in golden["kats"]["game_over"]:
+        assert Game.has_game_over(k["input"]) == k["expected"]
+
+
+def test_exhaustive_line_table_on_gpu():
+    """Every line of 4 cells with exponents 0..17, every direction: GPU == reference table."""
+    out, chg = O.line_table()
+    n = O.LINE_TABLE_N
+    idx = np.arange(n)
+    cells = np.stack([(idx // 18 ** (3 - k)) % 18 for k in range(4)], axis=1).astype(np.int8)
+    for d in range(4):
+        nb = n // 4  # 18^4 is divisible by 4: four lines per board
+        b = np.zeros((nb, 4, 4), np.int8)
+        want = np.zeros((nb, 4, 4), np.int8)
+        c4 = cells.reshape(nb, 4, 4)       # [board, slot, cell]
+        o4 = out[d].reshape(nb, 4, 4)
+        if d < 2:   # columns
+            b[:] = np.transpose(c4, (0, 2, 1))
+            want[:] = np.transpose(o4, (0, 2, 1))
+        else:       # rows
+            b[:] = c4
+            want[:] = o4
+        v = vec(nb)
+        put(v, b.reshape(nb, 16))
+        changed, _ = v.move(torch.full((nb,), d, dtype=torch.int8, device=DEV))
+        assert np.array_equal(host(v.boards), want.reshape(nb, 16)), d
+        any_chg = chg[d].reshape(nb, 4).max(axis=1)
+        assert np.array_equal(host(changed), any_chg), d
+
+
+# ---------------------------------------------------------------- reference trajectories
+def test_reference_trajectories_replayed_with_injected_draws(golden):
+    """All 128 reference episodes in lockstep: start board from reset_with_draws with the
+    reference's first two draws, then each step with the reference's action, randint rank
+    and uniform-derived 4/2 flag: every board and done flag bit-exact."""
+    z = golden["traj"]
+    keys = list(zip(z["start_seed"].tolist(), z["start_episode"].tolist()))
+    ne = len(keys)
+    lens = [int(((z["step_seed"] == s) & (z["step_episode"] == e)).sum()) for s, e in keys]
+    T = max(lens)
+    act = np.zeros((T, ne), np.int8)
+    rank = np.zeros((T, ne), np.uint8)
+    four = np.zeros((T, ne), np.uint8)
+    after = np.zeros((T, ne, 16), np.int8)
+    done = np.zeros((T, ne), np.uint8)
+    for j, (s, e) in enumerate(keys):
+        m = (z["step_seed"] == s) & (z["step_episode"] == e)
+        L = lens[j]
+        act[:L, j] = z["step_action"][m]
+        rank[:L, j] = np.maximum(z["step_rank"][m], 0)
+        four[:L, j] = np.maximum(z["step_four"][m], 0)
+        after[:L, j] = z["step_after"][m]
+        done[:L, j] = z["step_done"][m]
+    v = vec(ne)
+    v.reset_with_draws(torch.tensor(z["start_rank"], dtype=torch.uint8, device=DEV),
+                       torch.tensor(z["start_four"], dtype=torch.uint8, device=DEV))
+    assert np.array_equal(host(v.boards), z["start_board"])
+    for t in range(T):
+        v.step_with_draws(torch.from_numpy(act[t]).to(DEV), torch.from_numpy(rank[t]).to(DEV),
+                          torch.from_numpy(four[t]).to(DEV))
+        live = np.array([t < L for L in lens])
+        assert np.array_equal(host(v.boards)[live], after[t][live]), t
+        assert np.array_equal(host(v.done)[live], done[t][live]), t
+
+
+def test_drop_in_game_reproduces_reference_episodes(golden):
+    """rein48_amd.game.Game + rein48_amd.control.Rand under random.seed(s): the reference's
+    exact episodes (main.py:36-42 loop), with state aliasing preserved."""
+    import random
+    from rein48_amd.control import Rand
+    from rein48_amd.game import Game
+    z = golden["traj"]
+    for seed in range(6):
+        random.seed(seed)
+        for ep in range(2):
+            g = Game()
+            sm = (z["start_seed"] == seed) & (z["start_episode"] == ep)
+            m = (z["step_seed"] == seed) & (z["step_episode"] == ep)
+            assert to_exp_list(g.state_matrix) == z["start_board"][sm][0].tolist()
+            after, dn = z["step_after"][m], z["step_done"][m]
+            state0 = g.state_matrix
+            for t in range(after.shape[0]):
+                state, reward, done = g.step(Rand.random_action(g.state_matrix))
+                assert state is state0 and reward == 0
+                assert to_exp_list(state) == after[t].tolist(), (seed, ep, t)
+                assert done == bool(dn[t])
+
+
+def to_exp_list(m):
+    return [0 if v == 0 else int(v).bit_length() - 1 for r in m for v in r]
+
+
+def test_drop_in_game_surface():
+    from rein48_amd.game import Game
+    g = Game()
+    assert (g.action_space_size, g.reward_space_size, g.state_space_size) == (4, 1, 4)
+    assert sum(v != 0 for r in g.state_matrix for v in r) == 1
+    for bad in ("X", 4, -1, None, "upward"):
+        with pytest.raises(ValueError):
+            g.step(bad)
+    for alias in ("Up", "d", "LEFT", "r", 0, 1, 2, 3, True, 2.0):
+        g.step(alias)
+    with pytest.raises(NotImplementedError):
+        Game(5)
+    assert Game(3).state_space_size == 4
+
+
+# ---------------------------------------------------------------- Philox mode vs oracle
+@pytest.mark.parametrize("flags", [O.RANDOM_POLICY, O.RANDOM_POLICY | O.AUTO_RESET,
+                                   O.RANDOM_POLICY | O.AUTO_RESET | O.MERGE_REWARD])
+def test_philox_random_policy_matches_oracle(flags):
+    rng = np.random.default_rng(flags)
+    n, seed, off = 100_003, 0x2048_5EED, 12345
+    b0 = rand_boards(rng, n)
+    v = vec(n, seed=seed, offset=off)
+    put(v, b0)
+    ob = b0
+    score = torch.zeros(n, dtype=torch.int32, device=DEV)
+    for step in range(4):
+        v.step(None, auto_reset=bool(flags & O.AUTO_RESET), merge_reward=bool(flags & O.MERGE_REWARD),
+               want_changed=True, score=score)
+        r = O.step_philox(ob, seed, step, flags, board_offset=off, want_score=True)
+        ob = r["boards"]
+        assert np.array_equal(host(v.boards), ob), step
+        assert np.array_equal(host(v.actions), r["actions"])
+        assert np.array_equal(host(v.done), r["done"])
+        assert np.array_equal(host(v.changed), r["changed"])
+        assert np.array_equal(host(score), r["score"])
+        if flags & O.MERGE_REWARD:
+            assert np.array_equal(host(v.reward), r["reward"])
+    assert v.counters == (4, 0)
+
+
+def test_given_actions_with_bad_bytes_match_oracle():
+    rng = np.random.default_rng(5)
+    n = 65_536
+    b0 = rand_boards(rng, n, emax=17, p_empty=0.3)
+    acts = rng.integers(0, 4, n).astype(np.int8)
+    bad = rng.random(n) < 0.01
+    acts[bad] = rng.choice(np.array([-128, -1, 4, 5, 100, 127], np.int8), bad.sum())
+    v = vec(n, seed=99)
+    put(v, b0)
+    v.error_count(clear=True)
+    v.step(torch.from_numpy(acts).to(DEV), merge_reward=True, want_changed=True)
+    r = O.step_philox(b0, 99, 0, O.MERGE_REWARD, actions=acts)
+    assert np.array_equal(host(v.boards), r["boards"])
+    assert np.array_equal(host(v.done), r["done"])
+    assert np.array_equal(host(v.changed), r["changed"])
+    assert np.array_equal(host(v.reward), r["reward"])
+    assert np.array_equal(host(v.boards)[bad], b0[bad])  # a bad action leaves the board as it was
+    assert v.error_count() == int(bad.sum()) == r["bad"]
+
+
+def test_injected_draws_match_oracle():
+    rng = np.random.default_rng(11)
+    n = 50_000
+    b0 = rand_boards(rng, n)
+    acts = rng.integers(0, 4, n).astype(np.int8)
+    rank = rng.integers(0, 256, n).astype(np.uint8)
+    four = rng.integers(0, 2, n).astype(np.uint8)
+    v = vec(n)
+    put(v, b0)
+    v.step_with_draws(torch.from_numpy(acts).to(DEV), torch.from_numpy(rank).to(DEV),
+                      torch.from_numpy(four).to(DEV), merge_reward=True)
+    r = O.step_draws(b0, acts, rank, four, flags=O.MERGE_REWARD)
+    assert np.array_equal(host(v.boards), r["boards"])
+    assert np.array_equal(host(v.done), r["done"])
+    assert np.array_equal(host(v.changed), r["changed"])
+    assert np.array_equal(host(v.reward), r["reward"])
+
+
+def test_move_then_spawn_equals_step_with_draws():
+    rng = np.random.default_rng(12)
+    n = 40_000
+    b0 = rand_boards(rng, n)
+    acts = torch.from_numpy(rng.integers(0, 4, n).astype(np.int8)).to(DEV)
+    rank = torch.from_numpy(rng.integers(0, 256, n).astype(np.uint8)).to(DEV)
+    four = torch.from_numpy(rng.integers(0, 2, n).astype(np.uint8)).to(DEV)
+    a, b = vec(n), vec(n)
+    put(a, b0)
+    put(b, b0)
+    changed, n_blank = a.move(acts)
+    moved = host(a.boards)
+    assert np.array_equal(host(n_blank), (moved == 0).sum(1))
+    a.spawn(rank, four, mask=changed.clone())
+    b.step_with_draws(acts, rank, four)
+    assert np.array_equal(host(a.boards), host(b.boards))
+    assert np.array_equal(host(a.done), host(b.done))
+
+
+def test_reset_matches_oracle():
+    n, seed = 70_000, 31337
+    v = vec(n, seed=seed, offset=7)
+    mask = (np.arange(n) % 3 != 0).astype(np.uint8)
+    put(v, np.full((n, 16), 5, np.int8))
+    v.reset()
+    v.reset(mask=torch.from_numpy(mask).to(DEV))
+    ob = O.reset_philox(np.full((n, 16), 5, np.int8), seed, 0, board_offset=7)
+    ob = O.reset_philox(ob, seed, 1, mask=mask, board_offset=7)
+    assert np.array_equal(host(v.boards), ob)
+    nz = (ob != 0).sum(1)
+    assert (nz == 1).all()
+    assert v.counters == (0, 2)
+
+
+def test_rollout_equals_repeated_steps():
+    n, K, seed = 30_000, 37, 4242
+    rng = np.random.default_rng(3)
+    b0 = rand_boards(rng, n, emax=6, p_empty=0.4)
+    a, b = vec(n, seed=seed, offset=99), vec(n, seed=seed, offset=99)
+    put(a, b0)
+    put(b, b0)
+    acts = torch.empty((K, n), dtype=torch.int8, device=DEV)
+    dn = torch.empty((K, n), dtype=torch.uint8, device=DEV)
+    a.rollout(K, actions=acts, done=dn)
+    for t in range(K):
+        b.step(None, auto_reset=True)
+        assert torch.equal(acts[t], b.actions) and torch.equal(dn[t], b.done), t
+    assert torch.equal(a.boards, b.boards)
+    assert a.counters == b.counters == (K, 0)
+
+
+def test_sharded_envs_equal_one_env():
+    """Philox keyed by global board id: two half-size shards == one env (multi-GPU invariance)."""
+    n, seed = 20_000, 8
+    rng = np.random.default_rng(8)
+    b0 = rand_boards(rng, n)
+    whole = vec(n, seed=seed)
+    lo, hi = vec(n // 2, seed=seed, offset=0), vec(n // 2, seed=seed, offset=n // 2)
+    put(whole, b0)
+    put(lo, b0[: n // 2])
+    put(hi, b0[n // 2:])
+    for _ in range(5):
+        for e in (whole, lo, hi):
+            e.step(None, auto_reset=True)
+    assert torch.equal(whole.boards, torch.cat([lo.boards, hi.boards]))
+
+
+def test_score_matches_oracle():
+    rng = np.random.default_rng(4)
+    b0 = rand_boards(rng, 10_000, emax=17)
+    v = vec(10_000)
+    put(v, b0)
+    assert np.array_equal(host(v.score()), O.score(b0))
+
+
+# ---------------------------------------------------------------- full-size properties
+def test_full_size_properties():
+    """BASELINE config 2 size (2^20 boards): a move conserves the tile-value sum, a spawn adds
+    exactly one 2 or 4 iff the board changed, a sampled subset is bit-exact vs the oracle,
+    and the run is deterministic."""
+    n = 1 << 20
+    rng = np.random.default_rng(2048)
+    b0 = rand_boards(rng, n, emax=7)
+    acts = torch.from_numpy(rng.integers(0, 4, n).astype(np.int8)).to(DEV)
+    v = vec(n, seed=1)
+    put(v, b0)
+    s0 = v.score().to(torch.int64)
+    changed, _ = v.move(acts)
+    s1 = v.score().to(torch.int64)
+    assert torch.equal(s0, s1)
+    put(v, b0)
+    v.step(acts, want_changed=True)
+    s2 = v.score().to(torch.int64)
+    diff = s2 - s0
+    ch = v.changed.to(torch.bool)
+    assert torch.equal(ch, changed.to(torch.bool))
+    assert bool(((diff == 2) | (diff == 4))[ch].all()) and bool((diff == 0)[~ch].all())
+    nz_delta = (v.boards != 0).sum(1) - torch.from_numpy((b0 != 0).sum(1)).to(DEV)
+    assert bool((nz_delta <= 1).all())
+    # sampled boards bit-exact vs the oracle (its draws are keyed by the global board id)
+    got, ah = host(v.boards), host(acts)
+    for i in rng.choice(n, 512, replace=False):
+        rr = O.step_philox(b0[i:i + 1], 1, 0, 0, actions=ah[i:i + 1], board_offset=int(i))
+        assert np.array_equal(got[i], rr["boards"][0])
+    w = vec(n, seed=1)
+    put(w, b0)
+    w.step(acts)
+    assert torch.equal(w.boards, v.boards)
+
+
+def test_fingerprint_distribution_on_gpu(golden):
+    """Random policy on 65,536 boards: episode length statistics over complete episodes that
+    start in the first 1,000 steps (reference: mean 142.36, sd 47.27, 20,000 episodes)."""
+    fp = golden["fingerprint"]
+    n, T, window = 65_536, 3_000, 1_000
+    v = vec(n, seed=2024)
+    v.reset()
+    dn = torch.empty((T, n), dtype=torch.uint8, device=DEV)
+    v.rollout(T, done=dn)
+    d = host(dn).astype(bool)
+    lengths = []
+    t_idx, b_idx = np.nonzero(d)
+    order = np.lexsort((t_idx, b_idx))
+    t_idx, b_idx = t_idx[order], b_idx[order]
+    prev_b = -1
+    for t, b in zip(t_idx, b_idx):
+        if b != prev_b:
+            s = 0
+            prev_b = b
+        if s < window:
+            lengths.append(t + 1 - s)
+        s = t + 1
+    lengths = np.asarray(lengths, np.float64)
+    ref = fp["episode_length"]
+    se = np.sqrt(ref["sd"] ** 2 / lengths.size + ref["sd"] ** 2 / fp["n_episodes"])
+    assert lengths.size > 300_000
+    assert abs(lengths.mean() - ref["mean"]) < 4 * se, (lengths.mean(), ref["mean"])
+    assert abs(lengths.std(ddof=1) - ref["sd"]) < 0.03 * ref["sd"]
+    assert lengths.min() >= 10 and lengths.max() < 1500
+
+
+def test_input_validation():
+    v = vec(8)
+    with pytest.raises(TypeError):
+        v.step(torch.zeros(8, dtype=torch.int32, device=DEV))
+    with pytest.raises(ValueError):
+        v.step(torch.zeros(7, dtype=torch.int8, device=DEV))
+    with pytest.raises(ValueError):
+        v.step(torch.zeros(8, dtype=torch.int8))  # host tensor
+
+
+def test_step_n_graph_equals_repeated_steps():
+    """r48_env_step_n (cached hipGraph replay, device-side counter) == eager steps, across
+    several replays of the same graph and interleaved eager calls."""
+    n, seed = 50_000, 77
+    rng = np.random.default_rng(9)
+    b0 = rand_boards(rng, n, emax=6)
+    a, b = vec(n, seed=seed, offset=5), vec(n, seed=seed, offset=5)
+    put(a, b0)
+    put(b, b0)
+    for chunk in (16, 16, 3, 16):
+        a.step_n(chunk, auto_reset=True)
+        a.step(None, auto_reset=True)
+        for _ in range(chunk + 1):
+            b.step(None, auto_reset=True)
+        assert torch.equal(a.boards, b.boards), chunk
+        assert torch.equal(a.done, b.done) and torch.equal(a.actions, b.actions)
+    assert a.counters == b.counters
