@@ -49,17 +49,6 @@ def chunks(total, size):
     return out
 
 
-def warm_plan(warmup, chunk, timed_plan):
-    """Warm-up steps that also instantiate every graph size the timed plan uses."""
-    plan, left = [], warmup
-    for c in sorted(set(timed_plan), reverse=True):
-        if left >= c:
-            plan.append(c)
-            left -= c
-    plan += [1] * left
-    return plan
-
-
 def cpu_baseline(seconds):
     """oracle/game_port.py on one core for ~`seconds` (bounded sample)."""
     from oracle import game_port
@@ -164,7 +153,7 @@ def main():
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=200)
     ap.add_argument("--boards", type=int, default=1 << 20, help="boards per GPU")
-    ap.add_argument("--chunk", type=int, default=100, help="steps per hipGraph replay")
+    ap.add_argument("--chunk", type=int, default=4096, help="max steps per r48_env_step_n call (<= 4096)")
     ap.add_argument("--seed", type=int, default=0x20485EED)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -186,11 +175,13 @@ def main():
     n, K, W = args.boards, args.steps, args.warmup
     env = VecGame(n, device=dev, seed=args.seed, board_offset=rank * n)
     env.reset()
-    chunk = max(1, min(args.chunk, K))
+    chunk = max(1, min(args.chunk, K, 4096))
     plan = chunks(K, chunk)
-    for c in warm_plan(W, chunk, plan):
+    # warm-up: W steps through the same replay path, then build every graph the timed plan uses
+    for c in chunks(W, min(max(W, 1), 4096)) if W else []:
         env.step_n(c, auto_reset=True)
-
+    for c in sorted(set(plan)):
+        env.prepare_step_n(c, auto_reset=True)
     s = torch.cuda.current_stream(dev)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in plan]
     torch.cuda.synchronize(dev)
@@ -210,7 +201,7 @@ def main():
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     elapsed = float(elapsed.item())
     gpu_ms = sum(a.elapsed_time(b) for a, b in ev)       # device time of the K steps (events)
-    step_ms_dev = gpu_ms / K                              # per launch, incl. launch boundaries
+    step_ms_dev = gpu_ms / K                              # per step (all boards), device time
 
     # per-launch kernel duration (eager launches of the same kernel, HIP events per launch)
     ms = kernel_events(env, 50)
@@ -238,10 +229,12 @@ def main():
                    % world, "graph_chunk": chunk},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic_from_profile(n),
-                     "kernel": "k_step<RANDOM=1,AUTO_RESET=1,REWARD=0>",
-                     "algorithmic_bytes_per_launch": bytes_per_launch,
-                     "launch_ms_events_in_timed_region": step_ms_dev,
-                     "launch_ms_events_eager_median": kern_ms,
+                     "kernel": "k_step<RANDOM=1,AUTO_RESET=1,REWARD=0,B=%d>" % (4 if n // (2 if n >= (1 << 18) else 1)
+                                                                                 >= (1 << 22) else 1),
+                     "algorithmic_bytes_per_step": bytes_per_launch,
+                     "step_ms_device_events_timed_region": step_ms_dev,
+                     "chains": 2 if n >= (1 << 18) else 1,
+                     "single_launch_ms_eager_events_median": kern_ms,
                      "frac_of_measured_copy_ceiling": achieved / HBM_MEASURED_GBS},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

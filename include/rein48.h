@@ -81,11 +81,18 @@ int r48_env_step(r48_env *env, int8_t *actions, uint32_t flags, uint8_t *done, u
                  int32_t *reward, int32_t *score, void *stream);
 
 /* n_steps consecutive r48_env_step calls with the same arguments (outputs hold the last
- * step's values), replayed from a hipGraph of n_steps step kernels that is captured on the
- * first call and cached per (n_steps, flags, buffers). The step counter is read from device
- * memory, so replays advance it exactly like eager calls. n_steps <= 4096. One stream per env. */
+ * step's values), replayed from hipGraphs of n_steps step kernels captured on the first call
+ * and cached per (n_steps, flags, buffers). The step counter is read from device memory, so
+ * replays advance it exactly like eager calls. Envs of >= 2^18 boards run as two shard chains
+ * (the second on an env-owned stream, forked from and joined back into `stream`), so one
+ * shard's memory latency overlaps the other's compute. n_steps <= 4096; prefer large chunks
+ * (the fork/join costs tens of microseconds per call). One caller stream per env. */
 int r48_env_step_n(r48_env *env, int32_t n_steps, int8_t *actions, uint32_t flags, uint8_t *done,
                    uint8_t *changed, int32_t *reward, int32_t *score, void *stream);
+/* Capture + instantiate the graphs r48_env_step_n would replay for these arguments, without
+ * running anything (keeps graph construction out of a timed or latency-critical region). */
+int r48_env_prepare_step_n(r48_env *env, int32_t n_steps, int8_t *actions, uint32_t flags, uint8_t *done,
+                           uint8_t *changed, int32_t *reward, int32_t *score);
 
 /* Game.step with the spawn draws injected (parity mode, reproduces a reference trajectory
  * given the reference's randint/uniform draws): rank[i] modulo the post-move blank count,

@@ -26,8 +26,10 @@
 
 #if defined(__HIPCC__)
 #define R48_HD __host__ __device__ __forceinline__
+#define R48_UNROLL _Pragma("unroll")
 #else
 #define R48_HD static inline
+#define R48_UNROLL
 #endif
 
 namespace r48 {
@@ -73,8 +75,12 @@ R48_HD uint32_t mulhi(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a *
 // 0x80 in each byte that is nonzero / zero.
 R48_HD uint32_t nz80(uint32_t x) { return (x + 0x7F7F7F7Fu) & 0x80808080u; }
 R48_HD uint32_t z80(uint32_t x) { return ~(x + 0x7F7F7F7Fu) & 0x80808080u; }
-// 0x80 byte flags -> 0xFF byte masks
-R48_HD uint32_t ff(uint32_t m80) { return (m80 << 1) - (m80 >> 7); }
+// Bit 7 of each byte -> 0xFF/0x00 byte mask (other bits ignored): v_perm_b32's selectors
+// 8..11 replicate the sign bit of pool bytes 1, 3, 5, 7; with pool {f<<8 : f} those are
+// f's bytes 1, 3, 0, 2.  Two instructions (shift + perm).
+R48_HD uint32_t ff(uint32_t f) { return perm(f << 8, f, 0x090B080Au); }
+// 0xFF in each nonzero byte of x (bytes <= 0x80): add + shift + perm
+R48_HD uint32_t nzff(uint32_t x) { return ff(x + 0x7F7F7F7Fu); }
 // bytewise select: m ? x : y   (v_bfi_b32)
 R48_HD uint32_t bsel(uint32_t m, uint32_t x, uint32_t y) { return (x & m) | (y & ~m); }
 
@@ -124,47 +130,47 @@ R48_HD uint32_t move_lines(Board &L)
     uint32_t l0 = L.w0, l1 = L.w1, l2 = L.w2, l3 = L.w3;
     // (1) compaction, from the far side in: where line cell i is empty, the cells behind it
     //     shift one place toward L[0] (GameClient.py:147-160: j skips empties, i takes j).
-    uint32_t k = ff(nz80(l2));
+    uint32_t k = nzff(l2);
     l2 = bsel(k, l2, l3);
     l3 &= k;
-    k = ff(nz80(l1));
+    k = nzff(l1);
     l1 = bsel(k, l1, l2);
     l2 = bsel(k, l2, l3);
     l3 &= k;
-    k = ff(nz80(l0));
+    k = nzff(l0);
     l0 = bsel(k, l0, l1);
     l1 = bsel(k, l1, l2);
     l2 = bsel(k, l2, l3);
     l3 &= k;
     // (2) merge adjacent equal tiles once, nearest the wall first (GameClient.py:162-167):
     //     (0,1) always wins, (1,2) only if (0,1) did not, (2,3) unless (1,2) merged.
-    const uint32_t e01 = z80(l0 ^ l1) & nz80(l1);
-    const uint32_t e12 = z80(l1 ^ l2) & nz80(l2);
-    const uint32_t e23 = z80(l2 ^ l3) & nz80(l3);
-    const uint32_t m01 = e01;
-    const uint32_t m12 = e12 & ~e01;
-    const uint32_t m23 = e23 & (e01 | ~e12);
+    //     Flags live in bit 7 of each byte: equal = bit 7 of (a^b)+0x7F clear, nonzero =
+    //     bit 7 of b+0x7F set.
+    const uint32_t e01 = ~((l0 ^ l1) + 0x7F7F7F7Fu) & (l1 + 0x7F7F7F7Fu);
+    const uint32_t e12 = ~((l1 ^ l2) + 0x7F7F7F7Fu) & (l2 + 0x7F7F7F7Fu);
+    const uint32_t e23 = ~((l2 ^ l3) + 0x7F7F7F7Fu) & (l3 + 0x7F7F7F7Fu);
+    const uint32_t f01 = ff(e01);
+    const uint32_t f12 = ff(e12 & ~e01);
+    const uint32_t f23 = ff(e23 & (e01 | ~e12));
     uint32_t reward = 0;
     // apply the far pair first so the nearer pairs' shifts carry its result along
-    l2 += m23 >> 7;
+    l2 += f23 & 0x01010101u;
     if (REWARD) {
         for (int b = 0; b < 4; b++)
-            reward += ((m23 >> (8 * b + 7)) & 1u) << ((l2 >> (8 * b)) & 31u);
+            reward += ((f23 >> (8 * b)) & 1u) << ((l2 >> (8 * b)) & 31u);
     }
-    l3 &= ~ff(m23);
-    const uint32_t f12 = ff(m12);
-    l1 += m12 >> 7;
+    l3 &= ~f23;
+    l1 += f12 & 0x01010101u;
     if (REWARD) {
         for (int b = 0; b < 4; b++)
-            reward += ((m12 >> (8 * b + 7)) & 1u) << ((l1 >> (8 * b)) & 31u);
+            reward += ((f12 >> (8 * b)) & 1u) << ((l1 >> (8 * b)) & 31u);
     }
     l2 = bsel(f12, l3, l2);
     l3 &= ~f12;
-    const uint32_t f01 = ff(m01);
-    l0 += m01 >> 7;
+    l0 += f01 & 0x01010101u;
     if (REWARD) {
         for (int b = 0; b < 4; b++)
-            reward += ((m01 >> (8 * b + 7)) & 1u) << ((l0 >> (8 * b)) & 31u);
+            reward += ((f01 >> (8 * b)) & 1u) << ((l0 >> (8 * b)) & 31u);
     }
     l1 = bsel(f01, l2, l1);
     l2 = bsel(f01, l3, l2);
@@ -247,6 +253,7 @@ R48_HD uint32_t tile_sum(const Board &r) { return row_sum(r.w0) + row_sum(r.w1) 
 // ---- Philox4x32-10 (Salmon, Moraes, Dror, Shaw, SC'11) -----------------------------
 R48_HD void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1)
 {
+    R48_UNROLL
     for (int i = 0; i < 10; i++) {
         const uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
         const uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];

@@ -127,10 +127,7 @@ class VecGame:
                                      ptr(self.reward) if merge_reward else None, ptr(score), self._s()))
         return self.boards, (self.reward if merge_reward else self._zero_reward), self.done
 
-    def step_n(self, n_steps, actions=None, auto_reset=False, merge_reward=False, want_changed=False,
-               score=None):
-        """n_steps consecutive step() calls with the same arguments, replayed from a cached
-        hipGraph (one host call for the whole chunk). Outputs hold the last step's values."""
+    def _step_n_args(self, actions, auto_reset, merge_reward, want_changed, score):
         flags = (AUTO_RESET if auto_reset else 0) | (MERGE_REWARD if merge_reward else 0)
         if actions is None:
             flags |= RANDOM_POLICY
@@ -138,10 +135,23 @@ class VecGame:
         else:
             act = self._t(actions, torch.int8, "actions")
         score = self._t(score, torch.int32, "score")
-        check(self._lib.r48_env_step_n(self._env, int(n_steps), ptr(act), flags, ptr(self.done),
-                                       ptr(self.changed) if want_changed else None,
-                                       ptr(self.reward) if merge_reward else None, ptr(score), self._s()))
+        return (ptr(act), flags, ptr(self.done), ptr(self.changed) if want_changed else None,
+                ptr(self.reward) if merge_reward else None, ptr(score))
+
+    def step_n(self, n_steps, actions=None, auto_reset=False, merge_reward=False, want_changed=False,
+               score=None):
+        """n_steps consecutive step() calls with the same arguments, replayed from cached
+        hipGraphs (one host call for the whole chunk; 2 shard chains for >= 2^18 boards).
+        Outputs hold the last step's values. Prefer large chunks (<= 4096)."""
+        a = self._step_n_args(actions, auto_reset, merge_reward, want_changed, score)
+        check(self._lib.r48_env_step_n(self._env, int(n_steps), a[0], a[1], *a[2:], self._s()))
         return self.boards, (self.reward if merge_reward else self._zero_reward), self.done
+
+    def prepare_step_n(self, n_steps, actions=None, auto_reset=False, merge_reward=False, want_changed=False,
+                       score=None):
+        """Build (capture + instantiate) the graphs step_n would replay, without running them."""
+        a = self._step_n_args(actions, auto_reset, merge_reward, want_changed, score)
+        check(self._lib.r48_env_prepare_step_n(self._env, int(n_steps), a[0], a[1], *a[2:]))
 
     def step_with_draws(self, actions, rank, four, merge_reward=False):
         """Parity mode: Game.step with the reference's spawn draws injected."""

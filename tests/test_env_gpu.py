@@ -414,3 +414,26 @@ def test_step_n_graph_equals_repeated_steps():
         assert torch.equal(a.boards, b.boards), chunk
         assert torch.equal(a.done, b.done) and torch.equal(a.actions, b.actions)
     assert a.counters == b.counters
+
+
+@pytest.mark.parametrize("n", [300_001, 9_000_003])
+def test_step_n_chains_and_wide_tiles_match_oracle(n):
+    """Large envs: r48_env_step_n splits the boards into 2 shard chains (>= 2^18 boards) and
+    uses 4 boards per lane past 4M boards per launch; odd sizes exercise the partial tile.
+    Result == eager steps == the oracle."""
+    seed = 4040
+    rng = np.random.default_rng(n)
+    b0 = rand_boards(rng, n, emax=6)
+    a, b = vec(n, seed=seed, offset=3), vec(n, seed=seed, offset=3)
+    put(a, b0)
+    put(b, b0)
+    a.step_n(2, auto_reset=True)
+    a.step_n(2, auto_reset=True)
+    for _ in range(4):
+        b.step(None, auto_reset=True)
+    assert torch.equal(a.boards, b.boards)
+    assert torch.equal(a.done, b.done) and torch.equal(a.actions, b.actions)
+    want = b0
+    for t in range(4):
+        want = O.step_philox(want, seed, t, O.RANDOM_POLICY | O.AUTO_RESET, board_offset=3)["boards"]
+    assert np.array_equal(host(a.boards), want)
