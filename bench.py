@@ -42,6 +42,20 @@ HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROA
 HBM_MEASURED_GBS = 6290.0  # float4 copy measured on MI355X (same guide)
 
 
+def shard(rank, boards_per_gpu):
+    """Rank r owns global boards [r*N, (r+1)*N): weak scaling, Philox keyed by global id, so
+    the union of the shards is bit-identical to one N*world env (tests/test_distributed.py)."""
+    return rank * boards_per_gpu, boards_per_gpu
+
+
+def max_over_ranks(x, device, world):
+    """Timing aggregation: the slowest rank's elapsed time defines the job's time."""
+    t = torch.tensor([float(x)], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def chunks(total, size):
     out = [size] * (total // size)
     if total % size:
@@ -144,14 +158,15 @@ def traffic_from_profile(n_boards):
     d = json.load(open(p))
     if int(d.get("boards", -1)) != n_boards:
         return None
-    return d.get("hbm_bytes_per_launch")
+    return d.get("hbm_bytes_per_step")
 
 
 def main():
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=1000)
-    ap.add_argument("--warmup", type=int, default=200)
+    ap.add_argument("--steps", type=int, default=3000)
+    ap.add_argument("--warmup", type=int, default=3000,
+                    help="untimed steps (the GPU clock needs ~20 ms of load to settle)")
     ap.add_argument("--boards", type=int, default=1 << 20, help="boards per GPU")
     ap.add_argument("--chunk", type=int, default=4096, help="max steps per r48_env_step_n call (<= 4096)")
     ap.add_argument("--seed", type=int, default=0x20485EED)
@@ -173,12 +188,14 @@ def main():
     from rein48_amd import VecGame
 
     n, K, W = args.boards, args.steps, args.warmup
-    env = VecGame(n, device=dev, seed=args.seed, board_offset=rank * n)
+    offset, n = shard(rank, n)
+    env = VecGame(n, device=dev, seed=args.seed, board_offset=offset)
     env.reset()
     chunk = max(1, min(args.chunk, K, 4096))
     plan = chunks(K, chunk)
-    # warm-up: W steps through the same replay path, then build every graph the timed plan uses
-    for c in chunks(W, min(max(W, 1), 4096)) if W else []:
+    # warm-up: W steps through the same replay path (in chunks of the timed chunk size, so the
+    # timed region replays graphs that have already run), then build any graph still missing
+    for c in chunks(W, chunk) if W else []:
         env.step_n(c, auto_reset=True)
     for c in sorted(set(plan)):
         env.prepare_step_n(c, auto_reset=True)
@@ -196,10 +213,7 @@ def main():
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
-    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-    elapsed = float(elapsed.item())
+    elapsed = max_over_ranks(t1 - t0, dev, world)
     gpu_ms = sum(a.elapsed_time(b) for a, b in ev)       # device time of the K steps (events)
     step_ms_dev = gpu_ms / K                              # per step (all boards), device time
 
