@@ -139,6 +139,37 @@ int r48_values_move(int32_t *boards, const int8_t *actions, int64_t n, uint8_t *
 int r48_values_check(const int32_t *boards, int64_t n, int32_t rows, int32_t cols,
                      uint8_t *filled, uint8_t *over, void *stream);
 
+/* ---- A3C pieces around the env step (algorithm/a3c/a3c.py) ---- */
+#define R48_FEAT_VALUES 0     /* raw tile values 2^e, as a3c.py:37-39,139 feed the network */
+#define R48_FEAT_EXPONENTS 1  /* the exponent e (a normalised input for the corrected mode) */
+#define R48_F32 0
+#define R48_BF16 1
+
+/* Network input from boards: out[n][16] float32 or bf16 (16-byte aligned). */
+int r48_board_features(const int8_t *boards, int64_t n, int32_t mode, int32_t out_dtype, void *out,
+                       void *stream);
+
+/* LocalAgent.choose_action (a3c.py:89-93) batched: softmax over logits float[n][4], then the
+ * first action whose cumulative probability exceeds u (np.random.choice semantics), u from
+ * Philox4x32-10(key = seed, counter = {gid0+i, ctr, 0xA3C}) with 24 bits. Optional outputs
+ * logp[i] = log p[a_i] and entropy[i] = -sum_k p_k log(p_k + 1e-5) (a3c.py:114). */
+int r48_sample_actions(const float *logits, int64_t n, uint64_t seed, int64_t gid0, uint32_t ctr,
+                       int8_t *actions, float *logp, float *entropy, void *stream);
+
+/* Worker._get_target_value_list (a3c.py:246-256) for n segments at once, time-major:
+ * rewards/out float[T][n], lengths int32[n] (segment length, 1..T), bootstrap float[n].
+ * drop_last != 0: out[len-1] = bootstrap, out[t] = r_t + gamma*out[t+1] (the reference, whose
+ * last reward never enters); drop_last == 0: the textbook n-step return. out[t] = 0 for
+ * t >= len. */
+int r48_discounted_returns(const float *rewards, const int32_t *lengths, const float *bootstrap,
+                           int32_t T, int64_t n, float gamma, int32_t drop_last, float *out,
+                           void *stream);
+
+/* tf.train.RMSPropOptimizer(lr) (a3c.py:264-265; TF1 semantics: ms slot starts at ONES, eps
+ * inside the sqrt, momentum 0 by default) over one flat float32 parameter buffer of n values. */
+int r48_rmsprop_tf1(float *var, const float *grad, float *ms, float *mom, int64_t n, float lr,
+                    float decay, float momentum, float eps, void *stream);
+
 /* Thread-local message of the last failed call on this thread ("" if none). */
 const char *r48_last_error(void);
 /* "rein48 <version> gfx950" */

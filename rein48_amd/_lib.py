@@ -18,6 +18,8 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libr
 
 R48_OK, R48_EINVAL, R48_EHIP, R48_ENOMEM = 0, -1, -2, -3
 AUTO_RESET, RANDOM_POLICY, MERGE_REWARD = 1, 2, 4
+FEAT_VALUES, FEAT_EXPONENTS = 0, 1
+F32, BF16 = 0, 1
 
 # name -> (restype, argtypes); mirrors include/rein48.h one to one
 _P, _I32, _I64, _U32, _U64 = C.c_void_p, C.c_int32, C.c_int64, C.c_uint32, C.c_uint64
@@ -43,6 +45,10 @@ SIGNATURES = {
     "r48_env_clear_errors": (C.c_int, [_P, _P]),
     "r48_values_move": (C.c_int, [_P, _P, _I64, _P, _P, _P]),
     "r48_values_check": (C.c_int, [_P, _I64, _I32, _I32, _P, _P, _P]),
+    "r48_board_features": (C.c_int, [_P, _I64, _I32, _I32, _P, _P]),
+    "r48_sample_actions": (C.c_int, [_P, _I64, _U64, _I64, _U32, _P, _P, _P, _P]),
+    "r48_discounted_returns": (C.c_int, [_P, _P, _P, _I32, _I64, C.c_float, _I32, _P, _P]),
+    "r48_rmsprop_tf1": (C.c_int, [_P, _P, _P, _P, _I64, C.c_float, C.c_float, C.c_float, C.c_float, _P]),
     "r48_last_error": (C.c_char_p, []),
     "r48_version": (C.c_char_p, []),
 }

@@ -1,0 +1,66 @@
+"""Torch-facing wrappers of the A3C HIP kernels in librein48.so (include/rein48.h)."""
+import ctypes as C
+
+import torch
+
+from .. import _lib
+from .._lib import check, ptr
+
+
+def _stream(t):
+    return C.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def _dev(t, name, dtype=None):
+    if not t.is_cuda:
+        raise ValueError("%s must be a GPU tensor (the A3C kernels have no CPU path)" % name)
+    if dtype is not None and t.dtype != dtype:
+        raise TypeError("%s must be %s, got %s" % (name, dtype, t.dtype))
+    if not t.is_contiguous():
+        raise ValueError("%s must be contiguous" % name)
+    return t
+
+
+def board_features(boards, exponents=False, dtype=torch.float32, out=None):
+    """int8 boards [..., 16] -> network input [..., 16]: raw tile values (a3c.py:139) or exponents."""
+    _dev(boards, "boards", torch.int8)
+    n = boards.numel() // 16
+    if out is None:
+        out = torch.empty(boards.shape, dtype=dtype, device=boards.device)
+    _dev(out, "out", dtype)
+    code = {torch.float32: _lib.F32, torch.bfloat16: _lib.BF16}[dtype]
+    check(_lib.load().r48_board_features(ptr(boards), n, _lib.FEAT_EXPONENTS if exponents else _lib.FEAT_VALUES,
+                                         code, ptr(out), _stream(boards)))
+    return out
+
+
+def sample_actions(logits, seed, ctr, gid0=0, want_logp=False, want_entropy=False):
+    """choose_action (a3c.py:89-93) for every row of logits [n, 4] (post-ReLU, pre-softmax)."""
+    _dev(logits, "logits", torch.float32)
+    n = logits.numel() // 4
+    act = torch.empty(n, dtype=torch.int8, device=logits.device)
+    logp = torch.empty(n, dtype=torch.float32, device=logits.device) if want_logp else None
+    ent = torch.empty(n, dtype=torch.float32, device=logits.device) if want_entropy else None
+    check(_lib.load().r48_sample_actions(ptr(logits), n, int(seed) & (2 ** 64 - 1), int(gid0), int(ctr) & 0xFFFFFFFF,
+                                         ptr(act), ptr(logp), ptr(ent), _stream(logits)))
+    return act, logp, ent
+
+
+def discounted_returns(rewards, lengths, bootstrap, gamma=0.9, drop_last=True):
+    """_get_target_value_list (a3c.py:246-256) for n segments: rewards [T, n] -> targets [T, n]."""
+    _dev(rewards, "rewards", torch.float32)
+    _dev(lengths, "lengths", torch.int32)
+    _dev(bootstrap, "bootstrap", torch.float32)
+    T, n = rewards.shape
+    out = torch.empty_like(rewards)
+    check(_lib.load().r48_discounted_returns(ptr(rewards), ptr(lengths), ptr(bootstrap), T, n, float(gamma),
+                                             1 if drop_last else 0, ptr(out), _stream(rewards)))
+    return out
+
+
+def rmsprop_tf1_(var, grad, ms, mom, lr, decay=0.9, momentum=0.0, eps=1e-10):
+    """In-place TF1 RMSProp step on flat float32 buffers."""
+    for t, name in ((var, "var"), (grad, "grad"), (ms, "ms"), (mom, "mom")):
+        _dev(t, name, torch.float32)
+    check(_lib.load().r48_rmsprop_tf1(ptr(var), ptr(grad), ptr(ms), ptr(mom), var.numel(), float(lr), float(decay),
+                                      float(momentum), float(eps), _stream(var)))

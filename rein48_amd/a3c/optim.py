@@ -1,0 +1,70 @@
+"""TF1 RMSProp over a flat parameter buffer + synchronous gradient all-reduce.
+
+The reference applies each worker's gradients to the shared global net with
+tf.train.RMSPropOptimizer(1e-3) (a3c.py:79-80, 264-265) -- Hogwild, asynchronous. Here every
+replica (one per GPU) holds the net, gradients are averaged with ONE all-reduce of one flat fp32
+buffer per update (RCCL over xGMI on GPUs; the net is ~2.5 k (MLP) / ~38 k (CNN) parameters, so
+the message is latency-bound, never link-bound), and every replica applies the same update.
+
+FlatParams re-points every parameter and its .grad at views of two contiguous buffers, so the
+all-reduce and the optimizer are one call each. On GPU tensors the TF1 update is the fused HIP
+kernel r48_rmsprop_tf1 (one launch for all parameters); on CPU tensors (the CPU test-suite)
+the same arithmetic runs as torch ops.
+"""
+import torch
+import torch.distributed as dist
+
+
+class FlatParams:
+    def __init__(self, module):
+        params = [p for p in module.parameters() if p.requires_grad]
+        self.params = params
+        dev, dt = params[0].device, params[0].dtype
+        total = sum(p.numel() for p in params)
+        self.data = torch.zeros(total, dtype=dt, device=dev)
+        self.grad = torch.zeros(total, dtype=dt, device=dev)
+        off = 0
+        for p in params:
+            k = p.numel()
+            self.data[off:off + k].copy_(p.data.view(-1))
+            p.data = self.data[off:off + k].view_as(p)
+            p.grad = self.grad[off:off + k].view_as(p)
+            off += k
+
+    def zero_grad(self):
+        self.grad.zero_()
+
+    def allreduce_grad(self, group=None):
+        """Average the gradient over the process group (one collective)."""
+        if dist.is_available() and dist.is_initialized():
+            world = dist.get_world_size(group)
+            if world > 1:
+                dist.all_reduce(self.grad, op=dist.ReduceOp.SUM, group=group)
+                self.grad.div_(world)
+
+    def broadcast_(self, src=0, group=None):
+        """Start every replica from rank src's parameters."""
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+            dist.broadcast(self.data, src=src, group=group)
+
+
+class RMSPropTF1:
+    """tf.train.RMSPropOptimizer semantics: ms slot initialised to ONES, eps inside the sqrt,
+    decay 0.9, momentum 0 (a3c.py:264-265 uses the defaults with lr 1e-3)."""
+
+    def __init__(self, flat, lr=1e-3, decay=0.9, momentum=0.0, eps=1e-10):
+        self.flat = flat
+        self.lr, self.decay, self.momentum, self.eps = lr, decay, momentum, eps
+        self.ms = torch.ones_like(flat.data)
+        self.mom = torch.zeros_like(flat.data)
+
+    @torch.no_grad()
+    def step(self):
+        d, g = self.flat.data, self.flat.grad
+        if d.is_cuda:
+            from .kernels import rmsprop_tf1_
+            rmsprop_tf1_(d, g, self.ms, self.mom, self.lr, self.decay, self.momentum, self.eps)
+        else:
+            self.ms.mul_(self.decay).addcmul_(g, g, value=1.0 - self.decay)
+            self.mom.mul_(self.momentum).addcdiv_(g, (self.ms + self.eps).sqrt(), value=self.lr)
+            d.sub_(self.mom)

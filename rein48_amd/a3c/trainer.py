@@ -1,0 +1,155 @@
+"""Batched, synchronous A3C on the gfx950 env (the rows around the env step in SURVEY.md §8 a11-a16).
+
+The reference (algorithm/a3c/a3c.py) runs N_WORKERS Python threads, each with one Game and a
+local TF1 net: per episode segment it resets its game (:194), plays until done or MAX_STEP_NUM
+= 100 steps choosing actions by np.random.choice over the softmax (:201-212), bootstraps
+V(s_T) unless done (:218-223), builds discounted targets with gamma 0.9 dropping the last
+reward (:225, :246-256), and pushes its gradients into the global net with RMSProp (:233).
+
+Here one rollout advances every board of a VecGame in lockstep (millions of "workers" per GPU):
+    per step:  board_features kernel -> net forward (PyTorch-ROCm) -> r48_sample_actions
+               (fused softmax + Philox draw) -> r48_env_step (the env kernel)
+    update:    pass 1 (no grad) values, bootstrap and r48_discounted_returns, per-segment
+               constants; pass 2 chunked forward/backward of the loss (losses.py); one
+               all-reduce of the flat gradient (RCCL across GPUs); fused TF1 RMSProp kernel.
+mode "reference" keeps the reference's quirks: training pairs the POST-step state with the
+action chosen from the pre-step state (:203-209), reward is 0 (GameClient.py:138), the last
+reward is dropped, and the actor loss is the literal broadcast form. mode "textbook" uses
+pre-step states, the merge reward, full n-step returns and -(beta*H + td*log p[a]).
+"""
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+from ..env import VecGame
+from . import kernels as K
+from .losses import chunk_loss, segment_stats
+from .nets import make_net
+from .optim import FlatParams, RMSPropTF1
+
+
+@dataclass
+class A3CConfig:
+    n_boards: int = 4096          # boards (segments) per GPU
+    max_steps: int = 100          # MAX_STEP_NUM, a3c.py:20
+    gamma: float = 0.9            # a3c.py:247
+    beta: float = 0.001           # ENTROPY_BETA, a3c.py:21
+    lr: float = 1e-3              # LR_A = LR_C, a3c.py:22-23
+    net: str = "mlp"              # "mlp" (a3c.py:136-169) or "cnn" (ddpg/actor.py:51-85 trunk)
+    mode: str = "reference"       # "reference" | "textbook"
+    features: str = "values"      # "values" (raw tiles, a3c.py:139) | "exponents"
+    seed: int = 0
+    update_chunk: int = 25        # time steps per forward/backward chunk of the update
+    bf16: bool = False            # autocast the net to bf16 (MFMA) in rollout and update
+
+
+class A3CTrainer:
+    def __init__(self, cfg, device="cuda", group=None):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.group = group
+        self.rank = dist.get_rank(group) if dist.is_available() and dist.is_initialized() else 0
+        n, T = cfg.n_boards, cfg.max_steps
+        self.gid0 = self.rank * n
+        self.env = VecGame(n, device=self.device, seed=cfg.seed, board_offset=self.gid0)
+        torch.manual_seed(cfg.seed)
+        self.net = make_net(cfg.net).to(self.device)
+        self.flat = FlatParams(self.net)
+        self.flat.broadcast_(0, group)
+        self.opt = RMSPropTF1(self.flat, lr=cfg.lr)
+        self.boards = torch.zeros((T + 1, n, 16), dtype=torch.int8, device=self.device)
+        self.actions = torch.zeros((T, n), dtype=torch.int8, device=self.device)
+        self.done = torch.zeros((T, n), dtype=torch.uint8, device=self.device)
+        self.rewards = torch.zeros((T, n), dtype=torch.float32, device=self.device)
+        self.sample_ctr = 0
+        self.updates = 0
+
+    # ------------------------------------------------------------------ helpers
+    def _features(self, boards):
+        x = K.board_features(boards.reshape(-1, 16), exponents=self.cfg.features == "exponents")
+        return x
+
+    def _net(self, x):
+        if self.cfg.bf16:
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                logits, v = self.net(x)
+            return logits.float(), v.float()
+        return self.net(x)
+
+    # ------------------------------------------------------------------ rollout (a3c.py:194-212)
+    @torch.no_grad()
+    def rollout(self):
+        cfg, env = self.cfg, self.env
+        env.reset()
+        merge = cfg.mode == "textbook"
+        for t in range(cfg.max_steps):
+            self.boards[t].copy_(env.boards)
+            logits, _ = self._net(self._features(env.boards))
+            act, _, _ = K.sample_actions(logits.contiguous(), cfg.seed, self.sample_ctr, gid0=self.gid0)
+            self.sample_ctr += 1
+            _, reward, done = env.step(act, merge_reward=merge)
+            self.actions[t].copy_(act)
+            self.done[t].copy_(done)
+            if merge:
+                self.rewards[t].copy_(reward)
+            else:
+                self.rewards[t].zero_()  # GameClient.py:138: reward is always 0
+        self.boards[cfg.max_steps].copy_(env.boards)
+        # segment length: through the first done step, else max_steps (a3c.py:201)
+        notdone = (self.done.cumsum(0) == 0)
+        self.lengths = (notdone.sum(0) + 1).clamp(max=cfg.max_steps).to(torch.int32)
+        self.finished = self.done.bool().any(0)
+        t = torch.arange(cfg.max_steps, device=self.device).unsqueeze(1)
+        self.mask = t < self.lengths.unsqueeze(0)
+        return self.lengths
+
+    # ------------------------------------------------------------------ update (a3c.py:218-234)
+    def _states(self):
+        T = self.cfg.max_steps
+        return self.boards[1:T + 1] if self.cfg.mode == "reference" else self.boards[0:T]
+
+    def update(self):
+        cfg = self.cfg
+        T, n = cfg.max_steps, cfg.n_boards
+        states = self._states()
+        # pass 1: values of the training states and the bootstrap V(s_last) (a3c.py:218-223)
+        with torch.no_grad():
+            v_all = torch.empty((T, n), dtype=torch.float32, device=self.device)
+            for t0 in range(0, T, cfg.update_chunk):
+                t1 = min(T, t0 + cfg.update_chunk)
+                _, v = self._net(self._features(states[t0:t1]))
+                v_all[t0:t1] = v.view(t1 - t0, n)
+            # last post-step state of each segment = boards[len]
+            idx = self.lengths.long().view(1, n, 1).expand(1, n, 16)
+            last = self.boards.gather(0, idx)[0]
+            _, v_last = self._net(self._features(last))
+            boot = torch.where(self.finished, torch.zeros_like(v_last), v_last.view(n)).float().contiguous()
+            targets = K.discounted_returns(self.rewards, self.lengths, boot, cfg.gamma,
+                                           drop_last=cfg.mode == "reference")
+            stats = segment_stats(v_all, targets, self.actions, self.mask)
+        # pass 2: chunked forward/backward, gradients accumulate in the flat buffer
+        self.flat.zero_grad()
+        actor_total, critic_total = 0.0, 0.0
+        for t0 in range(0, T, cfg.update_chunk):
+            t1 = min(T, t0 + cfg.update_chunk)
+            logits, v = self._net(self._features(states[t0:t1]))
+            actor, critic = chunk_loss(logits.view(t1 - t0, n, 4), v.view(t1 - t0, n), self.actions[t0:t1],
+                                       targets[t0:t1], self.mask[t0:t1], stats, mode=cfg.mode, beta=cfg.beta)
+            (actor + critic).backward()
+            actor_total += float(actor.detach())
+            critic_total += float(critic.detach())
+        self.flat.allreduce_grad(self.group)   # RCCL across GPUs (a3c.py:79-80's push, synchronous)
+        self.opt.step()                        # fused TF1 RMSProp (a3c.py:264-265)
+        self.updates += 1
+        return {"actor_loss": actor_total, "critic_loss": critic_total,
+                "mean_length": float(self.lengths.float().mean()),
+                "finished": float(self.finished.float().mean())}
+
+    def train_step(self):
+        self.rollout()
+        return self.update()
+
+    def scores(self):
+        """a3c.py:214 SCORE: tile sum of each segment's final state."""
+        return self.env.score()

@@ -1,0 +1,239 @@
+// r48_a3c.hip -- gfx950 kernels for the A3C pieces on either side of the env step
+// (nevertiree/Rein48 algorithm/a3c/a3c.py), behind the same C-ABI (include/rein48.h).
+//
+//   k_features   board int8[16] -> network input float/bf16[16]: raw tile values 2^e
+//                (a3c.py:37-39,139 feed the raw state_matrix) or the exponent e
+//   k_sample     fused softmax + Philox inverse-CDF draw over 4 actions (choose_action,
+//                a3c.py:89-93: np.random.choice(range(4), p=softmax)); also log p[a] and the
+//                entropy term -sum p log(p+1e-5) of a3c.py:114
+//   k_returns    reverse discounted scan over a [T][n] reward slab (Worker._get_target_value_list,
+//                a3c.py:246-256, gamma 0.9, last reward dropped) or the textbook n-step return
+// All memory-bound elementwise/scan work: one row per lane, 16-B vector loads where the row
+// allows, time-major [T][n] slabs so every step of the scan is a coalesced row.
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+
+#include <cstdint>
+#include <string>
+
+#include "../../include/rein48.h"
+#include "r48_board.h"
+
+namespace r48 {
+void set_last_error(const std::string &msg);
+}
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr uint32_t kSampleTag = 0xA3Cu;
+
+inline dim3 grid_for(int64_t n) { return dim3((unsigned)((n + kBlock - 1) / kBlock)); }
+
+template <int MODE>
+__device__ __forceinline__ float cell_feature(uint32_t e)
+{
+    if (MODE == 0)
+        return e ? (float)(1u << (e & 31u)) : 0.0f;  // raw tile value
+    return (float)e;                                 // exponent
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void k_features_f32(const int8_t *__restrict__ boards, int64_t n,
+                                                         float *__restrict__ out)
+{
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n)
+        return;
+    const uint4 v = *reinterpret_cast<const uint4 *>(boards + 16 * i);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    float4 *o = reinterpret_cast<float4 *>(out + 16 * i);
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+        o[r] = make_float4(cell_feature<MODE>(w[r] & 0xffu), cell_feature<MODE>((w[r] >> 8) & 0xffu),
+                           cell_feature<MODE>((w[r] >> 16) & 0xffu), cell_feature<MODE>(w[r] >> 24));
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void k_features_bf16(const int8_t *__restrict__ boards, int64_t n,
+                                                          uint16_t *__restrict__ out)
+{
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n)
+        return;
+    const uint4 v = *reinterpret_cast<const uint4 *>(boards + 16 * i);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    uint32_t packed[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        const uint32_t lo = (w[k >> 1] >> (16 * (k & 1))) & 0xffu, hi = (w[k >> 1] >> (16 * (k & 1) + 8)) & 0xffu;
+        // 2^e and small integers are exact in bf16; plain casts keep NaN handling standard
+        const __hip_bfloat16 a = __float2bfloat16(cell_feature<MODE>(lo));
+        const __hip_bfloat16 b = __float2bfloat16(cell_feature<MODE>(hi));
+        packed[k] = (uint32_t)__bfloat16_as_ushort(a) | ((uint32_t)__bfloat16_as_ushort(b) << 16);
+    }
+    uint4 *o = reinterpret_cast<uint4 *>(out + 16 * i);
+    o[0] = make_uint4(packed[0], packed[1], packed[2], packed[3]);
+    o[1] = make_uint4(packed[4], packed[5], packed[6], packed[7]);
+}
+
+// softmax over 4 logits + inverse-CDF draw with a Philox uniform (24-bit, [0,1))
+__global__ __launch_bounds__(kBlock) void k_sample(const float *__restrict__ logits, int64_t n, int64_t gid0,
+                                                   uint32_t k0, uint32_t k1, uint32_t ctr,
+                                                   int8_t *__restrict__ actions, float *__restrict__ logp,
+                                                   float *__restrict__ entropy)
+{
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n)
+        return;
+    const float4 z = *reinterpret_cast<const float4 *>(logits + 4 * i);
+    const float m = fmaxf(fmaxf(z.x, z.y), fmaxf(z.z, z.w));
+    const float e0 = __expf(z.x - m), e1 = __expf(z.y - m), e2 = __expf(z.z - m), e3 = __expf(z.w - m);
+    const float s = e0 + e1 + e2 + e3, inv = 1.0f / s;
+    const float p0 = e0 * inv, p1 = e1 * inv, p2 = e2 * inv, p3 = e3 * inv;
+    uint32_t w[4] = {(uint32_t)(gid0 + i), (uint32_t)((uint64_t)(gid0 + i) >> 32), ctr, kSampleTag};
+    r48::philox4x32_10(w, k0, k1);
+    const float u = (float)(w[0] >> 8) * (1.0f / 16777216.0f);
+    // first k with cdf(k) > u (np.random.choice's searchsorted(..., side='right'))
+    const float c0 = p0, c1 = c0 + p1, c2 = c1 + p2;
+    const int a = (c0 > u) ? 0 : (c1 > u) ? 1 : (c2 > u) ? 2 : 3;
+    actions[i] = (int8_t)a;
+    if (logp) {
+        const float za = a == 0 ? z.x : a == 1 ? z.y : a == 2 ? z.z : z.w;
+        logp[i] = za - m - __logf(s);
+    }
+    if (entropy)
+        entropy[i] = -(p0 * __logf(p0 + 1e-5f) + p1 * __logf(p1 + 1e-5f) + p2 * __logf(p2 + 1e-5f) +
+                       p3 * __logf(p3 + 1e-5f));
+}
+
+// targets[t][i] for t < len[i]; 0 for t >= len[i]. DROP_LAST: the reference's scan
+// (targets[len-1] = bootstrap), else the textbook return (targets[len-1] = r + gamma*bootstrap).
+template <bool DROP_LAST>
+__global__ __launch_bounds__(kBlock) void k_returns(const float *__restrict__ rewards, const int32_t *__restrict__ len,
+                                                    const float *__restrict__ bootstrap, int32_t T, int64_t n,
+                                                    float gamma, float *__restrict__ out)
+{
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n)
+        return;
+    const int32_t L = min(max(len[i], 0), T);
+    for (int32_t t = T - 1; t >= L; t--)
+        out[(int64_t)t * n + i] = 0.0f;
+    float g = bootstrap[i];
+    for (int32_t t = L - 1; t >= 0; t--) {
+        if (DROP_LAST && t == L - 1) {
+            out[(int64_t)t * n + i] = g;
+            continue;
+        }
+        g = rewards[(int64_t)t * n + i] + gamma * g;
+        out[(int64_t)t * n + i] = g;
+    }
+}
+
+// tf.train.RMSPropOptimizer (TF1) ApplyRMSProp over one flat parameter buffer:
+//   ms  <- decay*ms + (1-decay)*g^2          (ms slot initialised to ONES by the caller)
+//   mom <- momentum*mom + lr*g/sqrt(ms + eps)
+//   var <- var - mom
+__global__ __launch_bounds__(kBlock) void k_rmsprop_tf1(float *__restrict__ var, const float *__restrict__ grad,
+                                                        float *__restrict__ ms, float *__restrict__ mom, int64_t n,
+                                                        float lr, float decay, float momentum, float eps)
+{
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n)
+        return;
+    const float g = grad[i];
+    const float m = decay * ms[i] + (1.0f - decay) * g * g;
+    const float u = momentum * mom[i] + lr * g / sqrtf(m + eps);
+    ms[i] = m;
+    mom[i] = u;
+    var[i] -= u;
+}
+
+int fail(int code, const char *msg)
+{
+    r48::set_last_error(msg);  // the thread-local message behind r48_last_error (r48_env.hip)
+    return code;
+}
+
+int launched(const char *what)
+{
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        r48::set_last_error(std::string(what) + ": " + hipGetErrorString(e));
+        return R48_EHIP;
+    }
+    return R48_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int r48_board_features(const int8_t *boards, int64_t n, int32_t mode, int32_t out_dtype, void *out, void *stream)
+{
+    if (!boards || !out || n < 0 || (mode != R48_FEAT_VALUES && mode != R48_FEAT_EXPONENTS) ||
+        (out_dtype != R48_F32 && out_dtype != R48_BF16))
+        return fail(R48_EINVAL, "boards/out NULL, n < 0, or bad mode/dtype");
+    if ((reinterpret_cast<uintptr_t>(boards) | reinterpret_cast<uintptr_t>(out)) & 15u)
+        return fail(R48_EINVAL, "boards and out must be 16-byte aligned");
+    if (n == 0)
+        return R48_OK;
+    const hipStream_t s = (hipStream_t)stream;
+    if (out_dtype == R48_F32) {
+        if (mode == R48_FEAT_VALUES)
+            hipLaunchKernelGGL(k_features_f32<0>, grid_for(n), dim3(kBlock), 0, s, boards, n, (float *)out);
+        else
+            hipLaunchKernelGGL(k_features_f32<1>, grid_for(n), dim3(kBlock), 0, s, boards, n, (float *)out);
+    } else {
+        if (mode == R48_FEAT_VALUES)
+            hipLaunchKernelGGL(k_features_bf16<0>, grid_for(n), dim3(kBlock), 0, s, boards, n, (uint16_t *)out);
+        else
+            hipLaunchKernelGGL(k_features_bf16<1>, grid_for(n), dim3(kBlock), 0, s, boards, n, (uint16_t *)out);
+    }
+    return launched("k_features");
+}
+
+int r48_sample_actions(const float *logits, int64_t n, uint64_t seed, int64_t gid0, uint32_t ctr, int8_t *actions,
+                       float *logp, float *entropy, void *stream)
+{
+    if (!logits || !actions || n < 0 || gid0 < 0)
+        return fail(R48_EINVAL, "logits/actions NULL or n/gid0 < 0");
+    if (reinterpret_cast<uintptr_t>(logits) & 15u)
+        return fail(R48_EINVAL, "logits must be 16-byte aligned");
+    if (n == 0)
+        return R48_OK;
+    hipLaunchKernelGGL(k_sample, grid_for(n), dim3(kBlock), 0, (hipStream_t)stream, logits, n, gid0, (uint32_t)seed,
+                       (uint32_t)(seed >> 32), ctr, actions, logp, entropy);
+    return launched("k_sample");
+}
+
+int r48_rmsprop_tf1(float *var, const float *grad, float *ms, float *mom, int64_t n, float lr, float decay,
+                    float momentum, float eps, void *stream)
+{
+    if (!var || !grad || !ms || !mom || n < 0)
+        return fail(R48_EINVAL, "NULL argument or n < 0");
+    if (n == 0)
+        return R48_OK;
+    hipLaunchKernelGGL(k_rmsprop_tf1, grid_for(n), dim3(kBlock), 0, (hipStream_t)stream, var, grad, ms, mom, n, lr,
+                       decay, momentum, eps);
+    return launched("k_rmsprop_tf1");
+}
+
+int r48_discounted_returns(const float *rewards, const int32_t *lengths, const float *bootstrap, int32_t T, int64_t n,
+                           float gamma, int32_t drop_last, float *out, void *stream)
+{
+    if (!rewards || !lengths || !bootstrap || !out || T < 1 || n < 0)
+        return fail(R48_EINVAL, "NULL argument, T < 1 or n < 0");
+    if (n == 0)
+        return R48_OK;
+    if (drop_last)
+        hipLaunchKernelGGL(k_returns<true>, grid_for(n), dim3(kBlock), 0, (hipStream_t)stream, rewards, lengths,
+                           bootstrap, T, n, gamma, out);
+    else
+        hipLaunchKernelGGL(k_returns<false>, grid_for(n), dim3(kBlock), 0, (hipStream_t)stream, rewards, lengths,
+                           bootstrap, T, n, gamma, out);
+    return launched("k_returns");
+}
+
+}  // extern "C"

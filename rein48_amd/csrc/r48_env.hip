@@ -418,6 +418,14 @@ namespace {
 
 thread_local std::string g_last_error;
 
+}  // namespace
+
+namespace r48 {
+void set_last_error(const std::string &msg) { g_last_error = msg; }
+}  // namespace r48
+
+namespace {
+
 int fail(int code, const std::string &msg)
 {
     g_last_error = msg;
