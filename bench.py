@@ -151,6 +151,38 @@ def extras(dev, seed, n_small):
     return out
 
 
+def a3c_config3(dev, seed, n_boards, updates=2):
+    """BASELINE configs[2]: 2^20 boards + 2-layer CNN policy (bf16 MFMA via hipBLASLt), A3C
+    rollout (MAX_STEP_NUM = 100 steps: features kernel -> CNN -> fused softmax/Philox sampling
+    -> env kernel) and the synchronous update (chunked forward/backward, TF1 RMSProp kernel)."""
+    from rein48_amd.a3c import A3CConfig, A3CTrainer
+    cfg = A3CConfig(n_boards=n_boards, max_steps=100, mode="textbook", net="cnn", bf16=True,
+                    features="exponents", seed=seed, update_chunk=10)
+    tr = A3CTrainer(cfg, device=dev)
+    tr.train_step()                                   # warm-up (allocator, hipBLASLt heuristics)
+    s = torch.cuda.current_stream(dev)
+    roll_ms, upd_ms, steps = [], [], 0
+    for _ in range(updates):
+        a, b, c = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+        a.record(s)
+        tr.rollout()
+        b.record(s)
+        out = tr.update()
+        c.record(s)
+        torch.cuda.synchronize(dev)
+        roll_ms.append(a.elapsed_time(b))
+        upd_ms.append(b.elapsed_time(c))
+        steps += int(tr.lengths.sum())
+    r, u = sum(roll_ms) / updates, sum(upd_ms) / updates
+    board_steps = n_boards * cfg.max_steps          # every board is stepped every rollout step
+    return {"boards": n_boards, "net": "cnn (conv2x2x32, conv2x2x64, heads 256->4/1), bf16 autocast",
+            "rollout_ms": r, "update_ms": u,
+            "rollout_env_steps_per_s": board_steps / (r * 1e-3),
+            "train_env_steps_per_s": board_steps / ((r + u) * 1e-3),
+            "valid_segment_steps_per_update": steps / updates,
+            "last_losses": {k: out[k] for k in ("actor_loss", "critic_loss")}}
+
+
 def traffic_from_profile(n_boards):
     p = os.path.join(ROOT, "profiles", "pmc_k_step.json")
     if not os.path.exists(p):
@@ -255,6 +287,10 @@ def main():
         line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
     if rank == 0 and world == 1 and not args.no_extras:
         ex = extras(dev, args.seed, n)
+        try:
+            ex["a3c_config3"] = a3c_config3(dev, args.seed, n)
+        except Exception as e:  # the env bench line must print even if the trainer fails
+            ex["a3c_config3"] = {"error": repr(e)}
         if not args.no_cpu_baseline:
             ex["cpu_strong_line"] = strong_cpu_line()
         line["extras"] = ex

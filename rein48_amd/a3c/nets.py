@@ -8,15 +8,58 @@ ActorCriticMLP  -- the reference network, algorithm/a3c/a3c.py:136-169:
 ActorCriticCNN  -- BASELINE config 3's "2-layer CNN policy", the trunk of the reference's only CNN
     (algorithm/ddpg/actor.py:51-85: conv 2x2 valid x32 ReLU -> conv 2x2 valid x64 ReLU -> 256),
     with an actor head (256->4, softmax) and a critic head (256->1). Xavier init as in a3c.py
-    (the DDPG actor's N(1, 2) init saturates on raw tile values). Both convolutions are written
-    as patch-gather + GEMM so the batch (millions of boards) lands on hipBLASLt/MFMA as two large
-    GEMMs instead of MIOpen convolutions over 4x4 images.
+    (the DDPG actor's N(1, 2) init saturates on raw tile values).
+
+MI355X layout: a board is only 4x4, so each convolution is ONE dense GEMM over the whole batch
+with a structured weight assembled (differentiably) from the small conv kernel: conv1 is
+16 -> 9x32 = 288 and conv2 is 288 -> 4x64 = 256. That trades ~2x dense FLOPs for zero gathers
+(a patch-gather formulation spent most of its update time in the gather's scatter-add
+backward), and every layer lands on hipBLASLt bf16 MFMA tiles with M = boards.
+The weight gradient of every layer is a reduction over millions of rows into a few thousand
+outputs; SplitKLinear computes it as a batched GEMM over row chunks followed by a sum, instead
+of one GEMM with K = rows that cannot fill the chip.
 forward(x[B,16]) returns (logits[B,4], value[B]); logits are what the softmax / the sampling
 kernel consume (for the MLP already through the ReLU of a3c.py:153).
 """
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
+
+SPLITK_MIN_ROWS = 1 << 16
+
+
+class _SplitKLinear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        ctx.has_bias = b is not None
+        return F.linear(x, w, b)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        acc = torch.float64 if x.dtype == torch.float64 else torch.float32  # bf16 partials sum in fp32
+        gx = gy @ w
+        rows = x.shape[0]
+        if rows >= SPLITK_MIN_ROWS:
+            s = min(1024, rows // 8192)
+            main = (rows // s) * s
+            gw = torch.bmm(gy[:main].view(s, -1, gy.shape[1]).transpose(1, 2),
+                           x[:main].view(s, -1, x.shape[1])).to(acc).sum(0)
+            if main < rows:
+                gw += (gy[main:].t() @ x[main:]).to(acc)
+        else:
+            gw = (gy.t() @ x).to(acc)
+        gb = gy.to(acc).sum(0) if ctx.has_bias else None
+        return gx, gw.to(w.dtype), (gb.to(w.dtype) if gb is not None else None)
+
+
+def linear(x, w, b, dtype):
+    """x @ w^T + b computed in `dtype` (bf16 -> MFMA) with the split-K weight gradient."""
+    if x.dim() != 2:
+        shp = x.shape
+        return linear(x.reshape(-1, shp[-1]), w, b, dtype).view(*shp[:-1], w.shape[0])
+    return _SplitKLinear.apply(x.to(dtype), w.to(dtype), None if b is None else b.to(dtype))
 
 
 def _xavier_(layer):
@@ -26,18 +69,20 @@ def _xavier_(layer):
 
 
 class ActorCriticMLP(nn.Module):
-    def __init__(self):
+    def __init__(self, dtype=torch.float32):
         super().__init__()
+        self.dtype = dtype
         self.a1 = _xavier_(nn.Linear(16, 64))
         self.a2 = _xavier_(nn.Linear(64, 4))
         self.c1 = _xavier_(nn.Linear(16, 64))
         self.c2 = _xavier_(nn.Linear(64, 1))
 
     def forward(self, x):
-        h = F.relu6(self.a1(x))
-        logits = F.relu(self.a2(h))
-        v = self.c2(F.relu6(self.c1(x)))[..., 0]
-        return logits, v
+        d = self.dtype
+        h = F.relu6(linear(x, self.a1.weight, self.a1.bias, d))
+        logits = F.relu(linear(h, self.a2.weight, self.a2.bias, d))
+        v = linear(F.relu6(linear(x, self.c1.weight, self.c1.bias, d)), self.c2.weight, self.c2.bias, d)[..., 0]
+        return logits.float(), v.float()
 
     @torch.no_grad()
     def load_reference_params(self, p):
@@ -54,35 +99,57 @@ class ActorCriticMLP(nn.Module):
         return out
 
 
-# patch indices: conv1 (2x2 valid on 4x4 -> 3x3) and conv2 (2x2 valid on 3x3 -> 2x2)
 def _patches(h, k):
+    """patch index lists of a k x k valid convolution over an h x h grid (row-major)."""
     out = h - k + 1
-    idx = []
-    for r in range(out):
-        for c in range(out):
-            idx.append([(r + dr) * h + (c + dc) for dr in range(k) for dc in range(k)])
-    return torch.tensor(idx, dtype=torch.long)
+    return [[(r + dr) * h + (c + dc) for dr in range(k) for dc in range(k)] for r in range(out) for c in range(out)]
 
 
 class ActorCriticCNN(nn.Module):
-    def __init__(self):
+    def __init__(self, dtype=torch.float32):
         super().__init__()
-        self.conv1 = nn.Linear(4, 32)      # 2x2x1 -> 32
-        self.conv2 = nn.Linear(4 * 32, 64)  # 2x2x32 -> 64
-        self.actor = nn.Linear(4 * 64, 4)
-        self.critic = nn.Linear(4 * 64, 1)
-        for lay in (self.conv1, self.conv2, self.actor, self.critic):
+        self.dtype = dtype
+        self.conv1 = nn.Linear(4, 32)       # 2x2x1 kernel, flattened (dr, dc)
+        self.conv2 = nn.Linear(4 * 32, 64)  # 2x2x32 kernel, flattened (patch position, channel)
+        self.heads = nn.Linear(4 * 64, 5)   # actor 4 + critic 1
+        for lay in (self.conv1, self.conv2, self.heads):
             _xavier_(lay)
-        self.register_buffer("p1", _patches(4, 2), persistent=False)   # [9, 4]
-        self.register_buffer("p2", _patches(3, 2), persistent=False)   # [4, 4]
+        # scatter maps from the conv kernels into the dense structured weights
+        p1, p2 = _patches(4, 2), _patches(3, 2)
+        r1, c1, k1 = [], [], []
+        for pos, cells in enumerate(p1):                 # 9 output positions
+            for f in range(32):
+                for k, cell in enumerate(cells):
+                    r1.append(pos * 32 + f)
+                    c1.append(cell)
+                    k1.append(f * 4 + k)                 # index into conv1.weight.view(-1)
+        r2, c2, k2 = [], [], []
+        for pos, cells in enumerate(p2):                 # 4 output positions over the 3x3 grid
+            for g in range(64):
+                for kk, cell in enumerate(cells):
+                    for f in range(32):
+                        r2.append(pos * 64 + g)
+                        c2.append(cell * 32 + f)
+                        k2.append(g * 128 + kk * 32 + f)
+        for name, v in (("r1", r1), ("c1", c1), ("k1", k1), ("r2", r2), ("c2", c2), ("k2", k2)):
+            self.register_buffer(name, torch.tensor(v, dtype=torch.long), persistent=False)
+
+    def dense_weights(self):
+        w1 = torch.zeros(9 * 32, 16, dtype=self.conv1.weight.dtype, device=self.conv1.weight.device)
+        w1 = w1.index_put((self.r1, self.c1), self.conv1.weight.reshape(-1)[self.k1])
+        w2 = torch.zeros(4 * 64, 9 * 32, dtype=self.conv2.weight.dtype, device=self.conv2.weight.device)
+        w2 = w2.index_put((self.r2, self.c2), self.conv2.weight.reshape(-1)[self.k2])
+        return w1, self.conv1.bias.repeat(9), w2, self.conv2.bias.repeat(4)
 
     def forward(self, x):
-        B = x.shape[0]
-        h1 = F.relu(self.conv1(x[:, self.p1]))                          # [B, 9, 32]
-        h2 = F.relu(self.conv2(h1[:, self.p2].reshape(B, 4, 4 * 32)))   # [B, 4, 64]
-        h = h2.reshape(B, 4 * 64)
-        return self.actor(h), self.critic(h)[..., 0]
+        d = self.dtype
+        w1, b1, w2, b2 = self.dense_weights()
+        h1 = F.relu(linear(x, w1, b1, d))               # [B, 9*32]  = conv 2x2 valid, 32 filters
+        h2 = F.relu(linear(h1, w2, b2, d))              # [B, 4*64]  = conv 2x2 valid, 64 filters
+        out = linear(h2, self.heads.weight, self.heads.bias, d).float()
+        return out[:, :4], out[:, 4]
 
 
-def make_net(kind):
-    return {"mlp": ActorCriticMLP, "cnn": ActorCriticCNN}[kind]()
+def make_net(kind, bf16=False):
+    dt = torch.bfloat16 if bf16 else torch.float32
+    return {"mlp": ActorCriticMLP, "cnn": ActorCriticCNN}[kind](dtype=dt)

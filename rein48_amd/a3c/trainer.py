@@ -41,7 +41,7 @@ class A3CConfig:
     features: str = "values"      # "values" (raw tiles, a3c.py:139) | "exponents"
     seed: int = 0
     update_chunk: int = 25        # time steps per forward/backward chunk of the update
-    bf16: bool = False            # autocast the net to bf16 (MFMA) in rollout and update
+    bf16: bool = False            # run the net's GEMMs in bf16 (MFMA, fp32 accumulate)
 
 
 class A3CTrainer:
@@ -54,7 +54,7 @@ class A3CTrainer:
         self.gid0 = self.rank * n
         self.env = VecGame(n, device=self.device, seed=cfg.seed, board_offset=self.gid0)
         torch.manual_seed(cfg.seed)
-        self.net = make_net(cfg.net).to(self.device)
+        self.net = make_net(cfg.net, bf16=cfg.bf16).to(self.device)
         self.flat = FlatParams(self.net)
         self.flat.broadcast_(0, group)
         self.opt = RMSPropTF1(self.flat, lr=cfg.lr)
@@ -71,11 +71,7 @@ class A3CTrainer:
         return x
 
     def _net(self, x):
-        if self.cfg.bf16:
-            with torch.autocast("cuda", dtype=torch.bfloat16):
-                logits, v = self.net(x)
-            return logits.float(), v.float()
-        return self.net(x)
+        return self.net(x)  # bf16 (MFMA) or fp32 compute per cfg.bf16; outputs fp32
 
     # ------------------------------------------------------------------ rollout (a3c.py:194-212)
     @torch.no_grad()
@@ -83,6 +79,8 @@ class A3CTrainer:
         cfg, env = self.cfg, self.env
         env.reset()
         merge = cfg.mode == "textbook"
+        if not merge:
+            self.rewards.zero_()  # GameClient.py:138: reward is always 0
         for t in range(cfg.max_steps):
             self.boards[t].copy_(env.boards)
             logits, _ = self._net(self._features(env.boards))
@@ -93,8 +91,6 @@ class A3CTrainer:
             self.done[t].copy_(done)
             if merge:
                 self.rewards[t].copy_(reward)
-            else:
-                self.rewards[t].zero_()  # GameClient.py:138: reward is always 0
         self.boards[cfg.max_steps].copy_(env.boards)
         # segment length: through the first done step, else max_steps (a3c.py:201)
         notdone = (self.done.cumsum(0) == 0)
