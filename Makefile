@@ -3,7 +3,7 @@ HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -Wall -Wno-unused-function
 LIBDIR := rein48_amd/lib
-SRC := rein48_amd/csrc/r48_env.hip rein48_amd/csrc/r48_a3c.hip
+SRC := rein48_amd/csrc/r48_env.hip rein48_amd/csrc/r48_a3c.hip rein48_amd/csrc/r48_policy.hip
 DEPS := rein48_amd/csrc/r48_board.h include/rein48.h
 
 all: $(LIBDIR)/librein48.so oracle
@@ -17,6 +17,8 @@ asm: $(SRC) $(DEPS)
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) --cuda-device-only -S -o build/r48_env.s rein48_amd/csrc/r48_env.hip
 	$(HIPCC) $(HIPFLAGS) --cuda-device-only -S -o build/r48_a3c.s rein48_amd/csrc/r48_a3c.hip
+	$(HIPCC) $(HIPFLAGS) --cuda-device-only -S -o build/r48_policy.s rein48_amd/csrc/r48_policy.hip
+	$(HIPCC) $(HIPFLAGS) --cuda-device-only -c -o /dev/null -Rpass-analysis=kernel-resource-usage rein48_amd/csrc/r48_policy.hip 2> build/resource_usage_policy.txt
 	$(HIPCC) $(HIPFLAGS) --cuda-device-only -c -o /dev/null -Rpass-analysis=kernel-resource-usage rein48_amd/csrc/r48_env.hip 2> build/resource_usage.txt
 
 oracle:

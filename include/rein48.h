@@ -170,6 +170,16 @@ int r48_discounted_returns(const float *rewards, const int32_t *lengths, const f
 int r48_rmsprop_tf1(float *var, const float *grad, float *ms, float *mom, int64_t n, float lr,
                     float decay, float momentum, float eps, void *stream);
 
+/* Fused 2-layer CNN policy inference (config 3; rein48_amd/a3c/nets.py:ActorCriticCNN, the
+ * conv trunk of algorithm/ddpg/actor.py:51-85 with actor/critic heads) on bf16 MFMA:
+ * boards int8[n][16] -> logits float[n][4] and value float[n] (each nullable), and, when
+ * actions != NULL, the choose_action draw of r48_sample_actions (same Philox contract) into
+ * actions int8[n]. wfrag: 41 x 64 x 8 bf16 weight fragments and bias: 104 floats, both packed
+ * by rein48_amd/a3c/fused.py:pack_cnn (16-byte aligned). mode: R48_FEAT_VALUES/EXPONENTS. */
+int r48_cnn_policy_forward(const int8_t *boards, int64_t n, const void *wfrag, const float *bias,
+                           int32_t mode, float *logits, float *value, int8_t *actions, uint64_t seed,
+                           int64_t gid0, uint32_t ctr, void *stream);
+
 /* Thread-local message of the last failed call on this thread ("" if none). */
 const char *r48_last_error(void);
 /* "rein48 <version> gfx950" */

@@ -24,6 +24,7 @@ import torch.distributed as dist
 
 from ..env import VecGame
 from . import kernels as K
+from .fused import cnn_forward, pack_cnn
 from .losses import chunk_loss, segment_stats
 from .nets import make_net
 from .optim import FlatParams, RMSPropTF1
@@ -42,6 +43,7 @@ class A3CConfig:
     seed: int = 0
     update_chunk: int = 25        # time steps per forward/backward chunk of the update
     bf16: bool = False            # run the net's GEMMs in bf16 (MFMA, fp32 accumulate)
+    fused_policy: bool = True     # cnn + bf16: rollout inference in one fused MFMA kernel (r48_policy.hip)
 
 
 class A3CTrainer:
@@ -81,10 +83,18 @@ class A3CTrainer:
         merge = cfg.mode == "textbook"
         if not merge:
             self.rewards.zero_()  # GameClient.py:138: reward is always 0
+        fused = cfg.net == "cnn" and cfg.bf16 and cfg.fused_policy
+        if fused:
+            wfrag, bias = pack_cnn(self.net)   # weights are fixed for the whole rollout
         for t in range(cfg.max_steps):
             self.boards[t].copy_(env.boards)
-            logits, _ = self._net(self._features(env.boards))
-            act, _, _ = K.sample_actions(logits.contiguous(), cfg.seed, self.sample_ctr, gid0=self.gid0)
+            if fused:   # board -> CNN -> softmax -> Philox draw in one kernel
+                _, _, act = cnn_forward(env.boards, wfrag, bias, exponents=cfg.features == "exponents",
+                                        logits=False, value=False, actions=True, seed=cfg.seed,
+                                        ctr=self.sample_ctr, gid0=self.gid0)
+            else:
+                logits, _ = self._net(self._features(env.boards))
+                act, _, _ = K.sample_actions(logits.contiguous(), cfg.seed, self.sample_ctr, gid0=self.gid0)
             self.sample_ctr += 1
             _, reward, done = env.step(act, merge_reward=merge)
             self.actions[t].copy_(act)

@@ -1,0 +1,47 @@
+"""Drop-in for nevertiree/Rein48 main.py: `python -m rein48_amd.main -c rand -v y`.
+
+play() is the reference's episode loop (main.py:11-48) over the drop-in Game (GPU kernels);
+the score is the tile-value sum (main.py:48). The CLI keeps the reference's flags (main.py:55-71).
+"""
+import argparse
+
+from .control.hand import Hand
+from .control.rand import Rand
+from .game.GameClient import Game
+
+BANNER = "PLEASE INPUT [ACTION DIRECTION] TO PLAY THIS GAME.\n" \
+         "Left: [L] or [l] \nRight:[R] or [r] \nUp:   [U] or [u] \nDown: [D] or [d] "
+
+
+def play(game, control="hand", show_state=False, show_result=True):
+    strategy = {"rand": Rand.random_action, "hand": Hand.hand_control}[control]
+    if control == "hand":
+        show_state, show_result = True, True
+        print(BANNER)
+    done = False
+    while not done:
+        if show_state:
+            Game.print_terminal(game.state_matrix)
+        _, _, done = game.step(strategy(game.state_matrix))
+    if show_result:
+        Game.print_terminal(game.state_matrix)
+    return sum(sum(row) for row in game.state_matrix)
+
+
+def parse(argv=None):
+    ap = argparse.ArgumentParser(description="Play terminal 2048...")
+    ap.add_argument("-c", "--control", type=str, dest="control", default="hand", help="Auto-control or hand-control")
+    ap.add_argument("-v", "--visual", type=str, dest="visual", default="y")
+    args = ap.parse_args(argv)
+    control = "rand" if args.control in ("rand", "Rand", "RAND", "r", "R") else "hand"
+    visual = args.visual in ("Y", "y", "Yes", "yes")
+    return control, visual
+
+
+def main(argv=None):
+    control, visual = parse(argv)
+    return play(game=Game(), control=control, show_result=visual)
+
+
+if __name__ == "__main__":
+    main()

@@ -128,3 +128,46 @@ def test_trainer_textbook_modes_run(net, bf16):
     for h in hist:
         assert np.isfinite(h["actor_loss"]) and np.isfinite(h["critic_loss"])
     assert tr.flat.grad.abs().sum() > 0
+
+
+@pytest.mark.parametrize("exponents", [False, True])
+def test_fused_cnn_policy_matches_torch(exponents):
+    """r48_cnn_policy_forward (bf16 MFMA, register-chained layers) vs the PyTorch CNN.
+    Error metric: max |got - ref| / (|ref| + mean|ref|). Against fp32 the kernel's error must be
+    within 1.5x of PyTorch's own bf16 forward's error (same rounding points: bf16 inputs, weights,
+    activations; fp32 accumulation) and below 4e-2 (exponent inputs) / 8e-2 (raw tile values up
+    to 2^11); against the bf16 PyTorch forward within 2e-2. The fused draw equals k_sample on the
+    kernel's own logits."""
+    from rein48_amd.a3c import kernels as K
+    from rein48_amd.a3c.fused import cnn_forward, pack_cnn
+    from rein48_amd.a3c.nets import ActorCriticCNN
+    torch.manual_seed(3)
+    net = ActorCriticCNN().to(DEV)
+    with torch.no_grad():                       # non-trivial biases so every bias path is checked
+        for m in (net.conv1, net.conv2, net.heads):
+            m.bias.uniform_(-0.5, 0.5)
+    rng = np.random.default_rng(4)
+    n = 100_003                                  # a partial last tile
+    b = rng.integers(1, 12, size=(n, 16)).astype(np.int8)
+    b[rng.random((n, 16)) < 0.4] = 0
+    boards = torch.from_numpy(b).to(DEV)
+    x = K.board_features(boards, exponents=exponents)
+    wfrag, bias = pack_cnn(net)
+    lg, v, _ = cnn_forward(boards, wfrag, bias, exponents=exponents)
+
+    def worst(a, b):
+        return max(float(((g - r).abs() / (r.abs() + r.abs().mean())).max()) for g, r in zip(a, b))
+
+    with torch.no_grad():
+        ref32 = net(x)
+        net.dtype = torch.bfloat16
+        ref16 = net(x)
+    e_kernel, e_torch_bf16 = worst((lg, v), ref32), worst(ref16, ref32)
+    # the fused kernel is as accurate as PyTorch's own bf16 path (both vs fp32), and close to it
+    assert e_kernel <= 1.5 * e_torch_bf16 + 1e-3, (e_kernel, e_torch_bf16)
+    assert e_kernel <= (4e-2 if exponents else 8e-2), e_kernel
+    assert worst((lg, v), ref16) <= 2e-2
+    _, _, act = cnn_forward(boards, wfrag, bias, exponents=exponents, logits=False, value=False, actions=True,
+                            seed=9, ctr=4, gid0=17)
+    want, _, _ = K.sample_actions(lg, 9, 4, gid0=17)
+    assert torch.equal(act, want)

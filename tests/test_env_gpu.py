@@ -437,3 +437,18 @@ def test_step_n_chains_and_wide_tiles_match_oracle(n):
     for t in range(4):
         want = O.step_philox(want, seed, t, O.RANDOM_POLICY | O.AUTO_RESET, board_offset=3)["boards"]
     assert np.array_equal(host(a.boards), want)
+
+
+def test_play_loop_matches_reference_score(golden):
+    """main.py's play() with the rand policy under random.seed: same final score as the
+    reference episode (tile sum, main.py:48)."""
+    import random
+    from rein48_amd.game import Game
+    from rein48_amd.main import play
+    z = golden["traj"]
+    for seed in range(3):
+        random.seed(seed)
+        score = play(Game(), control="rand", show_result=False)
+        m = (z["step_seed"] == seed) & (z["step_episode"] == 0)
+        last = z["step_after"][m][-1].astype(np.int64)
+        assert score == int(np.where(last > 0, 1 << last, 0).sum())
