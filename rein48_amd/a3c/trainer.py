@@ -120,16 +120,22 @@ class A3CTrainer:
         T, n = cfg.max_steps, cfg.n_boards
         states = self._states()
         # pass 1: values of the training states and the bootstrap V(s_last) (a3c.py:218-223)
+        fused = cfg.net == "cnn" and cfg.bf16 and cfg.fused_policy
         with torch.no_grad():
+            if fused:   # values of all T*n training states in one fused MFMA launch
+                wfrag, bias = pack_cnn(self.net)
+                value = lambda b: cnn_forward(b.reshape(-1, 16), wfrag, bias, exponents=cfg.features == "exponents",
+                                              logits=False, value=True)[1]
+            else:
+                value = lambda b: self._net(self._features(b))[1]
             v_all = torch.empty((T, n), dtype=torch.float32, device=self.device)
-            for t0 in range(0, T, cfg.update_chunk):
-                t1 = min(T, t0 + cfg.update_chunk)
-                _, v = self._net(self._features(states[t0:t1]))
-                v_all[t0:t1] = v.view(t1 - t0, n)
+            for t0 in range(0, T, T if fused else cfg.update_chunk):
+                t1 = min(T, t0 + (T if fused else cfg.update_chunk))
+                v_all[t0:t1] = value(states[t0:t1].contiguous()).view(t1 - t0, n)
             # last post-step state of each segment = boards[len]
             idx = self.lengths.long().view(1, n, 1).expand(1, n, 16)
-            last = self.boards.gather(0, idx)[0]
-            _, v_last = self._net(self._features(last))
+            last = self.boards.gather(0, idx)[0].contiguous()
+            v_last = value(last)
             boot = torch.where(self.finished, torch.zeros_like(v_last), v_last.view(n)).float().contiguous()
             targets = K.discounted_returns(self.rewards, self.lengths, boot, cfg.gamma,
                                            drop_last=cfg.mode == "reference")
