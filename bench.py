@@ -4,8 +4,9 @@
 Workload (BASELINE.json configs[1], "1M parallel 4x4 int8 boards, random policy, env-only
 throughput on 1 MI355X"): 2^20 boards per GPU, every step = one gfx950 k_step launch over
 all of them (move + spawn + game-over + auto-reset, in-kernel uniform random policy,
-actions and done flags written back). Boards start from the reference reset rule (one
-tile) and are resident in HBM before the timed region. Steps are issued in hipGraph
+actions and done flags written back). Boards start from SURVEY.md 8(d)'s synthetic fill
+(each cell empty w.p. 1/2, else exponent ~U{1..7}; the reference reset start is an extra)
+and are resident in HBM before the timed region. Steps are issued in hipGraph
 chunks (r48_env_step_n) so the host never gates the GPU.
 
 Multi-GPU: one process per GPU (torchrun), each rank owns boards [rank*N, (rank+1)*N)
@@ -19,8 +20,9 @@ Extra objects on the JSON line:
                 `traffic` = per-launch HBM bytes from rocprofv3 PMC passes when
                 profiles/pmc_k_step.json exists (tools/pmc_traffic.py), else null.
   cpu_baseline  oracle/game_port.py (faithful pure-Python restatement of the reference
-                Game + Rand, calibrated against the reference in BASELINE.md) on one host
-                core for a bounded sample, rank 0, N=1 only.
+                Game + Rand, calibrated against the reference in BASELINE.md) on one process
+                per available host CPU (at most 16, the box's share) for a bounded sample,
+                plus the 1-process figure; rank 0, N=1 only (oracle/port_bench.py).
   extras        HBM-honest point (2^26 boards/GPU, past the 256 MiB Infinity Cache), the
                 fused random-policy rollout kernel, and the C oracle as a strong CPU line.
 """
@@ -64,28 +66,16 @@ def chunks(total, size):
 
 
 def cpu_baseline(seconds):
-    """oracle/game_port.py on one core for ~`seconds` (bounded sample)."""
-    from oracle import game_port
-    import platform
-    steps, t0 = 0, time.perf_counter()
-    seed = 0
-    while time.perf_counter() - t0 < seconds:
-        game_port.run_steps(20_000, seed=seed)
-        steps += 20_000
-        seed += 1
-    dt = time.perf_counter() - t0
-    cpu = "unknown"
-    try:
-        for line in open("/proc/cpuinfo"):
-            if line.startswith("model name"):
-                cpu = line.split(":", 1)[1].strip()
-                break
-    except OSError:
-        pass
-    return {"value": steps / dt, "unit": "env steps/s", "cores": 1, "kind": "port",
-            "sample": "%d random-policy steps of oracle/game_port.py (list-of-lists, deepcopy per move, "
-                      "global random; auto-restart on game over) in %.1f s on 1 core of %s (%s)"
-                      % (steps, dt, cpu, platform.python_version())}
+    """oracle/port_bench.py: oracle/game_port.py on P processes (one per available CPU, at most
+    the box's 16-CPU share) for ~`seconds`, plus a 1-process run -- a bounded sample. Runs as a
+    child process before this process initialises the GPU."""
+    import subprocess
+    out = subprocess.run([sys.executable, "-m", "oracle.port_bench", "--seconds", str(seconds),
+                          "--single-seconds", str(max(1.0, seconds / 2))],
+                         cwd=ROOT, capture_output=True, text=True, timeout=seconds * 3 + 120)
+    if out.returncode != 0:
+        return {"error": out.stderr[-500:]}
+    return json.loads(out.stdout.strip().splitlines()[-1])
 
 
 def strong_cpu_line(seconds=2.0):
@@ -117,15 +107,16 @@ def extras(dev, seed, n_small):
     # HBM-honest: 2^26 boards (1 GiB of boards) -- far beyond the 256 MiB Infinity Cache
     big = 1 << 26
     env = VecGame(big, device=dev, seed=seed)
-    env.reset()
-    for _ in range(3):
-        env.step(None, auto_reset=True)
+    env.fill_random(7)
+    K = 200
+    el, gpu_ms = timed_steps(env, [K], 50, K, 1, dev)
     ms = kernel_events(env, 20)
-    avg = sum(ms) / len(ms)
-    out["hbm_honest"] = {"boards": big, "launches": len(ms), "kernel_ms": avg,
-                         "env_steps_per_s": big / (avg * 1e-3),
-                         "achieved_GBs": big * ALGO_BYTES / (avg * 1e-3) / 1e9,
-                         "frac_of_peak": big * ALGO_BYTES / (avg * 1e-3) / 1e9 / HBM_PEAK_GBS}
+    step_ms = gpu_ms / K
+    out["hbm_honest"] = {"boards": big, "steps": K, "step_ms_graph_replay": step_ms,
+                         "env_steps_per_s": big * K / el,
+                         "achieved_GBs": big * ALGO_BYTES / (step_ms * 1e-3) / 1e9,
+                         "frac_of_peak": big * ALGO_BYTES / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                         "single_launch_ms_eager_avg": sum(ms) / len(ms)}
     del env
     torch.cuda.empty_cache()
     # fused rollout: K steps per launch with the per-step trajectory (action, done) written
@@ -193,6 +184,32 @@ def traffic_from_profile(n_boards):
     return d.get("hbm_bytes_per_step")
 
 
+def timed_steps(env, plan, W, chunk, world, dev):
+    """W untimed warm-up steps through the same replay path (in chunks of the timed chunk
+    size, so the timed region replays graphs that have already run), then exactly sum(plan)
+    steps bracketed by barrier + synchronize. -> (slowest rank's wall seconds, device ms from
+    HIP events on the launch stream)."""
+    for c in chunks(W, chunk) if W else []:
+        env.step_n(c, auto_reset=True)
+    for c in sorted(set(plan)):
+        env.prepare_step_n(c, auto_reset=True)
+    s = torch.cuda.current_stream(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in plan]
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for (a, b), c in zip(ev, plan):
+        a.record(s)
+        env.step_n(c, auto_reset=True)
+        b.record(s)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    return max_over_ranks(t1 - t0, dev, world), sum(a.elapsed_time(b) for a, b in ev)
+
+
 def main():
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--gpus", type=int, default=1)
@@ -212,6 +229,9 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", 0))
     if world != args.gpus and not (world == 1 and args.gpus == 1):
         print("warning: --gpus %d but WORLD_SIZE=%d; using WORLD_SIZE" % (args.gpus, world), file=sys.stderr)
+    cpu_line = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu_line = cpu_baseline(args.cpu_seconds)          # before this process touches the GPU
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
@@ -222,31 +242,10 @@ def main():
     n, K, W = args.boards, args.steps, args.warmup
     offset, n = shard(rank, n)
     env = VecGame(n, device=dev, seed=args.seed, board_offset=offset)
-    env.reset()
+    env.fill_random(7)                                    # SURVEY.md 8(d) synthetic start boards
     chunk = max(1, min(args.chunk, K, 4096))
     plan = chunks(K, chunk)
-    # warm-up: W steps through the same replay path (in chunks of the timed chunk size, so the
-    # timed region replays graphs that have already run), then build any graph still missing
-    for c in chunks(W, chunk) if W else []:
-        env.step_n(c, auto_reset=True)
-    for c in sorted(set(plan)):
-        env.prepare_step_n(c, auto_reset=True)
-    s = torch.cuda.current_stream(dev)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in plan]
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for (a, b), c in zip(ev, plan):
-        a.record(s)
-        env.step_n(c, auto_reset=True)
-        b.record(s)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
-    elapsed = max_over_ranks(t1 - t0, dev, world)
-    gpu_ms = sum(a.elapsed_time(b) for a, b in ev)       # device time of the K steps (events)
+    elapsed, gpu_ms = timed_steps(env, plan, W, chunk, world, dev)
     step_ms_dev = gpu_ms / K                              # per step (all boards), device time
 
     # per-launch kernel duration (eager launches of the same kernel, HIP events per launch)
@@ -268,8 +267,9 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "int8",
-        "data": "synthetic: boards from the reference reset rule (one 2/4 tile), in-kernel uniform random "
-                "policy and spawns from Philox4x32-10, auto-reset on game over",
+        "data": "synthetic: start boards with each cell empty w.p. 1/2 else exponent ~U{1..7} (Philox, "
+                "r48_env_fill_random), in-kernel uniform random policy and spawns from Philox4x32-10, "
+                "auto-reset on game over",
         "config": {"workload": "BASELINE configs[1]: 2^20 4x4 int8 boards per GPU, random policy, env-only",
                    "boards_per_gpu": n, "global_boards": n * world, "parallelism": "env shards x%d, no collective"
                    % world, "graph_chunk": chunk},
@@ -283,10 +283,19 @@ def main():
                      "single_launch_ms_eager_events_median": kern_ms,
                      "frac_of_measured_copy_ceiling": achieved / HBM_MEASURED_GBS},
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+    if cpu_line is not None:
+        line["cpu_baseline"] = cpu_line
     if rank == 0 and world == 1 and not args.no_extras:
         ex = extras(dev, args.seed, n)
+        # median of 5 repeats of the same K-step region, and the reference
+        # reset-distribution start (one tile per board) instead of the synthetic fill
+        reps = [timed_steps(env, plan, 0, chunk, world, dev)[0] for _ in range(5)]
+        ex["repeat_5"] = {"values": [n * K / r for r in reps], "median": n * K / sorted(reps)[2]}
+        env2 = VecGame(n, device=dev, seed=args.seed, board_offset=offset)
+        env2.reset()
+        el2, _ = timed_steps(env2, plan, W, chunk, world, dev)
+        ex["reset_start"] = {"value": n * K / el2, "note": "boards start from Game.reset (one 2/4 tile)"}
+        del env2
         try:
             ex["a3c_config3"] = a3c_config3(dev, args.seed, n)
         except Exception as e:  # the env bench line must print even if the trainer fails

@@ -62,6 +62,12 @@ int r48_env_set_counters(r48_env *env, uint32_t step, uint32_t reset);
  * :102-127). mask (uint8[n], nullable = all boards) selects the boards to reset. */
 int r48_env_reset(r48_env *env, const uint8_t *mask, void *stream);
 
+/* Synthetic start boards (bench input; no reference counterpart): every cell
+ * empty w.p. 1/2, else exponent ~ U{1..max_exp} (max_exp in 1..17), from Philox keyed by
+ * (seed, global board id) -- independent of sharding and of the counters, which it leaves as
+ * they are. */
+int r48_env_fill_random(r48_env *env, uint32_t max_exp, void *stream);
+
 /* Game.reset with injected draws: rank[i] picks the blank (row-major, modulo the blank
  * count), four[i] != 0 spawns a 4 instead of a 2. */
 int r48_env_reset_with_draws(r48_env *env, const uint8_t *mask, const uint8_t *rank,

@@ -49,6 +49,7 @@ def lib():
             "orc_step_draws": (C.c_int64, [P, C.c_int64, P, P, P, P, P, P, C.c_uint32]),
             "orc_reset_philox": (None, [P, C.c_int64, C.c_uint64, C.c_int64, C.c_uint32, P]),
             "orc_score": (None, [P, C.c_int64, P]),
+            "orc_fill_random": (None, [P, C.c_int64, C.c_uint64, C.c_int64, C.c_uint32]),
             "orc_bench_pyrand": (C.c_int64, [C.c_uint64, C.c_int64]),
         }
         for name, (res, args) in sig.items():
@@ -134,6 +135,12 @@ def reset_philox(boards, seed, reset_ctr, mask=None, board_offset=0):
     b = _boards(boards).copy()
     m = None if mask is None else np.ascontiguousarray(mask, np.uint8)
     lib().orc_reset_philox(_p(b), b.shape[0], seed, board_offset, reset_ctr, _p(m))
+    return b
+
+
+def fill_random(n, seed, max_exp=7, board_offset=0):
+    b = np.zeros((n, 16), np.int8)
+    lib().orc_fill_random(_p(b), n, seed, board_offset, max_exp)
     return b
 
 

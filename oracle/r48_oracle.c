@@ -474,6 +474,27 @@ ORC_API void orc_reset_philox(int8_t *boards, int64_t n, uint64_t seed, int64_t 
     }
 }
 
+/* Synthetic start boards (r48_env_fill_random; SURVEY.md 8(d) bench input, no reference
+ * counterpart): two Philox blocks {gid lo, gid hi, j, 0xF111}, j = 0, 1, give 16 half-words,
+ * cell c takes half-word c in (block, word, low-then-high) order; odd -> tile
+ * 1 + ((h >> 1) * max_exp >> 15), even -> empty. */
+ORC_API void orc_fill_random(int8_t *boards, int64_t n, uint64_t seed, int64_t board_offset, uint32_t max_exp)
+{
+    const uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+    for (int64_t i = 0; i < n; i++) {
+        uint64_t gid = (uint64_t)(board_offset + i);
+        uint32_t w[8];
+        for (uint32_t j = 0; j < 2; j++) {
+            uint32_t ctr[4] = {(uint32_t)gid, (uint32_t)(gid >> 32), j, 0xF111u};
+            orc_philox4x32_10(ctr, key, w + 4 * j);
+        }
+        for (int c = 0; c < 16; c++) {
+            uint32_t h = (c & 1) ? (w[c >> 1] >> 16) : (w[c >> 1] & 0xFFFFu);
+            boards[16 * i + c] = (h & 1u) ? (int8_t)(1u + (((h >> 1) * max_exp) >> 15)) : 0;
+        }
+    }
+}
+
 /* Tile-value sum per board: main.py:48's np.sum(state_matrix). */
 ORC_API void orc_score(const int8_t *boards, int64_t n, int32_t *out)
 {

@@ -271,6 +271,7 @@ R48_HD void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1)
 // Draw-word contract (DESIGN.md "Philox mode"; restated in oracle/r48_oracle.c)
 static constexpr uint32_t kStepTag = 0x2048u;
 static constexpr uint32_t kResetTag = 0x5E7u;
+static constexpr uint32_t kFillTag = 0xF111u;   // synthetic start boards (r48_env_fill_random)
 static constexpr uint32_t kFourThresh = 0x1999999Au;     // P(4) = 0.1   (GameClient.py:125)
 static constexpr uint32_t kFourThresh28 = 0x0199999Au;   // same on 28 bits
 

@@ -251,6 +251,36 @@ __global__ __launch_bounds__(kBlock) void k_reset_draws(int8_t *__restrict__ boa
     store_board(boards, i, b);
 }
 
+// ---------------------------------------------------------------- synthetic start boards
+// SURVEY.md 8(d) bench input: each cell empty w.p. 1/2, else e ~ U{1..max_exp}. Two Philox
+// blocks per board (counter {gid lo, gid hi, j, kFillTag}, j = 0, 1) give 16 half-words; cell c
+// reads half-word h = block c>>3, word (c>>1)&3, half c&1 (low first): empty iff !(h & 1), else
+// e = 1 + (((h >> 1) * max_exp) >> 15).
+__global__ __launch_bounds__(kBlock) void k_fill_random(int8_t *__restrict__ boards, int64_t n, int64_t gid0,
+                                                        uint32_t k0, uint32_t k1, uint32_t max_exp)
+{
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n)
+        return;
+    uint32_t w[8];
+    philox_words(w, (uint64_t)(gid0 + i), 0u, r48::kFillTag, k0, k1);
+    philox_words(w + 4, (uint64_t)(gid0 + i), 1u, r48::kFillTag, k0, k1);
+    uint32_t row[4];
+    R48_UNROLL
+    for (int r = 0; r < 4; ++r) {
+        uint32_t word = 0;
+        R48_UNROLL
+        for (int k = 0; k < 4; ++k) {
+            const int c = 4 * r + k;
+            const uint32_t h = (w[4 * (c >> 3) + ((c >> 1) & 3)] >> (16 * (c & 1))) & 0xFFFFu;
+            const uint32_t e = (h & 1u) ? 1u + (((h >> 1) * max_exp) >> 15) : 0u;
+            word |= e << (8 * k);
+        }
+        row[r] = word;
+    }
+    store_board(boards, i, Board{row[0], row[1], row[2], row[3]});
+}
+
 // ---------------------------------------------------------------- rollout (K steps in registers)
 __global__ __launch_bounds__(kBlock) void k_rollout(int8_t *__restrict__ boards, int64_t n, int64_t gid0,
                                                     uint32_t k0, uint32_t k1, uint32_t step0, int32_t n_steps,
@@ -580,6 +610,18 @@ int r48_env_reset(r48_env *env, const uint8_t *mask, void *stream)
                        env->gid0, (uint32_t)env->seed, (uint32_t)(env->seed >> 32), env->reset_ctr, mask);
     env->reset_ctr++;
     return launched("k_reset");
+}
+
+int r48_env_fill_random(r48_env *env, uint32_t max_exp, void *stream)
+{
+    if (int s = check_env(env))
+        return s;
+    if (max_exp < 1 || max_exp > 17)
+        return fail(R48_EINVAL, "max_exp must be in 1..17");
+    DeviceGuard g(env->device);
+    hipLaunchKernelGGL(k_fill_random, grid_for(env->n), dim3(kBlock), 0, (hipStream_t)stream, env->boards,
+                       env->n, env->gid0, (uint32_t)env->seed, (uint32_t)(env->seed >> 32), max_exp);
+    return launched("k_fill_random");
 }
 
 int r48_env_reset_with_draws(r48_env *env, const uint8_t *mask, const uint8_t *rank, const uint8_t *four,

@@ -106,6 +106,12 @@ class VecGame:
         check(self._lib.r48_env_reset_with_draws(self._env, ptr(mask), ptr(rank), ptr(four), self._s()))
         return self.boards
 
+    def fill_random(self, max_exp=7):
+        """Synthetic start boards (SURVEY.md 8(d) bench input): each cell empty w.p. 1/2, else
+        exponent ~ U{1..max_exp}, Philox keyed by (seed, global board id). Counters unchanged."""
+        check(self._lib.r48_env_fill_random(self._env, int(max_exp), self._s()))
+        return self.boards
+
     # ------------------------------------------------------------------ step
     def step(self, actions=None, auto_reset=False, merge_reward=False, want_changed=False, score=None):
         """Game.step (GameClient.py:40-51) for every board.

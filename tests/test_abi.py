@@ -48,6 +48,7 @@ def test_argument_errors_without_gpu():
     assert lib.r48_env_bind_boards(None, None) == _lib.R48_EINVAL
     assert lib.r48_env_step(None, None, 0, None, None, None, None, None) == _lib.R48_EINVAL
     assert lib.r48_values_check(None, 1, 4, 4, None, None, None) == _lib.R48_EINVAL
+    assert lib.r48_env_fill_random(None, 7, None) == _lib.R48_EINVAL
     assert lib.r48_values_move(None, None, 1, None, None, None) == _lib.R48_EINVAL
     assert lib.r48_env_destroy(None) == _lib.R48_OK
     with pytest.raises(_lib.Rein48Error):

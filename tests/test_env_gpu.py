@@ -280,6 +280,24 @@ def test_reset_matches_oracle():
     assert v.counters == (0, 2)
 
 
+@pytest.mark.parametrize("max_exp", [7, 17])
+def test_fill_random_matches_oracle(max_exp):
+    """Synthetic start boards: bit-exact vs the oracle, independent of the
+    shard split (board_offset), counters untouched, then a step runs from them."""
+    n, seed = 50_001, 0x20485EED
+    v = vec(n, seed=seed, offset=123)
+    v.fill_random(max_exp)
+    want = O.fill_random(n, seed, max_exp, board_offset=123)
+    assert np.array_equal(host(v.boards), want)
+    lo = vec(1000, seed=seed, offset=123 + 20_000)
+    lo.fill_random(max_exp)
+    assert np.array_equal(host(lo.boards), want[20_000:21_000])
+    assert v.counters == (0, 0)
+    assert abs((want == 0).mean() - 0.5) < 0.01 and want.max() == max_exp and want[want > 0].min() == 1
+    with pytest.raises(Exception):
+        v.fill_random(0)
+
+
 def test_rollout_equals_repeated_steps():
     n, K, seed = 30_000, 37, 4242
     rng = np.random.default_rng(3)

@@ -138,3 +138,15 @@ def test_philox_mode_matches_reference_fingerprint(golden):
 def test_oracle_rejects_bad_action():
     with pytest.raises(ValueError):
         O.move(np.zeros(16, np.int8), 7)
+
+
+def test_fill_random_distribution():
+    """Synthetic bench boards (no reference counterpart -- statistics only):
+    cells empty w.p. 1/2, tiles uniform over 1..max_exp, shard-independent."""
+    b = O.fill_random(200_000, 0x20485EED, 7)
+    assert abs((b == 0).mean() - 0.5) < 0.003
+    counts = np.bincount(b[b > 0].astype(np.int64), minlength=8)[1:]
+    exp = counts.sum() / 7
+    chi2 = float(((counts - exp) ** 2 / exp).sum())
+    assert chi2 < 30, chi2                        # 6 dof; p ~ 4e-5
+    assert np.array_equal(O.fill_random(100, 0x20485EED, 7, board_offset=5000), b[5000:5100])
