@@ -186,6 +186,46 @@ int r48_cnn_policy_forward(const int8_t *boards, int64_t n, const void *wfrag, c
                            int32_t mode, float *logits, float *value, int8_t *actions, uint64_t seed,
                            int64_t gid0, uint32_t ctr, void *stream);
 
+/* ---- Transition store for replay-based training (config 5; algorithm/ddpg/replay.py) ----
+ * HBM-resident, structure of arrays, 38 B per transition: state int8[16], action int8,
+ * reward float, next_state int8[16], done uint8. State pointers must be 16-byte aligned. */
+typedef struct r48_replay r48_replay;
+#define R48_REPLAY_RING 0u        /* overwrite the oldest; sample uniformly WITH replacement */
+#define R48_REPLAY_FILL_DRAIN 1u  /* Replay (replay.py:8-47): store drops once max_size is held
+                                   * (:18-21); sample = random.sample WITHOUT replacement (a
+                                   * permutation when batch == size), or the whole buffer in
+                                   * insertion order if batch > size (:23-34),
+                                   * then clear() (:26, :45-47) */
+
+/* Replay.__init__(replay_size) (replay.py:10-13): `capacity` slots on `device`. Draws are
+ * Philox4x32-10 keyed by `seed` with a per-sample counter. */
+int r48_replay_create(r48_replay **out, int device, int64_t capacity, uint32_t mode, uint64_t seed);
+int r48_replay_destroy(r48_replay *rep);
+int64_t r48_replay_capacity(const r48_replay *rep);
+/* cur_size (replay.py:12), the ring's next slot, the sample counter (checkpoint/resume). */
+int r48_replay_get_counters(const r48_replay *rep, int64_t *size, int64_t *head, uint32_t *sample_ctr);
+int r48_replay_set_counters(r48_replay *rep, int64_t size, int64_t head, uint32_t sample_ctr);
+/* Device planes, for zero-copy readers: state/next_state [capacity][16], action, reward, done. */
+int r48_replay_planes(const r48_replay *rep, int8_t **state, int8_t **action, float **reward,
+                      int8_t **next_state, uint8_t **done);
+/* Replay.clear (replay.py:45-47). */
+int r48_replay_clear(r48_replay *rep);
+/* Replay.store (replay.py:18-21) for n transitions at once (device arrays; reward and done
+ * nullable = 0). *stored = how many were kept (FILL_DRAIN drops past capacity; RING keeps the
+ * newest min(n, capacity)). */
+int r48_replay_store(r48_replay *rep, const int8_t *state, const int8_t *action, const float *reward,
+                     const int8_t *next_state, const uint8_t *done, int64_t n, int64_t *stored,
+                     void *stream);
+/* Replay.sample (replay.py:23-27) into device arrays of `batch` rows (each nullable; index =
+ * the slot of each row). *count = rows written (FILL_DRAIN: min(batch, size)). */
+int r48_replay_sample(r48_replay *rep, int64_t batch, int8_t *state, int8_t *action, float *reward,
+                      int8_t *next_state, uint8_t *done, int64_t *index, int64_t *count, void *stream);
+/* Gather the given slots (index int64[n], each in [0, size)); out-of-range indices produce
+ * zero rows and are counted in r48_replay_error_count. */
+int r48_replay_gather(r48_replay *rep, const int64_t *index, int64_t n, int8_t *state, int8_t *action,
+                      float *reward, int8_t *next_state, uint8_t *done, void *stream);
+int r48_replay_error_count(const r48_replay *rep, uint64_t *count);
+
 /* Thread-local message of the last failed call on this thread ("" if none). */
 const char *r48_last_error(void);
 /* "rein48 <version> gfx950" */

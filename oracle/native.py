@@ -50,6 +50,8 @@ def lib():
             "orc_reset_philox": (None, [P, C.c_int64, C.c_uint64, C.c_int64, C.c_uint32, P]),
             "orc_score": (None, [P, C.c_int64, P]),
             "orc_fill_random": (None, [P, C.c_int64, C.c_uint64, C.c_int64, C.c_uint32]),
+            "orc_replay_ring_index": (None, [C.c_uint64, C.c_uint32, C.c_int64, C.c_int64, P]),
+            "orc_replay_perm_index": (None, [C.c_uint64, C.c_uint32, C.c_int64, C.c_int64, P]),
             "orc_bench_pyrand": (C.c_int64, [C.c_uint64, C.c_int64]),
         }
         for name, (res, args) in sig.items():
@@ -142,6 +144,15 @@ def fill_random(n, seed, max_exp=7, board_offset=0):
     b = np.zeros((n, 16), np.int8)
     lib().orc_fill_random(_p(b), n, seed, board_offset, max_exp)
     return b
+
+
+def replay_index(seed, sample_ctr, size, n, ring=True):
+    """Slots drawn by r48_replay_sample: ring (uniform, with replacement) or fill-drain
+    (Feistel permutation, without replacement; n <= size)."""
+    out = np.zeros(n, np.int64)
+    f = lib().orc_replay_ring_index if ring else lib().orc_replay_perm_index
+    f(seed, sample_ctr, size, n, _p(out))
+    return out
 
 
 def score(boards):

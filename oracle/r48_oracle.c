@@ -495,6 +495,53 @@ ORC_API void orc_fill_random(int8_t *boards, int64_t n, uint64_t seed, int64_t b
     }
 }
 
+/* Replay sampling draws (rein48_amd/csrc/r48_replay.hip). Ring: uniform with replacement,
+ * index = mulhi64(w0 | w1 << 32, size), counter {i lo, i hi, sample_ctr, 0x5A4}. */
+ORC_API void orc_replay_ring_index(uint64_t seed, uint32_t sample_ctr, int64_t size, int64_t n, int64_t *out)
+{
+    const uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+    for (int64_t i = 0; i < n; i++) {
+        uint32_t ctr[4] = {(uint32_t)i, (uint32_t)((uint64_t)i >> 32), sample_ctr, 0x5A4u}, w[4];
+        orc_philox4x32_10(ctr, key, w);
+        const uint64_t u = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+        out[i] = (int64_t)(((unsigned __int128)u * (uint64_t)size) >> 64);
+    }
+}
+
+/* Fill-drain sampling without replacement (replay.py:34's random.sample, restated with a keyed
+ * permutation): a 4-round balanced Feistel network on 2h bits (h = ceil(ceil(log2 size) / 2),
+ * h >= 1), round j: (L, R) -> (R, L ^ (Philox({R, sample_ctr, j, 0x5A3}).w0 & (2^h - 1))),
+ * cycle-walked until the value is < size. Row i < n (n <= size) takes slot perm(i). */
+static uint64_t orc_feistel(uint64_t x, uint32_t h, uint32_t ctr, const uint32_t key[2])
+{
+    const uint64_t mask = (1ull << h) - 1ull;
+    uint64_t L = x >> h, R = x & mask;
+    for (uint32_t j = 0; j < 4; j++) {
+        uint32_t c[4] = {(uint32_t)R, ctr, j, 0x5A3u}, w[4];
+        orc_philox4x32_10(c, key, w);
+        const uint64_t nl = R;
+        R = L ^ ((uint64_t)w[0] & mask);
+        L = nl;
+    }
+    return (L << h) | R;
+}
+
+ORC_API void orc_replay_perm_index(uint64_t seed, uint32_t sample_ctr, int64_t size, int64_t n, int64_t *out)
+{
+    const uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+    uint32_t k = 1;
+    while (k < 63 && ((int64_t)1 << k) < size)
+        k++;
+    const uint32_t h = (k + 1) / 2;
+    for (int64_t i = 0; i < n; i++) {
+        uint64_t x = (uint64_t)i;
+        do
+            x = orc_feistel(x, h, sample_ctr, key);
+        while (x >= (uint64_t)size);
+        out[i] = (int64_t)x;
+    }
+}
+
 /* Tile-value sum per board: main.py:48's np.sum(state_matrix). */
 ORC_API void orc_score(const int8_t *boards, int64_t n, int32_t *out)
 {

@@ -20,10 +20,23 @@ R48_OK, R48_EINVAL, R48_EHIP, R48_ENOMEM = 0, -1, -2, -3
 AUTO_RESET, RANDOM_POLICY, MERGE_REWARD = 1, 2, 4
 FEAT_VALUES, FEAT_EXPONENTS = 0, 1
 F32, BF16 = 0, 1
+REPLAY_RING, REPLAY_FILL_DRAIN = 0, 1
 
 # name -> (restype, argtypes); mirrors include/rein48.h one to one
 _P, _I32, _I64, _U32, _U64 = C.c_void_p, C.c_int32, C.c_int64, C.c_uint32, C.c_uint64
 SIGNATURES = {
+    "r48_replay_create": (C.c_int, [C.POINTER(_P), C.c_int, _I64, _U32, _U64]),
+    "r48_replay_destroy": (C.c_int, [_P]),
+    "r48_replay_capacity": (_I64, [_P]),
+    "r48_replay_get_counters": (C.c_int, [_P, C.POINTER(_I64), C.POINTER(_I64), C.POINTER(_U32)]),
+    "r48_replay_set_counters": (C.c_int, [_P, _I64, _I64, _U32]),
+    "r48_replay_planes": (C.c_int, [_P, C.POINTER(_P), C.POINTER(_P), C.POINTER(_P), C.POINTER(_P),
+                                    C.POINTER(_P)]),
+    "r48_replay_clear": (C.c_int, [_P]),
+    "r48_replay_store": (C.c_int, [_P, _P, _P, _P, _P, _P, _I64, C.POINTER(_I64), _P]),
+    "r48_replay_sample": (C.c_int, [_P, _I64, _P, _P, _P, _P, _P, _P, C.POINTER(_I64), _P]),
+    "r48_replay_gather": (C.c_int, [_P, _P, _I64, _P, _P, _P, _P, _P, _P]),
+    "r48_replay_error_count": (C.c_int, [_P, C.POINTER(_U64)]),
     "r48_env_create": (C.c_int, [C.POINTER(_P), C.c_int, _I64, _U64, _I64]),
     "r48_env_destroy": (C.c_int, [_P]),
     "r48_env_bind_boards": (C.c_int, [_P, _P]),

@@ -83,8 +83,14 @@ def main():
         for name, fmt in (("conv NCHW", torch.contiguous_format), ("conv channels_last", torch.channels_last)):
             n2 = net.to(memory_format=fmt)
             xx = x.contiguous(memory_format=fmt)
-            ms = timeit(lambda: [n2(xx[i:i + chunk]) for i in range(0, B, chunk)], reps=3)
-            print("%-22s fwd 2^21: %8.2f ms  %7.1f TFLOP/s useful" % (name, ms, fl * B / ms / 1e9))
+            for ck in (1 << 16, 1 << 14):
+                try:
+                    ms = timeit(lambda: [n2(xx[i:i + ck]) for i in range(0, B, ck)], reps=3)
+                    print("%-22s fwd 2^21 (chunks 2^%d): %8.2f ms  %7.1f TFLOP/s useful"
+                          % (name, ck.bit_length() - 1, ms, fl * B / ms / 1e9), flush=True)
+                    break
+                except RuntimeError as e:
+                    print("%-22s chunk 2^%d failed: %s" % (name, ck.bit_length() - 1, str(e)[:80]), flush=True)
         mats = ((dense_of(net.stem), net.stem.bias.repeat(16)),
                 [(dense_of(c), c.bias.repeat(16)) for c in net.convs])
         xp = torch.randn(B, 16 * IN, device=DEV, dtype=torch.bfloat16)
@@ -103,7 +109,11 @@ def main():
     def fb():
         n2.zero_grad(set_to_none=True)
         n2(xt).float().square().mean().backward()
-    ms = timeit(fb, reps=5)
+    try:
+        ms = timeit(fb, reps=5)
+    except RuntimeError as e:
+        print("fwd+bwd failed", str(e)[:80])
+        return
     print("conv channels_last fwd+bwd 2^16: %.2f ms  %.1f TFLOP/s useful (3x fwd)" % (ms, 3 * fl * Bt / ms / 1e9))
 
 
