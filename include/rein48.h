@@ -226,6 +226,22 @@ int r48_replay_gather(r48_replay *rep, const int64_t *index, int64_t n, int8_t *
                       float *reward, int8_t *next_state, uint8_t *done, void *stream);
 int r48_replay_error_count(const r48_replay *rep, uint64_t *count);
 
+/* ---- Value-based training around the env (config 5: ResNet-10 Q-network + replay) ----
+ * No reference code exists for these (README.md:15-17 names ResNet + BN + ReLU for 2048; the
+ * only replay anchor is algorithm/ddpg/replay.py). */
+/* One-hot input planes: out[n][16][18] (position-major, plane e = exponent 0..17), f32/bf16. */
+int r48_board_onehot(const int8_t *boards, int64_t n, int32_t out_dtype, void *out, void *stream);
+/* Epsilon-greedy over q float[n][4] (16-byte aligned): Philox4x32-10(key = seed, counter =
+ * {gid lo, gid hi, ctr, 0xD0E}), u = (w0 >> 8) / 2^24; u < eps -> action w1 >> 30, else the
+ * first argmax. */
+int r48_egreedy_actions(const float *q, int64_t n, float eps, uint64_t seed, int64_t gid0, uint32_t ctr,
+                        int8_t *actions, void *stream);
+/* TD target y[i] = reward[i] + gamma * (1 - done[i]) * q_next_target[i][a*], a* = argmax of
+ * q_next_online[i] (double DQN) or of q_next_target[i] when q_next_online is NULL. done
+ * nullable (= 0). Q arrays float[n][4], 16-byte aligned. */
+int r48_td_target(const float *reward, const uint8_t *done, const float *q_next_target,
+                  const float *q_next_online, int64_t n, float gamma, float *y, void *stream);
+
 /* Thread-local message of the last failed call on this thread ("" if none). */
 const char *r48_last_error(void);
 /* "rein48 <version> gfx950" */

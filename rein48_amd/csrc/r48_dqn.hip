@@ -1,0 +1,161 @@
+// r48_dqn.hip -- gfx950 kernels around the env step for value-based training (BASELINE
+// config 5: ResNet-10 Q-network, DQN replay resident in HBM), behind include/rein48.h.
+//
+//   k_onehot    board int8[16] -> bf16/f32 [16 positions][18 planes] one-hot of the exponent
+//               (e = 0..17; the largest tile a 4x4 board can hold is 2^17). Position-major,
+//               plane-minor: the layout the structured-GEMM stem and the fused kernel read.
+//   k_egreedy   epsilon-greedy over Q float[n][4]: u < eps -> uniform action, else the first
+//               argmax (np.argmax tie rule). Philox4x32-10(key = seed, counter = {gid lo,
+//               gid hi, ctr, 0xD0E}): u = (w0 >> 8) / 2^24, random action = w1 >> 30.
+//   k_td_target y = r + gamma * (1 - done) * Q'(s', a*), a* = argmax_a Q'(s') (DQN) or
+//               argmax_a Q(s') of the online net (double DQN); fp32.
+// All are memory-bound one-row-per-lane kernels.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+
+#include "../../include/rein48.h"
+#include "r48_board.h"
+
+namespace r48 {
+void set_last_error(const std::string &msg);
+}
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr uint32_t kEgreedyTag = 0xD0Eu;
+constexpr int kPlanes = 18;
+
+inline dim3 grid_for(int64_t n) { return dim3((unsigned)((n + kBlock - 1) / kBlock)); }
+
+int fail(int code, const char *msg)
+{
+    r48::set_last_error(msg);
+    return code;
+}
+
+int launched(const char *what)
+{
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        r48::set_last_error(std::string(what) + ": " + hipGetErrorString(e));
+        return R48_EHIP;
+    }
+    return R48_OK;
+}
+
+// one lane per (board, position): writes 18 values (36 B bf16 / 72 B f32)
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_onehot(const int8_t *__restrict__ boards, int64_t n_cells,
+                                                   T *__restrict__ out)
+{
+    const int64_t c = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (c >= n_cells)
+        return;
+    const uint32_t e = (uint32_t)(uint8_t)boards[c];
+    T *o = out + kPlanes * c;
+#pragma unroll
+    for (int k = 0; k < kPlanes; ++k)
+        o[k] = (T)(e == (uint32_t)k ? 1.0f : 0.0f);
+}
+
+__device__ __forceinline__ uint32_t argmax4(float4 q)
+{
+    uint32_t a = 0;
+    float m = q.x;
+    if (q.y > m) { m = q.y; a = 1; }
+    if (q.z > m) { m = q.z; a = 2; }
+    if (q.w > m) { a = 3; }
+    return a;
+}
+
+__device__ __forceinline__ float pick(float4 q, uint32_t a)
+{
+    return a == 0 ? q.x : a == 1 ? q.y : a == 2 ? q.z : q.w;
+}
+
+__global__ __launch_bounds__(kBlock) void k_egreedy(const float *__restrict__ q, int64_t n, float eps, uint32_t k0,
+                                                    uint32_t k1, int64_t gid0, uint32_t ctr,
+                                                    int8_t *__restrict__ actions)
+{
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n)
+        return;
+    const uint64_t gid = (uint64_t)(gid0 + i);
+    uint32_t w[4] = {(uint32_t)gid, (uint32_t)(gid >> 32), ctr, kEgreedyTag};
+    r48::philox4x32_10(w, k0, k1);
+    const float u = (float)(w[0] >> 8) * (1.0f / 16777216.0f);
+    const float4 qv = reinterpret_cast<const float4 *>(q)[i];
+    actions[i] = (int8_t)(u < eps ? (w[1] >> 30) : argmax4(qv));
+}
+
+template <bool DOUBLE>
+__global__ __launch_bounds__(kBlock) void k_td_target(const float *__restrict__ reward,
+                                                      const uint8_t *__restrict__ done,
+                                                      const float *__restrict__ q_next_target,
+                                                      const float *__restrict__ q_next_online, int64_t n,
+                                                      float gamma, float *__restrict__ y)
+{
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n)
+        return;
+    const float4 qt = reinterpret_cast<const float4 *>(q_next_target)[i];
+    const uint32_t a = DOUBLE ? argmax4(reinterpret_cast<const float4 *>(q_next_online)[i]) : argmax4(qt);
+    const float boot = (done && done[i]) ? 0.0f : pick(qt, a);
+    y[i] = reward[i] + gamma * boot;
+}
+
+bool aligned16(const void *p) { return ((uintptr_t)p & 15u) == 0; }
+
+}  // namespace
+
+extern "C" {
+
+int r48_board_onehot(const int8_t *boards, int64_t n, int32_t out_dtype, void *out, void *stream)
+{
+    if (!boards || !out || n < 0 || (out_dtype != R48_F32 && out_dtype != R48_BF16))
+        return fail(R48_EINVAL, "boards/out NULL, n < 0 or bad dtype");
+    if (n == 0)
+        return R48_OK;
+    const int64_t cells = 16 * n;
+    if (out_dtype == R48_F32)
+        hipLaunchKernelGGL(k_onehot<float>, grid_for(cells), dim3(kBlock), 0, (hipStream_t)stream, boards, cells,
+                           (float *)out);
+    else
+        hipLaunchKernelGGL(k_onehot<__bf16>, grid_for(cells), dim3(kBlock), 0, (hipStream_t)stream, boards, cells,
+                           (__bf16 *)out);
+    return launched("k_onehot");
+}
+
+int r48_egreedy_actions(const float *q, int64_t n, float eps, uint64_t seed, int64_t gid0, uint32_t ctr,
+                        int8_t *actions, void *stream)
+{
+    if (!q || !actions || n < 0 || gid0 < 0 || !aligned16(q))
+        return fail(R48_EINVAL, "q/actions NULL, q not 16-byte aligned, n < 0 or gid0 < 0");
+    if (n == 0)
+        return R48_OK;
+    hipLaunchKernelGGL(k_egreedy, grid_for(n), dim3(kBlock), 0, (hipStream_t)stream, q, n, eps, (uint32_t)seed,
+                       (uint32_t)(seed >> 32), gid0, ctr, actions);
+    return launched("k_egreedy");
+}
+
+int r48_td_target(const float *reward, const uint8_t *done, const float *q_next_target,
+                  const float *q_next_online, int64_t n, float gamma, float *y, void *stream)
+{
+    if (!reward || !q_next_target || !y || n < 0 || !aligned16(q_next_target) ||
+        (q_next_online && !aligned16(q_next_online)))
+        return fail(R48_EINVAL, "reward/q_next_target/y NULL, n < 0 or Q not 16-byte aligned");
+    if (n == 0)
+        return R48_OK;
+    if (q_next_online)
+        hipLaunchKernelGGL(k_td_target<true>, grid_for(n), dim3(kBlock), 0, (hipStream_t)stream, reward, done,
+                           q_next_target, q_next_online, n, gamma, y);
+    else
+        hipLaunchKernelGGL(k_td_target<false>, grid_for(n), dim3(kBlock), 0, (hipStream_t)stream, reward, done,
+                           q_next_target, nullptr, n, gamma, y);
+    return launched("k_td_target");
+}
+
+}  // extern "C"

@@ -1,0 +1,115 @@
+"""ResNet-10 Q-network for 4x4 boards (BASELINE config 5), PyTorch-ROCm.
+
+No reference code exists for it: README.md:15-17 proposes a ResNet with ReLU and Batch
+Normalization as the 2048 feature extractor, and BASELINE config 5 names "ResNet-10 policy bf16".
+Architecture (10 weight layers):
+    input  18 one-hot exponent planes on the 4x4 grid (r48_board_onehot)
+    stem   conv3x3 (pad 1) 18 -> C, BN, ReLU
+    4 x BasicBlock: conv3x3 C -> C, BN, ReLU, conv3x3 C -> C, BN, + identity, ReLU
+    head   Linear(16 C -> 4): one Q-value per action (0 UP, 1 DOWN, 2 LEFT, 3 RIGHT)
+with C = 64 and no downsampling (the grid is only 4x4).
+
+MI355X layout: activations are [B, 16 * C] (position-major, channel-minor) and every 3x3
+convolution on the 4x4 grid is ONE structured dense GEMM [B, 16 C_in] x [16 C_in, 16 C_out]^T
+whose weight is scattered (differentiably) from the conv kernel: 100 of the 144 (position,
+tap) pairs are inside the grid, so the dense GEMM does 2.56x the useful FLOPs but runs as one
+large hipBLASLt bf16 MFMA GEMM per layer with M = boards. At 2^21 boards it measured 2x
+MIOpen's channels-last conv (tools/exp_resnet.py; MIOpen also rejects batches >= 2^18 on 4x4
+inputs). BatchNorm is per channel over (boards x positions), computed in fp32.
+forward(x [B, 16*18]) -> Q [B, 4] (fp32).
+"""
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..a3c.nets import linear
+from .kernels import PLANES
+
+_MAPS = {}
+
+
+def conv_scatter_map(co, ci, device):
+    """(rows, cols, src) index lists placing a [co, ci, 3, 3] kernel into the [16 co, 16 ci]
+    dense matrix of a pad-1 3x3 conv on the 4x4 grid."""
+    key = (co, ci, str(device))
+    if key not in _MAPS:
+        rows, cols, src = [], [], []
+        o = torch.arange(co).view(-1, 1).expand(co, ci).reshape(-1)
+        i = torch.arange(ci).view(1, -1).expand(co, ci).reshape(-1)
+        for p in range(16):
+            r, c = divmod(p, 4)
+            for dr in (-1, 0, 1):
+                for dc in (-1, 0, 1):
+                    rr, cc = r + dr, c + dc
+                    if 0 <= rr < 4 and 0 <= cc < 4:
+                        q = 4 * rr + cc
+                        rows.append(p * co + o)
+                        cols.append(q * ci + i)
+                        src.append(((o * ci + i) * 3 + (dr + 1)) * 3 + (dc + 1))
+        _MAPS[key] = tuple(torch.cat(t).to(device) for t in (rows, cols, src))
+    return _MAPS[key]
+
+
+def dense_conv_weight(conv):
+    """[16 co, 16 ci] structured matrix of a Conv2d(ci, co, 3, padding=1) on the 4x4 grid."""
+    w = conv.weight
+    co, ci = w.shape[:2]
+    r, c, k = conv_scatter_map(co, ci, w.device)
+    d = torch.zeros(16 * co, 16 * ci, dtype=w.dtype, device=w.device)
+    return d.index_put((r, c), w.reshape(-1)[k])
+
+
+class ResNet10Q(nn.Module):
+    def __init__(self, channels=64, blocks=4, bn=True, dtype=torch.float32):
+        super().__init__()
+        self.dtype = dtype
+        self.channels, self.n_blocks, self.use_bn = channels, blocks, bn
+        C = channels
+        self.stem = nn.Conv2d(PLANES, C, 3, padding=1)
+        self.convs = nn.ModuleList([nn.Conv2d(C, C, 3, padding=1) for _ in range(2 * blocks)])
+        self.bns = nn.ModuleList([nn.BatchNorm1d(C) for _ in range(1 + 2 * blocks)]) if bn else None
+        self.head = nn.Linear(16 * C, 4)
+        for m in [self.stem, *self.convs]:
+            nn.init.kaiming_normal_(m.weight, nonlinearity="relu")
+            nn.init.zeros_(m.bias)
+        nn.init.normal_(self.head.weight, std=1e-2)
+        nn.init.zeros_(self.head.bias)
+
+    def conv_layers(self):
+        return [self.stem, *self.convs]
+
+    def _bn(self, k, h):
+        if not self.use_bn:
+            return h
+        B = h.shape[0]
+        bn = self.bns[k]
+        y = bn(h.to(bn.weight.dtype).reshape(B * 16, self.channels))      # fp32 (fp64 in tests)
+        return y.view(B, 16 * self.channels)
+
+    def _conv(self, conv, h):
+        return linear(h, dense_conv_weight(conv), conv.bias.repeat(16), self.dtype)
+
+    def forward(self, x):
+        d = self.dtype
+        h = F.relu(self._bn(0, self._conv(self.stem, x))).to(d)
+        for b in range(self.n_blocks):
+            c1, c2 = self.convs[2 * b], self.convs[2 * b + 1]
+            y = F.relu(self._bn(1 + 2 * b, self._conv(c1, h))).to(d)
+            z = self._bn(2 + 2 * b, self._conv(c2, y))
+            h = F.relu(z + h.to(z.dtype)).to(d)
+        return linear(h, self.head.weight, self.head.bias, d).float()
+
+    @torch.no_grad()
+    def folded(self):
+        """Inference weights with eval-mode BN folded into each conv: list of (w [co, ci, 3, 3],
+        b [co]) for the 9 convs, plus (head w [4, 16 C], head b [4]); fp32."""
+        out = []
+        for k, conv in enumerate(self.conv_layers()):
+            w, b = conv.weight.float(), conv.bias.float()
+            if self.use_bn:
+                bn = self.bns[k]
+                s = bn.weight.float() / torch.sqrt(bn.running_var.float() + bn.eps)
+                w = w * s.view(-1, 1, 1, 1)
+                b = (b - bn.running_mean.float()) * s + bn.bias.float()
+            out.append((w.contiguous(), b.contiguous()))
+        return out, (self.head.weight.float().contiguous(), self.head.bias.float().contiguous())

@@ -1,0 +1,176 @@
+"""DQN around the vectorized env with an HBM-resident replay ring (BASELINE config 5).
+
+No reference trainer exists (the reference's value-based code is the unfinished DDPG under
+algorithm/ddpg/; its replay buffer, replay.py, is what ReplayStore's fill_drain mode restates).
+One train_step per env step, per GPU:
+  act      Q = ResNet10Q(onehot(boards)) in eval mode (bf16 MFMA GEMMs), epsilon-greedy
+           (r48_egreedy_actions, Philox keyed by global board id)
+  step     r48_env_step with the opt-in merge reward (the reference reward is always 0,
+           GameClient.py:138, which gives a value learner nothing to learn) and auto-reset
+  store    (s, a, r, s', done) of every board into the ring (r48_replay_store; 38 B each).
+           For a done board s' is the auto-reset board: the target masks it, (1 - done)
+  update   `updates_per_step` minibatches sampled uniformly from the ring, TD target from the
+           target net (double DQN by default; r48_td_target), Huber loss, ONE all-reduce of
+           the flat fp32 gradient across GPUs (RCCL), Adam; target net synced every
+           `target_sync` updates
+Rewards enter the loss as log2(1 + merged value) (reward_transform="log2") or raw.
+Each rank owns boards [rank*N, (rank+1)*N) and its own ring shard; no replay traffic crosses
+GPUs.
+"""
+import copy
+import math
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+import torch.nn.functional as F
+
+from ..a3c.optim import FlatParams
+from ..env import VecGame
+from ..replay import ReplayStore
+from .kernels import board_onehot, egreedy_actions, td_target
+from .nets import ResNet10Q
+
+
+@dataclass
+class DQNConfig:
+    n_boards: int = 4096             # boards per GPU
+    replay_capacity: int = 1 << 20   # transitions per GPU (38 B each)
+    batch: int = 4096                # minibatch per GPU per update
+    updates_per_step: int = 1
+    learn_start: int = 16384         # transitions held before the first update
+    gamma: float = 0.99
+    lr: float = 1e-4
+    eps_start: float = 1.0
+    eps_end: float = 0.05
+    eps_decay_steps: int = 1000
+    target_sync: int = 250
+    double: bool = True
+    reward_transform: str = "log2"
+    channels: int = 64
+    blocks: int = 4
+    bn: bool = True
+    bf16: bool = True
+    act_chunk: int = 1 << 18         # boards per Q forward while acting
+    seed: int = 0
+
+
+class Adam:
+    """torch.optim.Adam semantics over one flat fp32 buffer (bias-corrected, eps outside sqrt)."""
+
+    def __init__(self, flat, lr, betas=(0.9, 0.999), eps=1e-8):
+        self.flat, self.lr, self.b1, self.b2, self.eps = flat, lr, betas[0], betas[1], eps
+        self.m = torch.zeros_like(flat.data)
+        self.v = torch.zeros_like(flat.data)
+        self.t = 0
+
+    @torch.no_grad()
+    def step(self):
+        self.t += 1
+        g = self.flat.grad
+        self.m.mul_(self.b1).add_(g, alpha=1 - self.b1)
+        self.v.mul_(self.b2).addcmul_(g, g, value=1 - self.b2)
+        c1, c2 = 1 - self.b1 ** self.t, 1 - self.b2 ** self.t
+        denom = (self.v / c2).sqrt_().add_(self.eps)
+        self.flat.data.addcdiv_(self.m, denom, value=-self.lr / c1)
+
+
+class DQNTrainer:
+    def __init__(self, cfg: DQNConfig, device="cuda:0"):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.rank = dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
+        n = cfg.n_boards
+        self.env = VecGame(n, device=self.device, seed=cfg.seed, board_offset=self.rank * n)
+        self.env.reset()
+        self.replay = ReplayStore(cfg.replay_capacity, self.device, mode="ring",
+                                  seed=(cfg.seed * 0x9E3779B97F4A7C15 + self.rank + 1) & (2 ** 64 - 1))
+        torch.manual_seed(cfg.seed)                       # identical init on every replica
+        dt = torch.bfloat16 if cfg.bf16 else torch.float32
+        self.net = ResNet10Q(cfg.channels, cfg.blocks, cfg.bn, dtype=dt).to(self.device)
+        self.target = copy.deepcopy(self.net).eval()
+        for p in self.target.parameters():
+            p.requires_grad_(False)
+        self.flat = FlatParams(self.net)
+        self.flat.broadcast_()
+        self.opt = Adam(self.flat, cfg.lr)
+        self.steps = 0
+        self.updates = 0
+        self.q = torch.empty((n, 4), dtype=torch.float32, device=self.device)
+        self.actions = torch.empty(n, dtype=torch.int8, device=self.device)
+
+    def epsilon(self):
+        c = self.cfg
+        f = min(1.0, self.steps / max(1, c.eps_decay_steps))
+        return c.eps_start + f * (c.eps_end - c.eps_start)
+
+    @torch.no_grad()
+    def q_values(self, net, boards, out=None):
+        """Q [n, 4] of int8 boards [n, 16] in eval mode, in act_chunk slices."""
+        n = boards.shape[0]
+        out = torch.empty((n, 4), dtype=torch.float32, device=boards.device) if out is None else out
+        was = net.training
+        net.eval()
+        dt = torch.bfloat16 if self.cfg.bf16 else torch.float32
+        for s in range(0, n, self.cfg.act_chunk):
+            e = min(n, s + self.cfg.act_chunk)
+            out[s:e] = net(board_onehot(boards[s:e], dtype=dt))
+        net.train(was)
+        return out
+
+    @torch.no_grad()
+    def act(self):
+        self.q_values(self.net, self.env.boards, out=self.q)
+        return egreedy_actions(self.q, self.epsilon(), self.cfg.seed, self.steps, gid0=self.rank * self.cfg.n_boards,
+                               out=self.actions)
+
+    @torch.no_grad()
+    def env_step(self):
+        """act + step + store: one transition per board into the ring."""
+        s = self.env.boards.clone()
+        a = self.act()
+        _, reward, done = self.env.step(a, auto_reset=True, merge_reward=True)
+        self.replay.store(s, a, reward.float(), self.env.boards, done)
+        self.steps += 1
+        return reward, done
+
+    def _reward(self, r):
+        return torch.log2(1.0 + r) if self.cfg.reward_transform == "log2" else r
+
+    def update(self, batch=None):
+        c = self.cfg
+        dt = torch.bfloat16 if c.bf16 else torch.float32
+        b = self.replay.sample(batch or c.batch)
+        x, x2 = board_onehot(b["state"], dtype=dt), board_onehot(b["next_state"], dtype=dt)
+        with torch.no_grad():
+            self.target.eval()
+            qt = self.target(x2).contiguous()
+            qo = None
+            if c.double:
+                self.net.eval()
+                qo = self.net(x2).contiguous()
+            y = td_target(self._reward(b["reward"]).contiguous(), b["done"], qt, qo, c.gamma)
+        self.net.train()
+        self.flat.zero_grad()
+        q = self.net(x)
+        q_sa = q.gather(1, b["action"].long().view(-1, 1)).squeeze(1)
+        loss = F.smooth_l1_loss(q_sa, y)
+        loss.backward()
+        self.flat.allreduce_grad()
+        self.opt.step()
+        self.updates += 1
+        if self.updates % c.target_sync == 0:
+            self.sync_target()
+        return {"loss": float(loss.detach()), "q_mean": float(q_sa.detach().mean()), "batch": b}
+
+    def sync_target(self):
+        self.target.load_state_dict(self.net.state_dict())
+
+    def train_step(self):
+        reward, done = self.env_step()
+        out = {"loss": math.nan}
+        if len(self.replay) >= self.cfg.learn_start:
+            for _ in range(self.cfg.updates_per_step):
+                out = self.update()
+        out["epsilon"] = self.epsilon()
+        return out

@@ -1,0 +1,112 @@
+"""Config-5 value-based pieces on the CPU (no GPU): the structured-GEMM ResNet-10 vs
+F.conv2d and vs the float64 oracle (oracle/dqn_ref.py; parity UNPINNED against the reference,
+which has no DQN/ResNet code), BN folding, the flat Adam vs torch.optim.Adam, and the oracle's
+TD target / Huber against torch's definitions."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import dqn_ref as R
+
+
+def _params(net):
+    return {"convs": [(c.weight.detach().numpy(), c.bias.detach().numpy()) for c in net.conv_layers()],
+            "bns": [dict(mean=m.running_mean.numpy(), var=m.running_var.numpy(), gamma=m.weight.detach().numpy(),
+                         beta=m.bias.detach().numpy()) for m in net.bns] if net.use_bn else None,
+            "head": (net.head.weight.detach().numpy(), net.head.bias.detach().numpy())}
+
+
+def _net(bn=True, channels=8, blocks=2):
+    from rein48_amd.dqn.nets import ResNet10Q
+    torch.manual_seed(0)
+    net = ResNet10Q(channels=channels, blocks=blocks, bn=bn, dtype=torch.float64).double()
+    if bn:
+        for m in net.bns:
+            m.running_mean.uniform_(-0.3, 0.3)
+            m.running_var.uniform_(0.5, 1.5)
+            m.weight.data.uniform_(0.5, 1.5)
+            m.bias.data.uniform_(-0.2, 0.2)
+    return net
+
+
+@pytest.mark.parametrize("ci,co", [(18, 8), (8, 8)])
+def test_structured_conv_equals_conv2d(ci, co):
+    from rein48_amd.dqn.nets import dense_conv_weight
+    torch.manual_seed(1)
+    conv = torch.nn.Conv2d(ci, co, 3, padding=1).double()
+    x = torch.randn(7, ci, 4, 4, dtype=torch.float64, requires_grad=True)
+    ref = conv(x)                                                   # [7, co, 4, 4]
+    xp = x.permute(0, 2, 3, 1).reshape(7, 16 * ci)                  # position-major, channel-minor
+    got = F.linear(xp, dense_conv_weight(conv), conv.bias.repeat(16)).view(7, 4, 4, co).permute(0, 3, 1, 2)
+    torch.testing.assert_close(got, ref, rtol=1e-12, atol=1e-12)
+    g = torch.randn_like(ref)
+    gw_ref, gx_ref = torch.autograd.grad(ref, (conv.weight, x), g)
+    gw, gx = torch.autograd.grad(got, (conv.weight, x), g)
+    torch.testing.assert_close(gw, gw_ref, rtol=1e-12, atol=1e-12)
+    torch.testing.assert_close(gx, gx_ref, rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.parametrize("bn", [False, True])
+def test_resnet10_matches_oracle(bn):
+    net = _net(bn).eval()
+    b = np.random.default_rng(0).integers(0, 18, size=(64, 16))
+    q = net(torch.from_numpy(R.onehot(b).reshape(64, -1))).detach().numpy()
+    np.testing.assert_allclose(q, R.resnet10_q(_params(net), b), rtol=1e-6, atol=1e-8)   # Q is returned in fp32
+
+
+def test_full_size_net_shape_and_param_count():
+    from rein48_amd.dqn.nets import ResNet10Q
+    net = ResNet10Q()
+    n_w = sum(m.weight.numel() for m in net.conv_layers()) + net.head.weight.numel()
+    assert len(net.conv_layers()) + 1 == 10                                  # 10 weight layers
+    assert n_w == 18 * 64 * 9 + 8 * 64 * 64 * 9 + 16 * 64 * 4
+    assert net(torch.zeros(3, 16 * 18)).shape == (3, 4)
+
+
+def test_bn_folding_matches_eval_forward():
+    from rein48_amd.dqn.nets import ResNet10Q
+    net = _net(True).eval()
+    convs, head = net.folded()
+    plain = ResNet10Q(channels=8, blocks=2, bn=False, dtype=torch.float64).double().eval()
+    with torch.no_grad():
+        for c, (w, b) in zip(plain.conv_layers(), convs):
+            c.weight.copy_(w)
+            c.bias.copy_(b)
+        plain.head.weight.copy_(head[0])
+        plain.head.bias.copy_(head[1])
+    x = torch.from_numpy(R.onehot(np.random.default_rng(2).integers(0, 18, size=(40, 16))).reshape(40, -1))
+    torch.testing.assert_close(plain(x), net(x), rtol=1e-5, atol=1e-6)     # folded weights are fp32
+
+
+def test_flat_adam_matches_torch_adam():
+    from rein48_amd.a3c.optim import FlatParams
+    from rein48_amd.dqn.trainer import Adam
+    torch.manual_seed(3)
+    a = torch.nn.Linear(5, 3).double()
+    b = torch.nn.Linear(5, 3).double()
+    b.load_state_dict(a.state_dict())
+    flat = FlatParams(a)
+    mine = Adam(flat, lr=1e-2)
+    ref = torch.optim.Adam(b.parameters(), lr=1e-2)
+    for _ in range(5):
+        x = torch.randn(8, 5, dtype=torch.float64)
+        flat.zero_grad()
+        a(x).square().sum().backward()
+        mine.step()
+        ref.zero_grad()
+        b(x).square().sum().backward()
+        ref.step()
+    torch.testing.assert_close(a.weight, b.weight, rtol=1e-10, atol=1e-12)
+
+
+def test_oracle_td_target_and_huber():
+    rng = np.random.default_rng(4)
+    qt, qo = rng.normal(size=(100, 4)), rng.normal(size=(100, 4))
+    r, d = rng.normal(size=100), (rng.random(100) < 0.3)
+    y = R.td_target(r, d, qt, None, 0.9)
+    np.testing.assert_allclose(y, r + 0.9 * (1 - d) * qt.max(1))
+    y2 = R.td_target(r, d, qt, qo, 0.9)
+    np.testing.assert_allclose(y2, r + 0.9 * (1 - d) * qt[np.arange(100), qo.argmax(1)])
+    x = rng.normal(size=100) * 3
+    assert abs(R.huber(x, y) - float(F.smooth_l1_loss(torch.tensor(x), torch.tensor(y)))) < 1e-12

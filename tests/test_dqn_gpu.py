@@ -1,0 +1,125 @@
+"""Config-5 kernels and trainer on the GPU vs the float64 oracle (oracle/dqn_ref.py).
+
+One-hot planes (exact), epsilon-greedy (exact given the Philox draw), TD target (fp32 vs f64),
+ResNet-10 forward in fp32 (vs f64) and bf16 (vs f64, bounded by PyTorch's own bf16 rounding),
+and one DQN update whose loss equals the oracle's recomputation from the sampled minibatch and
+the pre-update weights.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import dqn_ref as R
+from oracle import native as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def test_onehot_exact():
+    from rein48_amd.dqn.kernels import board_onehot
+    b = np.random.default_rng(0).integers(0, 18, size=(10_001, 16)).astype(np.int8)
+    t = torch.from_numpy(b).to(DEV)
+    want = R.onehot(b).reshape(-1, 16 * 18)
+    np.testing.assert_array_equal(board_onehot(t, dtype=torch.float32).cpu().numpy(), want)
+    np.testing.assert_array_equal(board_onehot(t, dtype=torch.bfloat16).float().cpu().numpy(), want)
+
+
+def test_egreedy_exact():
+    from rein48_amd.dqn.kernels import egreedy_actions
+    rng = np.random.default_rng(1)
+    n, seed, ctr, gid0, eps = 100_000, 5, 9, 300, 0.3
+    q = rng.normal(size=(n, 4)).astype(np.float32)
+    q[::7, 1] = q[::7, 0]                                          # ties -> first argmax
+    got = egreedy_actions(torch.from_numpy(q).to(DEV), eps, seed, ctr, gid0=gid0).cpu().numpy()
+    idx = np.arange(0, n, 53)
+    w = np.array([O.philox([(gid0 + i) & 0xFFFFFFFF, (gid0 + i) >> 32, ctr, 0xD0E], [seed, 0]) for i in idx],
+                 np.uint64)
+    u = (w[:, 0] >> 8).astype(np.float64) / 16777216.0
+    want = R.egreedy(q[idx], u, (w[:, 1] >> 30).astype(np.int64), eps)
+    np.testing.assert_array_equal(got[idx], want)
+    assert abs((got != q.argmax(1)).mean() - eps * 0.75) < 0.01    # 3/4 of random picks differ
+
+
+@pytest.mark.parametrize("double", [False, True])
+def test_td_target_matches_oracle(double):
+    from rein48_amd.dqn.kernels import td_target
+    rng = np.random.default_rng(2)
+    n = 50_001
+    r = rng.normal(size=n).astype(np.float32)
+    d = (rng.random(n) < 0.2).astype(np.uint8)
+    qt, qo = (rng.normal(size=(n, 4)).astype(np.float32) for _ in range(2))
+    T = lambda a: torch.from_numpy(a).to(DEV)
+    y = td_target(T(r), T(d), T(qt), T(qo) if double else None, 0.97).cpu().numpy()
+    np.testing.assert_allclose(y, R.td_target(r, d, qt, qo if double else None, 0.97), rtol=1e-6, atol=1e-6)
+
+
+def _params(net):
+    return {"convs": [(c.weight.detach().double().cpu().numpy(), c.bias.detach().double().cpu().numpy())
+                      for c in net.conv_layers()],
+            "bns": [dict(mean=m.running_mean.double().cpu().numpy(), var=m.running_var.double().cpu().numpy(),
+                         gamma=m.weight.detach().double().cpu().numpy(), beta=m.bias.detach().double().cpu().numpy())
+                    for m in net.bns] if net.use_bn else None,
+            "head": (net.head.weight.detach().double().cpu().numpy(), net.head.bias.detach().double().cpu().numpy())}
+
+
+def test_resnet10_gpu_matches_oracle():
+    """fp32 forward vs f64 within 1e-4 and the bf16 forward within 5e-2, both as max |error|
+    relative to mean |Q| (bf16 rounds inputs, weights and activations; fp32 accumulation)."""
+    from rein48_amd.dqn.kernels import board_onehot
+    from rein48_amd.dqn.nets import ResNet10Q
+    torch.manual_seed(0)
+    net = ResNet10Q().to(DEV).eval()
+    with torch.no_grad():
+        for m in net.bns:
+            m.running_mean.uniform_(-0.2, 0.2)
+            m.running_var.uniform_(0.5, 2.0)
+        net.head.weight.normal_(std=0.05)
+    b = np.random.default_rng(3).integers(0, 12, size=(512, 16)).astype(np.int8)
+    bt = torch.from_numpy(b).to(DEV)
+    want = R.resnet10_q(_params(net), b)
+    scale = np.abs(want).mean()
+    with torch.no_grad():
+        q32 = net(board_onehot(bt, dtype=torch.float32)).cpu().numpy()
+        net.dtype = torch.bfloat16
+        q16 = net(board_onehot(bt, dtype=torch.bfloat16)).cpu().numpy()
+    e32 = np.abs(q32 - want).max() / scale
+    e16 = np.abs(q16 - want).max() / scale
+    assert e32 < 1e-4, e32
+    assert e16 < 5e-2, e16
+
+
+def test_dqn_update_loss_matches_oracle():
+    """fp32, no BN (train-mode BN would use batch statistics the eval-mode oracle does not
+    model): the reported Huber loss of one update equals the oracle's recomputation from the
+    sampled minibatch with the pre-update online and target weights (double DQN)."""
+    from rein48_amd.dqn import DQNConfig, DQNTrainer
+    cfg = DQNConfig(n_boards=2048, replay_capacity=1 << 16, batch=1024, learn_start=1 << 30, bn=False, bf16=False,
+                    channels=16, blocks=2, seed=7, double=True, gamma=0.95)
+    tr = DQNTrainer(cfg, device=DEV)
+    for _ in range(6):
+        tr.train_step()
+    assert len(tr.replay) == 6 * 2048
+    with torch.no_grad():                                            # make target != online
+        for p in tr.target.parameters():
+            p.add_(0.01 * torch.randn_like(p))
+    p_on, p_tg = _params(tr.net), _params(tr.target)
+    out = tr.update()
+    b = {k: v.cpu().numpy() for k, v in out["batch"].items()}
+    q = R.resnet10_q(p_on, b["state"])[np.arange(len(b["action"])), b["action"].astype(np.int64)]
+    y = R.td_target(np.log2(1.0 + b["reward"].astype(np.float64)), b["done"], R.resnet10_q(p_tg, b["next_state"]),
+                    R.resnet10_q(p_on, b["next_state"]), 0.95)
+    np.testing.assert_allclose(out["loss"], R.huber(q, y), rtol=1e-4, atol=1e-6)
+    assert any(not np.allclose(a, c) for a, c in zip(p_on["convs"][0], _params(tr.net)["convs"][0]))
+
+
+def test_dqn_bf16_resnet10_trains():
+    from rein48_amd.dqn import DQNConfig, DQNTrainer
+    cfg = DQNConfig(n_boards=4096, replay_capacity=1 << 17, batch=2048, learn_start=8192, seed=1, target_sync=2)
+    tr = DQNTrainer(cfg, device=DEV)
+    outs = [tr.train_step() for _ in range(5)]
+    assert np.isnan(outs[0]["loss"]) and all(np.isfinite(o["loss"]) for o in outs[1:])
+    assert tr.updates == 4 and len(tr.replay) == 5 * 4096          # learn_start reached at step 2
+    assert tr.epsilon() < 1.0
+    for a, b in zip(tr.target.state_dict().values(), tr.net.state_dict().values()):
+        assert torch.equal(a, b)                                     # synced after update 4
