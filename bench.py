@@ -174,6 +174,47 @@ def a3c_config3(dev, seed, n_boards, updates=2):
             "last_losses": {k: out[k] for k in ("actor_loss", "critic_loss")}}
 
 
+def dqn_config5(dev, seed, n_boards, steps=3):
+    """BASELINE configs[4] per GPU (16M boards over 8 GPUs = 2^21 per GPU): ResNet-10 Q-network
+    in bf16 (structured-GEMM convs on hipBLASLt), epsilon-greedy acting on every board, env step
+    with merge reward + auto-reset, (s, a, r, s', done) of every board into the HBM replay ring,
+    one 64K-transition double-DQN update per env step."""
+    from rein48_amd.dqn import DQNConfig, DQNTrainer
+    cfg = DQNConfig(n_boards=n_boards, replay_capacity=1 << 25, batch=1 << 16, learn_start=1, seed=seed,
+                    act_chunk=1 << 18)
+    tr = DQNTrainer(cfg, device=dev)
+    tr.train_step()                                   # warm-up (hipBLASLt heuristics, allocator)
+    s = torch.cuda.current_stream(dev)
+    act, env, upd = [], [], []
+    for _ in range(steps):
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        e[0].record(s)
+        st = tr.env.boards.clone()
+        a = tr.act()
+        e[1].record(s)
+        _, reward, done = tr.env.step(a, auto_reset=True, merge_reward=True)
+        tr.replay.store(st, a, reward.float(), tr.env.boards, done)
+        tr.steps += 1
+        e[2].record(s)
+        out = tr.update()
+        e[3].record(s)
+        torch.cuda.synchronize(dev)
+        act.append(e[0].elapsed_time(e[1]))
+        env.append(e[1].elapsed_time(e[2]))
+        upd.append(e[2].elapsed_time(e[3]))
+    a_ms, e_ms, u_ms = (sum(x) / steps for x in (act, env, upd))
+    from rein48_amd.dqn.nets import ResNet10Q
+    C = cfg.channels
+    useful = 2 * 100 * (18 * C + 2 * cfg.blocks * C * C) + 2 * 16 * C * 4     # valid taps only
+    return {"boards": n_boards, "net": "ResNet-10 (stem + 4 basic blocks, C=%d, BN) bf16" % C,
+            "replay_capacity": cfg.replay_capacity, "batch": cfg.batch,
+            "act_ms": a_ms, "env_step_store_ms": e_ms, "update_ms": u_ms,
+            "env_steps_per_s": n_boards / ((a_ms + e_ms + u_ms) * 1e-3),
+            "act_useful_TFLOPs": n_boards * useful / (a_ms * 1e-3) / 1e12,
+            "act_frac_of_bf16_dense_peak": n_boards * useful / (a_ms * 1e-3) / 2.5e15,
+            "loss": out["loss"]}
+
+
 def traffic_from_profile(n_boards):
     p = os.path.join(ROOT, "profiles", "pmc_k_step.json")
     if not os.path.exists(p):
@@ -300,6 +341,10 @@ def main():
             ex["a3c_config3"] = a3c_config3(dev, args.seed, n)
         except Exception as e:  # the env bench line must print even if the trainer fails
             ex["a3c_config3"] = {"error": repr(e)}
+        try:
+            ex["dqn_config5"] = dqn_config5(dev, args.seed, 1 << 21)
+        except Exception as e:
+            ex["dqn_config5"] = {"error": repr(e)}
         if not args.no_cpu_baseline:
             ex["cpu_strong_line"] = strong_cpu_line()
         line["extras"] = ex

@@ -242,6 +242,16 @@ int r48_egreedy_actions(const float *q, int64_t n, float eps, uint64_t seed, int
 int r48_td_target(const float *reward, const uint8_t *done, const float *q_next_target,
                   const float *q_next_online, int64_t n, float gamma, float *y, void *stream);
 
+/* Fused ResNet-10 Q-network inference on bf16 MFMA (rein48_amd/dqn/nets.py:ResNet10Q with
+ * C = 64, 4 basic blocks, eval-mode BN folded): boards int8[n][16] -> q float[n][4] (nullable,
+ * 16-byte aligned) and, when actions != NULL, the epsilon-greedy draw of r48_egreedy_actions
+ * (same Philox contract) into actions int8[n]. wblob (r48_resnet_q_blob_bytes() bytes), head_w
+ * (8 KiB bf16) and head_b (4 floats) are packed by rein48_amd/dqn/fused.py:pack_resnet. */
+int r48_resnet_q_forward(const int8_t *boards, int64_t n, const void *wblob, const void *head_w,
+                         const float *head_b, float *q, int8_t *actions, float eps, uint64_t seed,
+                         int64_t gid0, uint32_t ctr, void *stream);
+int64_t r48_resnet_q_blob_bytes(void);
+
 /* Thread-local message of the last failed call on this thread ("" if none). */
 const char *r48_last_error(void);
 /* "rein48 <version> gfx950" */

@@ -1,0 +1,116 @@
+"""Host side of the fused ResNet-10 inference kernel (r48_resnet_q_forward, csrc/r48_resnet.hip).
+
+pack_resnet(net) folds eval-mode BatchNorm into each conv (ResNet10Q.folded) and lays the
+weights out as the kernel's v_mfma_f32_32x32x16_bf16 A-operand fragments (lane l, row
+r = l & 31, half h = l >> 5, element j):
+  stem fragment (tap t, k-chunk s, row tile m):  W[32m + r][16s + 8h + j][t // 3][t % 3]   (planes >= 18: 0)
+  conv fragment (tap t, k-chunk s, row tile m):  W[32m + r][16s + 8(j>>2) + 4h + (j&3)][t // 3][t % 3]
+each layer's fragments followed by one bias fragment (64 floats, zero padded to 1 KiB):
+  blob = stem (36 + 1 fragments) | conv1 .. conv8 (72 + 1 each), bf16 fragments of 1 KiB.
+The head weight is packed per lane: head_w[cell][h][a][2k + e] (bf16) = Wh[a][64 cell + ci]
+with ci the channel of the lane's packed activation register k, element e (k = 4s + q:
+row tile m = s >> 1, accumulator register i = 8(s & 1) + 2q + e, ci = 32m + 8(i>>2) + 4h + (i&3)).
+"""
+import ctypes as C
+
+import numpy as np
+import torch
+
+from .. import _lib
+from .._lib import check, ptr
+
+_MAPS = {}
+
+
+def _lane_maps():
+    lane = np.arange(64)
+    r, h = lane & 31, lane >> 5
+    j = np.arange(8)
+    stem_plane = lambda s: 16 * s + 8 * h[:, None] + j[None, :]                              # [64, 8]
+    conv_ci = lambda s: 16 * s + 8 * (j[None, :] >> 2) + 4 * h[:, None] + (j[None, :] & 3)  # [64, 8]
+    return r, stem_plane, conv_ci
+
+
+def _maps(channels, planes=18):
+    key = (channels, planes)
+    if key in _MAPS:
+        return _MAPS[key]
+    C_ = channels
+    r, stem_plane, conv_ci = _lane_maps()
+    # stem: indices into w.reshape(-1) of shape [C, planes, 3, 3]; -1 = zero
+    st = []
+    for t in range(9):
+        for s in range(2):
+            for m in range(2):
+                co = (32 * m + r)[:, None].repeat(8, 1)
+                pl = stem_plane(s)
+                idx = ((co * planes + pl) * 3 + t // 3) * 3 + t % 3
+                st.append(np.where(pl < planes, idx, -1))
+    cv = []
+    for t in range(9):
+        for s in range(4):
+            for m in range(2):
+                co = (32 * m + r)[:, None].repeat(8, 1)
+                ci = conv_ci(s)
+                cv.append(((co * C_ + ci) * 3 + t // 3) * 3 + t % 3)
+    # head: [cell][h][a][32] -> index into Wh.reshape(-1) of shape [4, 16 * C]
+    hd = np.zeros((16, 2, 4, 32), np.int64)
+    for cell in range(16):
+        for hh in range(2):
+            for k in range(16):
+                s, q = k >> 2, k & 3
+                m = s >> 1
+                for e in range(2):
+                    i = 8 * (s & 1) + 2 * q + e
+                    ci = 32 * m + 8 * (i >> 2) + 4 * hh + (i & 3)
+                    for a in range(4):
+                        hd[cell, hh, a, 2 * k + e] = a * 16 * C_ + cell * C_ + ci
+    _MAPS[key] = (np.stack(st), np.stack(cv), hd)
+    return _MAPS[key]
+
+
+def _gather(flat, idx, dev):
+    """flat[idx] with idx < 0 -> 0 (bf16 out)."""
+    ext = torch.cat([flat, torch.zeros(1, dtype=flat.dtype, device=dev)])
+    it = torch.as_tensor(idx, device=dev)
+    return ext[torch.where(it < 0, ext.numel() - 1, it)].to(torch.bfloat16)
+
+
+def _bias_frag(b, dev):
+    f = torch.zeros(256, dtype=torch.float32, device=dev)
+    f[:b.numel()] = b
+    return f.view(torch.bfloat16)           # 1 KiB
+
+
+@torch.no_grad()
+def pack_resnet(net):
+    """-> (blob bf16 [frags * 512], head_w bf16 [4096], head_b f32 [4]) on the net's device."""
+    if net.channels != 64 or net.n_blocks != 4:
+        raise ValueError("the fused kernel is built for ResNet10Q(channels=64, blocks=4)")
+    dev = net.head.weight.device
+    convs, (hw, hb) = net.folded()
+    st, cv, hd = _maps(net.channels)
+    parts = []
+    w, b = convs[0]
+    parts += [_gather(w.reshape(-1), st, dev).reshape(-1), _bias_frag(b, dev)]
+    for w, b in convs[1:]:
+        parts += [_gather(w.reshape(-1), cv, dev).reshape(-1), _bias_frag(b, dev)]
+    blob = torch.cat(parts).contiguous()
+    assert blob.numel() * 2 == _lib.load().r48_resnet_q_blob_bytes()
+    head_w = _gather(hw.reshape(-1), hd.reshape(-1), dev).contiguous()
+    return blob, head_w, hb.float().contiguous()
+
+
+def resnet_q_forward(boards, packed, q=True, actions=False, eps=0.0, seed=0, ctr=0, gid0=0):
+    """Fused ResNet-10 inference over int8 boards [n, 16] -> (Q [n, 4] or None, actions [n] or None)."""
+    if not boards.is_cuda or boards.dtype != torch.int8 or not boards.is_contiguous():
+        raise ValueError("boards must be a contiguous int8 GPU tensor")
+    blob, head_w, head_b = packed
+    n = boards.numel() // 16
+    dev = boards.device
+    qt = torch.empty((n, 4), dtype=torch.float32, device=dev) if q else None
+    at = torch.empty(n, dtype=torch.int8, device=dev) if actions else None
+    check(_lib.load().r48_resnet_q_forward(ptr(boards), n, ptr(blob), ptr(head_w), ptr(head_b), ptr(qt), ptr(at),
+                                           float(eps), int(seed) & (2 ** 64 - 1), int(gid0), int(ctr) & 0xFFFFFFFF,
+                                           C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)))
+    return qt, at

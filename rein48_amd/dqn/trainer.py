@@ -3,8 +3,9 @@
 No reference trainer exists (the reference's value-based code is the unfinished DDPG under
 algorithm/ddpg/; its replay buffer, replay.py, is what ReplayStore's fill_drain mode restates).
 One train_step per env step, per GPU:
-  act      Q = ResNet10Q(onehot(boards)) in eval mode (bf16 MFMA GEMMs), epsilon-greedy
-           (r48_egreedy_actions, Philox keyed by global board id)
+  act      Q = ResNet10Q(boards) in eval mode + epsilon-greedy (Philox keyed by global board
+           id) in ONE fused bf16 MFMA kernel (r48_resnet_q_forward; weights repacked with BN
+           folded after every update), or the PyTorch structured-GEMM net + r48_egreedy_actions
   step     r48_env_step with the opt-in merge reward (the reference reward is always 0,
            GameClient.py:138, which gives a value learner nothing to learn) and auto-reset
   store    (s, a, r, s', done) of every board into the ring (r48_replay_store; 38 B each).
@@ -51,7 +52,8 @@ class DQNConfig:
     blocks: int = 4
     bn: bool = True
     bf16: bool = True
-    act_chunk: int = 1 << 18         # boards per Q forward while acting
+    act_chunk: int = 1 << 18         # boards per Q forward while acting (PyTorch path)
+    fused: bool = True               # eval-mode Q through r48_resnet_q_forward (bf16, C=64, 4 blocks)
     seed: int = 0
 
 
@@ -98,6 +100,9 @@ class DQNTrainer:
         self.updates = 0
         self.q = torch.empty((n, 4), dtype=torch.float32, device=self.device)
         self.actions = torch.empty(n, dtype=torch.int8, device=self.device)
+        self.use_fused = cfg.fused and cfg.bf16 and cfg.channels == 64 and cfg.blocks == 4
+        self._packed = {}                                   # id(net) -> (version, packed weights)
+        self._version = 0                                   # bumped by every optimizer step / sync
 
     def epsilon(self):
         c = self.cfg
@@ -118,11 +123,34 @@ class DQNTrainer:
         net.train(was)
         return out
 
+    def packed(self, net):
+        """Fused-kernel weights of `net` (eval-mode BN folded), repacked when the weights changed."""
+        from .fused import pack_resnet
+        ver, p = self._packed.get(id(net), (-1, None))
+        if ver != self._version:
+            p = pack_resnet(net)
+            self._packed[id(net)] = (self._version, p)
+        return p
+
+    @torch.no_grad()
+    def q_eval(self, net, boards):
+        """Eval-mode Q [n, 4] of int8 boards [n, 16]."""
+        if self.use_fused:
+            from .fused import resnet_q_forward
+            return resnet_q_forward(boards.contiguous(), self.packed(net))[0]
+        return self.q_values(net, boards)
+
     @torch.no_grad()
     def act(self):
+        eps, gid0 = self.epsilon(), self.rank * self.cfg.n_boards
+        if self.use_fused:
+            from .fused import resnet_q_forward
+            _, a = resnet_q_forward(self.env.boards, self.packed(self.net), q=False, actions=True, eps=eps,
+                                    seed=self.cfg.seed, ctr=self.steps, gid0=gid0)
+            self.actions.copy_(a)
+            return self.actions
         self.q_values(self.net, self.env.boards, out=self.q)
-        return egreedy_actions(self.q, self.epsilon(), self.cfg.seed, self.steps, gid0=self.rank * self.cfg.n_boards,
-                               out=self.actions)
+        return egreedy_actions(self.q, eps, self.cfg.seed, self.steps, gid0=gid0, out=self.actions)
 
     @torch.no_grad()
     def env_step(self):
@@ -141,14 +169,11 @@ class DQNTrainer:
         c = self.cfg
         dt = torch.bfloat16 if c.bf16 else torch.float32
         b = self.replay.sample(batch or c.batch)
-        x, x2 = board_onehot(b["state"], dtype=dt), board_onehot(b["next_state"], dtype=dt)
+        x = board_onehot(b["state"], dtype=dt)
         with torch.no_grad():
             self.target.eval()
-            qt = self.target(x2).contiguous()
-            qo = None
-            if c.double:
-                self.net.eval()
-                qo = self.net(x2).contiguous()
+            qt = self.q_eval(self.target, b["next_state"]).contiguous()
+            qo = self.q_eval(self.net, b["next_state"]).contiguous() if c.double else None
             y = td_target(self._reward(b["reward"]).contiguous(), b["done"], qt, qo, c.gamma)
         self.net.train()
         self.flat.zero_grad()
@@ -158,6 +183,7 @@ class DQNTrainer:
         loss.backward()
         self.flat.allreduce_grad()
         self.opt.step()
+        self._version += 1
         self.updates += 1
         if self.updates % c.target_sync == 0:
             self.sync_target()
@@ -165,6 +191,7 @@ class DQNTrainer:
 
     def sync_target(self):
         self.target.load_state_dict(self.net.state_dict())
+        self._version += 1
 
     def train_step(self):
         reward, done = self.env_step()
