@@ -77,26 +77,6 @@ __device__ __forceinline__ uint32_t cell_shift(uint32_t v)
         return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x110 - D, 0xF, 0xF, true);   // row_shr: lane i <- i - |D|
 }
 
-// B fragment of tap (DR, DC) from the 4 packed registers of one k-chunk
-template <int DR, int DC>
-__device__ __forceinline__ bf16x8 tap_frag(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3, bool col0, bool col3)
-{
-    constexpr int D = 4 * DR + DC;
-    uint32_t r[4] = {cell_shift<D>(a0), cell_shift<D>(a1), cell_shift<D>(a2), cell_shift<D>(a3)};
-    if constexpr (DC == 1) {
-#pragma unroll
-        for (int q = 0; q < 4; q++)
-            r[q] = col3 ? 0u : r[q];
-    } else if constexpr (DC == -1) {
-#pragma unroll
-        for (int q = 0; q < 4; q++)
-            r[q] = col0 ? 0u : r[q];
-    }
-    bf16x8 f;
-    __builtin_memcpy(&f, r, 16);
-    return f;
-}
-
 __device__ __forceinline__ bf16x8 lds_frag(const uint4 *lds, int frag, int lane)
 {
     const uint4 v = lds[frag * 64 + lane];
@@ -105,79 +85,93 @@ __device__ __forceinline__ bf16x8 lds_frag(const uint4 *lds, int frag, int lane)
     return f;
 }
 
-// one tap of a layer: for every k-chunk, two A fragments (row tiles) x G column groups
+// tap (DR, DC) of k-chunk s for all column groups: B = the chunk's registers shifted by DR
+// grid rows (xs[g][DC + 1] already holds the column-shifted, edge-masked copy), times both
+// row tiles -- one pair of LDS weight fragments feeds 2G MFMAs
 template <int DR, int DC, int NCH>
-__device__ __forceinline__ void conv_tap(const uint4 *wl, const uint32_t (&src)[G][16], f32x16 (&acc)[G][2], int lane,
-                                         bool col0, bool col3)
+__device__ __forceinline__ void tap_mfma(const uint4 *wl, int s, const uint32_t (&xs)[G][3][4], f32x16 (&acc)[G][2],
+                                         int lane)
 {
     constexpr int t = (DR + 1) * 3 + (DC + 1);
+    const bf16x8 A0 = lds_frag(wl, (t * NCH + s) * 2 + 0, lane);
+    const bf16x8 A1 = lds_frag(wl, (t * NCH + s) * 2 + 1, lane);
 #pragma unroll
-    for (int s = 0; s < NCH; s++) {
-        const bf16x8 A0 = lds_frag(wl, (t * NCH + s) * 2 + 0, lane);
-        const bf16x8 A1 = lds_frag(wl, (t * NCH + s) * 2 + 1, lane);
+    for (int g = 0; g < G; g++) {
+        uint32_t r[4];
 #pragma unroll
-        for (int g = 0; g < G; g++) {
-            const bf16x8 B = tap_frag<DR, DC>(src[g][4 * s], src[g][4 * s + 1], src[g][4 * s + 2], src[g][4 * s + 3],
-                                              col0, col3);
-            acc[g][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A0, B, acc[g][0], 0, 0, 0);
-            acc[g][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A1, B, acc[g][1], 0, 0, 0);
-        }
+        for (int q = 0; q < 4; q++)
+            r[q] = cell_shift<4 * DR>(xs[g][DC + 1][q]);
+        bf16x8 B;
+        __builtin_memcpy(&B, r, 16);
+        acc[g][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A0, B, acc[g][0], 0, 0, 0);
+        acc[g][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A1, B, acc[g][1], 0, 0, 0);
     }
 }
 
-template <int NCH>
-__device__ __forceinline__ void conv_layer(const uint4 *wl, const uint32_t (&src)[G][16], f32x16 (&acc)[G][2],
-                                           int lane, bool col0, bool col3)
-{
-#pragma unroll
-    for (int g = 0; g < G; g++)
-#pragma unroll
-        for (int m = 0; m < 2; m++)
-#pragma unroll
-            for (int r = 0; r < 16; r++)
-                acc[g][m][r] = 0.0f;
-    conv_tap<-1, -1, NCH>(wl, src, acc, lane, col0, col3);
-    conv_tap<-1, 0, NCH>(wl, src, acc, lane, col0, col3);
-    conv_tap<-1, 1, NCH>(wl, src, acc, lane, col0, col3);
-    conv_tap<0, -1, NCH>(wl, src, acc, lane, col0, col3);
-    conv_tap<0, 0, NCH>(wl, src, acc, lane, col0, col3);
-    conv_tap<0, 1, NCH>(wl, src, acc, lane, col0, col3);
-    conv_tap<1, -1, NCH>(wl, src, acc, lane, col0, col3);
-    conv_tap<1, 0, NCH>(wl, src, acc, lane, col0, col3);
-    conv_tap<1, 1, NCH>(wl, src, acc, lane, col0, col3);
-}
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef short i16x2 __attribute__((ext_vector_type(2)));
 
-// bias (+ residual) + ReLU -> packed bf16 activations in B-fragment order:
-// dst[g][4s + q] = channels of row tile s >> 1, accumulator registers 8(s & 1) + 2q, +1
-template <bool RESID>
-__device__ __forceinline__ void epilogue(const f32x16 (&acc)[G][2], const float *bias, int h,
-                                         const uint32_t (&resid)[G][16], uint32_t (&dst)[G][16])
+// One conv layer: k-chunk by k-chunk, the column-shifted copies x[p-1] (zero on the left edge),
+// x[p], x[p+1] (zero on the right edge) of every group are built once and each of the 9 taps
+// is then a single DPP row shift by 4dr; then the epilogue (bias, optional residual, ReLU,
+// bf16) per group. act[g] is the layer's input and output; SAVE keeps the input in res[g] for
+// the block's skip connection. act[g][4s + q] = channels of row tile s >> 1, accumulator
+// registers 8(s & 1) + 2q, +1.
+// The edge masks are applied as AND with a 0 / all-ones lane mask, never as a select around the
+// DPP: the compiler lowers `edge ? 0 : dpp(x)` to an EXEC-masked DPP move, and a DPP read from a
+// lane disabled in EXEC returns 0 -- interior cells would lose their edge neighbours.
+template <int NCH, bool RESID, bool SAVE>
+__device__ __forceinline__ void layer(const uint4 *wl, const float *bias, uint32_t (&act)[G][16],
+                                      uint32_t (&res)[G][16], f32x16 (&acc)[G][2], int lane, int h, uint32_t keep_l,
+                                      uint32_t keep_r)
 {
-    float b[2][16];
-#pragma unroll
-    for (int m = 0; m < 2; m++)
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const float4 v = *reinterpret_cast<const float4 *>(bias + 32 * m + 8 * u + 4 * h);
-            b[m][4 * u + 0] = v.x;
-            b[m][4 * u + 1] = v.y;
-            b[m][4 * u + 2] = v.z;
-            b[m][4 * u + 3] = v.w;
-        }
 #pragma unroll
     for (int g = 0; g < G; g++)
+        acc[g][0] = acc[g][1] = f32x16{};
+#pragma unroll
+    for (int s = 0; s < NCH; s++) {
+        uint32_t xs[G][3][4];
+#pragma unroll
+        for (int g = 0; g < G; g++)
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const uint32_t x = act[g][4 * s + q];
+                xs[g][0][q] = cell_shift<-1>(x) & keep_l;   // cell p - 1, zero on the left edge
+                xs[g][1][q] = x;
+                xs[g][2][q] = cell_shift<1>(x) & keep_r;    // cell p + 1, zero on the right edge
+            }
+        tap_mfma<-1, -1, NCH>(wl, s, xs, acc, lane);
+        tap_mfma<-1, 0, NCH>(wl, s, xs, acc, lane);
+        tap_mfma<-1, 1, NCH>(wl, s, xs, acc, lane);
+        tap_mfma<0, -1, NCH>(wl, s, xs, acc, lane);
+        tap_mfma<0, 0, NCH>(wl, s, xs, acc, lane);
+        tap_mfma<0, 1, NCH>(wl, s, xs, acc, lane);
+        tap_mfma<1, -1, NCH>(wl, s, xs, acc, lane);
+        tap_mfma<1, 0, NCH>(wl, s, xs, acc, lane);
+        tap_mfma<1, 1, NCH>(wl, s, xs, acc, lane);
+    }
+#pragma unroll
+    for (int g = 0; g < G; g++) {
+        if (SAVE) {
+#pragma unroll
+            for (int k = 0; k < 16; k++)
+                res[g][k] = act[g][k];
+        }
 #pragma unroll
         for (int s = 0; s < 4; s++)
 #pragma unroll
             for (int q = 0; q < 4; q++) {
-                const int m = s >> 1, i = 8 * (s & 1) + 2 * q;
-                float lo = acc[g][m][i] + b[m][i], hi = acc[g][m][i + 1] + b[m][i + 1];
-                if (RESID) {
-                    lo += bf_lo(resid[g][4 * s + q]);
-                    hi += bf_hi(resid[g][4 * s + q]);
-                }
-                dst[g][4 * s + q] = pack_bf16x2(fmaxf(lo, 0.0f), fmaxf(hi, 0.0f));
+                const int i = 8 * (s & 1) + 2 * q;
+                // bias of accumulator rows i, i+1: channels 32m + 8(i>>2) + 4h + (i&3), +1
+                const f32x2 bb = *reinterpret_cast<const f32x2 *>(bias + 32 * (s >> 1) + 8 * (i >> 2) + 4 * h + (i & 3));
+                f32x2 v = f32x2{acc[g][s >> 1][i], acc[g][s >> 1][i + 1]} + bb;
+                if (RESID)
+                    v += f32x2{bf_lo(res[g][4 * s + q]), bf_hi(res[g][4 * s + q])};
+                // ReLU on the packed bf16 pair as signed int16 (negative bf16 <=> negative int16)
+                const i16x2 p = __builtin_bit_cast(i16x2, __builtin_convertvector(v, bf16x2_t));   // one v_cvt_pk_bf16_f32
+                act[g][4 * s + q] = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(p, i16x2{0, 0}));
             }
+    }
 }
 
 // LDS-DMA of one layer block (frags x 1 KiB) into an LDS buffer: wave w moves fragments w, w+4, ...
@@ -210,7 +204,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_resnet_q(const int8_t *__restri
     const uint16_t *head_lds = reinterpret_cast<const uint16_t *>(lds + 2 * kBufFrags * 64);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int h = lane >> 5, cell = lane & 15;
-    const bool col0 = (lane & 3) == 0, col3 = (lane & 3) == 3;
+    const uint32_t keep_l = (lane & 3) == 0 ? 0u : ~0u, keep_r = (lane & 3) == 3 ? 0u : ~0u;
     const int64_t tiles = (n + kBoardsPerTile - 1) / kBoardsPerTile;
 
     // head weights once per workgroup; first stem block into buffer 0
@@ -247,8 +241,8 @@ __global__ __launch_bounds__(kThreads, 1) void k_resnet_q(const int8_t *__restri
         __builtin_amdgcn_s_waitcnt(0);                 // vmcnt(0) lgkmcnt(0): this wave's DMA done
         __syncthreads();
         stage_block(blob + kStemBlock * 64, buf(cur ^ 1), kConvBlock, wave, lane);
-        conv_layer<2>(buf(cur), act, acc, lane, col0, col3);
-        epilogue<false>(acc, reinterpret_cast<const float *>(buf(cur) + kStemFrags * 64), h, res, act);
+        layer<2, false, false>(buf(cur), reinterpret_cast<const float *>(buf(cur) + kStemFrags * 64), act, res, acc,
+                               lane, h, keep_l, keep_r);
         // ---- 8 convs = 4 basic blocks
         for (int L = 0; L < kConvLayers; ++L) {
             cur ^= 1;
@@ -260,18 +254,10 @@ __global__ __launch_bounds__(kThreads, 1) void k_resnet_q(const int8_t *__restri
             else if (tile + gridDim.x < tiles)
                 stage_block(blob, buf(cur ^ 1), kStemBlock, wave, lane);
             const float *bias = reinterpret_cast<const float *>(buf(cur) + kConvFrags * 64);
-            if ((L & 1) == 0) {                      // first conv of a block: keep its input for the skip
-#pragma unroll
-                for (int g = 0; g < G; g++)
-#pragma unroll
-                    for (int k = 0; k < 16; k++)
-                        res[g][k] = act[g][k];
-                conv_layer<4>(buf(cur), act, acc, lane, col0, col3);
-                epilogue<false>(acc, bias, h, res, act);
-            } else {
-                conv_layer<4>(buf(cur), act, acc, lane, col0, col3);
-                epilogue<true>(acc, bias, h, res, act);
-            }
+            if ((L & 1) == 0)                        // first conv of a block: keep its input for the skip
+                layer<4, false, true>(buf(cur), bias, act, res, acc, lane, h, keep_l, keep_r);
+            else
+                layer<4, true, false>(buf(cur), bias, act, res, acc, lane, h, keep_l, keep_r);
         }
         // ---- head: per-lane partial dot products over the lane's 32 channels, then sum over the
         // 16 cells (DPP row) and the two halves
