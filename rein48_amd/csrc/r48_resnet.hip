@@ -108,8 +108,53 @@ __device__ __forceinline__ void tap_mfma(const uint4 *wl, int s, const uint32_t 
     }
 }
 
+// the same tap for ONE column group (the last k-chunk runs group by group)
+template <int DR, int DC, int NCH>
+__device__ __forceinline__ void tap_mfma1(const uint4 *wl, int s, const uint32_t (&xs)[3][4], f32x16 &a0, f32x16 &a1,
+                                          int lane)
+{
+    constexpr int t = (DR + 1) * 3 + (DC + 1);
+    const bf16x8 A0 = lds_frag(wl, (t * NCH + s) * 2 + 0, lane);
+    const bf16x8 A1 = lds_frag(wl, (t * NCH + s) * 2 + 1, lane);
+    uint32_t r[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+        r[q] = cell_shift<4 * DR>(xs[DC + 1][q]);
+    bf16x8 B;
+    __builtin_memcpy(&B, r, 16);
+    a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A0, B, a0, 0, 0, 0);
+    a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A1, B, a1, 0, 0, 0);
+}
+
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef short i16x2 __attribute__((ext_vector_type(2)));
+
+// bias (+ residual) + ReLU of one column group -> packed bf16 activations; SAVE first keeps
+// the layer input in res for the block's skip connection
+template <bool RESID, bool SAVE>
+__device__ __forceinline__ void epilogue1(const f32x16 (&acc)[2], const float *bias, int h, uint32_t (&act)[16],
+                                          uint32_t (&res)[16])
+{
+    if (SAVE) {
+#pragma unroll
+        for (int k = 0; k < 16; k++)
+            res[k] = act[k];
+    }
+#pragma unroll
+    for (int s = 0; s < 4; s++)
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int i = 8 * (s & 1) + 2 * q;
+            // bias of accumulator rows i, i+1: channels 32m + 8(i>>2) + 4h + (i&3), +1
+            const f32x2 bb = *reinterpret_cast<const f32x2 *>(bias + 32 * (s >> 1) + 8 * (i >> 2) + 4 * h + (i & 3));
+            f32x2 v = f32x2{acc[s >> 1][i], acc[s >> 1][i + 1]} + bb;
+            if (RESID)
+                v += f32x2{bf_lo(res[4 * s + q]), bf_hi(res[4 * s + q])};
+            // ReLU on the packed bf16 pair as signed int16 (negative bf16 <=> negative int16)
+            const i16x2 p = __builtin_bit_cast(i16x2, __builtin_convertvector(v, bf16x2_t));   // one v_cvt_pk_bf16_f32
+            act[4 * s + q] = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(p, i16x2{0, 0}));
+        }
+}
 
 // One conv layer: k-chunk by k-chunk, the column-shifted copies x[p-1] (zero on the left edge),
 // x[p], x[p+1] (zero on the right edge) of every group are built once and each of the 9 taps
@@ -129,7 +174,7 @@ __device__ __forceinline__ void layer(const uint4 *wl, const float *bias, uint32
     for (int g = 0; g < G; g++)
         acc[g][0] = acc[g][1] = f32x16{};
 #pragma unroll
-    for (int s = 0; s < NCH; s++) {
+    for (int s = 0; s < NCH - 1; s++) {
         uint32_t xs[G][3][4];
 #pragma unroll
         for (int g = 0; g < G; g++)
@@ -150,27 +195,29 @@ __device__ __forceinline__ void layer(const uint4 *wl, const float *bias, uint32
         tap_mfma<1, 0, NCH>(wl, s, xs, acc, lane);
         tap_mfma<1, 1, NCH>(wl, s, xs, acc, lane);
     }
+    // last k-chunk group by group, each group's epilogue right behind its last MFMAs so the
+    // scheduler can run it under the next group's MFMAs
+    constexpr int s = NCH - 1;
 #pragma unroll
     for (int g = 0; g < G; g++) {
-        if (SAVE) {
+        uint32_t xs[3][4];
 #pragma unroll
-            for (int k = 0; k < 16; k++)
-                res[g][k] = act[g][k];
+        for (int q = 0; q < 4; q++) {
+            const uint32_t x = act[g][4 * s + q];
+            xs[0][q] = cell_shift<-1>(x) & keep_l;
+            xs[1][q] = x;
+            xs[2][q] = cell_shift<1>(x) & keep_r;
         }
-#pragma unroll
-        for (int s = 0; s < 4; s++)
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const int i = 8 * (s & 1) + 2 * q;
-                // bias of accumulator rows i, i+1: channels 32m + 8(i>>2) + 4h + (i&3), +1
-                const f32x2 bb = *reinterpret_cast<const f32x2 *>(bias + 32 * (s >> 1) + 8 * (i >> 2) + 4 * h + (i & 3));
-                f32x2 v = f32x2{acc[g][s >> 1][i], acc[g][s >> 1][i + 1]} + bb;
-                if (RESID)
-                    v += f32x2{bf_lo(res[g][4 * s + q]), bf_hi(res[g][4 * s + q])};
-                // ReLU on the packed bf16 pair as signed int16 (negative bf16 <=> negative int16)
-                const i16x2 p = __builtin_bit_cast(i16x2, __builtin_convertvector(v, bf16x2_t));   // one v_cvt_pk_bf16_f32
-                act[g][4 * s + q] = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(p, i16x2{0, 0}));
-            }
+        tap_mfma1<-1, -1, NCH>(wl, s, xs, acc[g][0], acc[g][1], lane);
+        tap_mfma1<-1, 0, NCH>(wl, s, xs, acc[g][0], acc[g][1], lane);
+        tap_mfma1<-1, 1, NCH>(wl, s, xs, acc[g][0], acc[g][1], lane);
+        tap_mfma1<0, -1, NCH>(wl, s, xs, acc[g][0], acc[g][1], lane);
+        tap_mfma1<0, 0, NCH>(wl, s, xs, acc[g][0], acc[g][1], lane);
+        tap_mfma1<0, 1, NCH>(wl, s, xs, acc[g][0], acc[g][1], lane);
+        tap_mfma1<1, -1, NCH>(wl, s, xs, acc[g][0], acc[g][1], lane);
+        tap_mfma1<1, 0, NCH>(wl, s, xs, acc[g][0], acc[g][1], lane);
+        tap_mfma1<1, 1, NCH>(wl, s, xs, acc[g][0], acc[g][1], lane);
+        epilogue1<RESID, SAVE>(acc[g], bias, h, act[g], res[g]);
     }
 }
 
