@@ -69,10 +69,21 @@ def _maps(channels, planes=18):
     return _MAPS[key]
 
 
+_DEV_MAPS = {}
+
+
+def _dev_index(idx, dev):
+    """Device copy of an index map, made once per (map, device); -1 entries stay -1."""
+    key = (id(idx), str(dev))
+    if key not in _DEV_MAPS:
+        _DEV_MAPS[key] = torch.as_tensor(np.ascontiguousarray(idx).reshape(-1), device=dev)
+    return _DEV_MAPS[key]
+
+
 def _gather(flat, idx, dev):
     """flat[idx] with idx < 0 -> 0 (bf16 out)."""
     ext = torch.cat([flat, torch.zeros(1, dtype=flat.dtype, device=dev)])
-    it = torch.as_tensor(idx, device=dev)
+    it = _dev_index(idx, dev)
     return ext[torch.where(it < 0, ext.numel() - 1, it)].to(torch.bfloat16)
 
 
@@ -97,7 +108,7 @@ def pack_resnet(net):
         parts += [_gather(w.reshape(-1), cv, dev).reshape(-1), _bias_frag(b, dev)]
     blob = torch.cat(parts).contiguous()
     assert blob.numel() * 2 == _lib.load().r48_resnet_q_blob_bytes()
-    head_w = _gather(hw.reshape(-1), hd.reshape(-1), dev).contiguous()
+    head_w = _gather(hw.reshape(-1), hd, dev).contiguous()
     return blob, head_w, hb.float().contiguous()
 
 

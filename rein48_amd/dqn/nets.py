@@ -25,38 +25,54 @@ import torch.nn.functional as F
 from ..a3c.nets import linear
 from .kernels import PLANES
 
-_MAPS = {}
+_BLOCKS = {}
 
 
-def conv_scatter_map(co, ci, device):
-    """(rows, cols, src) index lists placing a [co, ci, 3, 3] kernel into the [16 co, 16 ci]
-    dense matrix of a pad-1 3x3 conv on the 4x4 grid."""
-    key = (co, ci, str(device))
-    if key not in _MAPS:
-        rows, cols, src = [], [], []
-        o = torch.arange(co).view(-1, 1).expand(co, ci).reshape(-1)
-        i = torch.arange(ci).view(1, -1).expand(co, ci).reshape(-1)
+def _tap_blocks(device):
+    """The 100 in-grid (cell p, tap t) pairs of a pad-1 3x3 conv on the 4x4 grid as index
+    tensors P (output cell), Q (input cell p + 4dr + dc) and T (tap (dr+1)*3 + (dc+1))."""
+    key = str(device)
+    if key not in _BLOCKS:
+        P, Q, T = [], [], []
         for p in range(16):
             r, c = divmod(p, 4)
             for dr in (-1, 0, 1):
                 for dc in (-1, 0, 1):
-                    rr, cc = r + dr, c + dc
-                    if 0 <= rr < 4 and 0 <= cc < 4:
-                        q = 4 * rr + cc
-                        rows.append(p * co + o)
-                        cols.append(q * ci + i)
-                        src.append(((o * ci + i) * 3 + (dr + 1)) * 3 + (dc + 1))
-        _MAPS[key] = tuple(torch.cat(t).to(device) for t in (rows, cols, src))
-    return _MAPS[key]
+                    if 0 <= r + dr < 4 and 0 <= c + dc < 4:
+                        P.append(p)
+                        Q.append(4 * (r + dr) + c + dc)
+                        T.append((dr + 1) * 3 + dc + 1)
+        _BLOCKS[key] = tuple(torch.tensor(v, dtype=torch.long, device=device) for v in (P, Q, T))
+    return _BLOCKS[key]
+
+
+class _StructuredConvWeight(torch.autograd.Function):
+    """w [co, ci, 3, 3] -> the [16 co, 16 ci] matrix of the conv on the 4x4 grid (block
+    (p, q) = w[:, :, dr + 1, dc + 1] for every in-grid pair). Backward sums each tap's 100
+    blocks with one index_add over 100 rows (no per-element scatter, no sort)."""
+
+    @staticmethod
+    def forward(ctx, w):
+        co, ci = w.shape[:2]
+        P, Q, T = _tap_blocks(w.device)
+        taps = w.permute(2, 3, 0, 1).reshape(9, co, ci)
+        d = torch.zeros(16, co, 16, ci, dtype=w.dtype, device=w.device)
+        d[P, :, Q, :] = taps[T]
+        ctx.shape = (co, ci)
+        return d.view(16 * co, 16 * ci)
+
+    @staticmethod
+    def backward(ctx, gd):
+        co, ci = ctx.shape
+        P, Q, T = _tap_blocks(gd.device)
+        blocks = gd.reshape(16, co, 16, ci)[P, :, Q, :]                       # [100, co, ci]
+        g9 = torch.zeros(9, co, ci, dtype=gd.dtype, device=gd.device).index_add_(0, T, blocks)
+        return g9.view(3, 3, co, ci).permute(2, 3, 0, 1).contiguous()
 
 
 def dense_conv_weight(conv):
     """[16 co, 16 ci] structured matrix of a Conv2d(ci, co, 3, padding=1) on the 4x4 grid."""
-    w = conv.weight
-    co, ci = w.shape[:2]
-    r, c, k = conv_scatter_map(co, ci, w.device)
-    d = torch.zeros(16 * co, 16 * ci, dtype=w.dtype, device=w.device)
-    return d.index_put((r, c), w.reshape(-1)[k])
+    return _StructuredConvWeight.apply(conv.weight)
 
 
 class ResNet10Q(nn.Module):
@@ -79,12 +95,16 @@ class ResNet10Q(nn.Module):
         return [self.stem, *self.convs]
 
     def _bn(self, k, h):
+        """BatchNorm per channel over (boards x cells): statistics and affine in the BN
+        parameters' dtype (fp32), activations stay in their own dtype (bf16 on the GPU path)."""
         if not self.use_bn:
             return h
         B = h.shape[0]
         bn = self.bns[k]
-        y = bn(h.to(bn.weight.dtype).reshape(B * 16, self.channels))      # fp32 (fp64 in tests)
-        return y.view(B, 16 * self.channels)
+        x = h.reshape(B * 16, self.channels)
+        if x.dtype != bn.weight.dtype and not x.is_cuda:
+            x = x.to(bn.weight.dtype)                   # CPU batch_norm needs matching dtypes
+        return bn(x).view(B, 16 * self.channels)
 
     def _conv(self, conv, h):
         return linear(h, dense_conv_weight(conv), conv.bias.repeat(16), self.dtype)
