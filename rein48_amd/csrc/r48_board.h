@@ -216,6 +216,27 @@ R48_HD uint32_t select_blank(const Blanks &b, uint32_t rank)
     return 4u * row + col;
 }
 
+// select_blank + place in one: the row of the rank-th blank is where the prefix counts
+// cross `rank`; the three comparisons are lane masks, so the row-hit masks are SGPR logic
+// and each row word takes one v_cndmask + v_or (no row index, no per-row compares).
+R48_HD void spawn_at_rank(Board &r, const Blanks &b, uint32_t rank, uint32_t e, bool on)
+{
+    const bool s1 = rank >= b.p1, s2 = rank >= b.p2, s3 = rank >= b.p3;
+    const uint32_t base = sel(s3, b.p3, sel(s2, b.p2, sel(s1, b.p1, 0u)));
+    uint32_t z = sel(s3, b.z3, sel(s2, b.z2, sel(s1, b.z1, b.z0)));
+    uint32_t j = rank - base;
+    const uint32_t lo = popc(z & 0x8080u);
+    const bool hi = j >= lo;
+    j -= hi ? lo : 0u;
+    z = hi ? (z >> 16) : z;
+    const uint32_t col = (hi ? 2u : 0u) + ((j >= ((z >> 7) & 1u)) ? 1u : 0u);
+    const uint32_t v = (e & (0u - (uint32_t)on)) << (8u * col);   // arithmetic, not a select: no branch
+    r.w0 |= sel(!s1, v, 0u);
+    r.w1 |= sel(s1 && !s2, v, 0u);
+    r.w2 |= sel(s2 && !s3, v, 0u);
+    r.w3 |= sel(s3, v, 0u);
+}
+
 // Put exponent e (1 = tile 2, 2 = tile 4) into cell `cell` when `on` (GameClient.py:125).
 R48_HD void place(Board &r, uint32_t cell, uint32_t e, bool on)
 {
@@ -250,15 +271,36 @@ R48_HD uint32_t row_sum(uint32_t w)
 
 R48_HD uint32_t tile_sum(const Board &r) { return row_sum(r.w0) + row_sum(r.w1) + row_sum(r.w2) + row_sum(r.w3); }
 
+// a ^ b ^ k with k wave-uniform: ONE v_bitop3_b32 (the compiler emits two v_xor_b32 when one
+// operand is an SGPR)
+R48_HD uint32_t xor3_uniform(uint32_t a, uint32_t b, uint32_t k)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "s"(k));
+    return r;
+#else
+    return a ^ b ^ k;
+#endif
+}
+
 // ---- Philox4x32-10 (Salmon, Moraes, Dror, Shaw, SC'11) -----------------------------
+// Round 0 stays in C so the compiler can move its wave-uniform counter words to the SALU;
+// rounds 1-9 fold each round's two XORs into one v_bitop3_b32.
 R48_HD void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1)
 {
     R48_UNROLL
     for (int i = 0; i < 10; i++) {
         const uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
         const uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
-        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0;
-        const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1;
+        uint32_t n0, n2;
+        if (i == 0) {
+            n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0;
+            n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1;
+        } else {
+            n0 = xor3_uniform((uint32_t)(p1 >> 32), c[1], k0);
+            n2 = xor3_uniform((uint32_t)(p0 >> 32), c[3], k1);
+        }
         c[1] = (uint32_t)p1;
         c[3] = (uint32_t)p0;
         c[0] = n0;
@@ -281,12 +323,14 @@ struct StepOut {
 
 // One env step on registers (Game.step, GameClient.py:40-51) given the action and the
 // two spawn draws. `rank_word` is either a Philox word (rank = mulhi(word, n_blank)) or,
-// when RANK_IS_INDEX, the injected rank itself (taken modulo n_blank).
-template <bool REWARD, bool RANK_IS_INDEX>
+// when RANK_IS_INDEX, the injected rank itself (taken modulo n_blank). VALID_ACTION: the
+// caller guarantees a < 4 (in-kernel random policy), so the moved board is taken as is -- an
+// unchanged move maps back to the same board (from_lines inverts to_lines exactly).
+template <bool REWARD, bool RANK_IS_INDEX, bool VALID_ACTION = false>
 R48_HD StepOut step_board(Board &r, uint32_t a, uint32_t rank_word, bool four)
 {
     StepOut o;
-    const bool valid = a < 4u;
+    const bool valid = VALID_ACTION || a < 4u;
     const uint32_t ac = a & 3u;
     Board L = to_lines(r, ac);
     const Board L0 = L;
@@ -294,8 +338,11 @@ R48_HD StepOut step_board(Board &r, uint32_t a, uint32_t rank_word, bool four)
     const uint32_t diff = (L.w0 ^ L0.w0) | (L.w1 ^ L0.w1) | (L.w2 ^ L0.w2) | (L.w3 ^ L0.w3);
     const bool changed = valid && diff != 0u;
     const Board moved = from_lines(L, ac);
-    r = Board{sel(changed, moved.w0, r.w0), sel(changed, moved.w1, r.w1), sel(changed, moved.w2, r.w2),
-              sel(changed, moved.w3, r.w3)};
+    if (VALID_ACTION)
+        r = moved;
+    else
+        r = Board{sel(changed, moved.w0, r.w0), sel(changed, moved.w1, r.w1), sel(changed, moved.w2, r.w2),
+                  sel(changed, moved.w3, r.w3)};
     o.reward = changed ? o.reward : 0u;
     const Blanks bl = blanks(r);
     o.n_blank = bl.n;
@@ -304,8 +351,7 @@ R48_HD StepOut step_board(Board &r, uint32_t a, uint32_t rank_word, bool four)
         rank = bl.n ? rank_word % bl.n : 0u;
     else
         rank = mulhi(rank_word, bl.n);
-    const uint32_t cell = select_blank(bl, rank);
-    place(r, cell, four ? 2u : 1u, changed);
+    spawn_at_rank(r, bl, rank, four ? 2u : 1u, changed);
     o.changed = changed;
     o.done = game_over(r, bl.n - (changed ? 1u : 0u));
     return o;

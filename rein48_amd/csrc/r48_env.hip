@@ -63,7 +63,7 @@ struct LaneOut {
     uint32_t a, done, changed, reward, score;
 };
 
-template <bool RANDOM, bool AUTO_RESET, bool REWARD>
+template <bool RANDOM, bool AUTO_RESET, bool REWARD, bool RESET_BRANCH = true>
 __device__ __forceinline__ LaneOut step_lane(Board b, int64_t i, int64_t gid0, uint32_t k0, uint32_t k1,
                                              uint32_t step, const int8_t *actions, bool want_score,
                                              unsigned long long *err)
@@ -77,10 +77,17 @@ __device__ __forceinline__ LaneOut step_lane(Board b, int64_t i, int64_t gid0, u
         r.a = (uint32_t)(uint8_t)actions[i];
         count_bad(r.a > 3u, err);
     }
-    const r48::StepOut o = r48::step_board<REWARD, false>(b, r.a, w[1], w[2] < r48::kFourThresh);
+    const r48::StepOut o = r48::step_board<REWARD, false, RANDOM>(b, r.a, w[1], w[2] < r48::kFourThresh);
     r.score = want_score ? r48::tile_sum(b) : 0u;
-    if (AUTO_RESET && o.done)
-        r48::reset_board(b, w[3] >> 28, (w[3] & 0x0FFFFFFFu) < r48::kFourThresh28);
+    // auto-reset: ~1 board-step in 140 is done, so most waves skip it (wave-uniform branch).
+    // Inside a multi-board tile (RESET_BRANCH = false) the branch would split the straight-line
+    // load/compute pipeline, so there it is a select.
+    if (AUTO_RESET && (RESET_BRANCH ? __ballot(o.done) != 0 : true)) {
+        Board z;
+        r48::reset_board(z, w[3] >> 28, (w[3] & 0x0FFFFFFFu) < r48::kFourThresh28);
+        b = Board{r48::sel(o.done, z.w0, b.w0), r48::sel(o.done, z.w1, b.w1), r48::sel(o.done, z.w2, b.w2),
+                  r48::sel(o.done, z.w3, b.w3)};
+    }
     r.b = b;
     r.done = o.done;
     r.changed = o.changed;
@@ -133,8 +140,8 @@ __global__ __launch_bounds__(kBlock) void k_step(int8_t *__restrict__ boards, in
         LaneOut r[B];
 #pragma unroll
         for (int j = 0; j < B; j++)
-            r[j] = step_lane<RANDOM, AUTO_RESET, REWARD>(b[j], base + kBlock * j, gid0, k0, k1, step, actions,
-                                                         want_score, err);
+            r[j] = step_lane<RANDOM, AUTO_RESET, REWARD, (B == 1)>(b[j], base + kBlock * j, gid0, k0, k1, step,
+                                                                   actions, want_score, err);
 #pragma unroll
         for (int j = 0; j < B; j++)
             emit<RANDOM, REWARD>(r[j], base + kBlock * j, boards, actions, done, changed, reward, score);
