@@ -316,8 +316,8 @@ def main():
                    % world, "graph_chunk": chunk},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic_from_profile(n),
-                     "kernel": "k_step<RANDOM=1,AUTO_RESET=1,REWARD=0,B=%d>" % (4 if n // (2 if n >= (1 << 18) else 1)
-                                                                                 >= (1 << 22) else 1),
+                     "kernel": "k_step<RANDOM=1,AUTO_RESET=1,REWARD=0,NP=1> (one board pair per lane, "
+                               "one Philox4x32-10 call per pair)",
                      "algorithmic_bytes_per_step": bytes_per_launch,
                      "step_ms_device_events_timed_region": step_ms_dev,
                      "chains": 2 if n >= (1 << 18) else 1,

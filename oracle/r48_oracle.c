@@ -376,8 +376,12 @@ static inline uint32_t mulhi32(uint32_t a, uint32_t b)
     return (uint32_t)(((uint64_t)a * b) >> 32);
 }
 
-/* Batched step in the kernel's Philox mode (r48_env_step). actions are read, or written in
- * random-policy mode. Outputs may be NULL. Returns the number of boards with a bad action. */
+/* Batched step in the kernel's Philox mode (r48_env_step; draw contract in DESIGN.md section 7):
+ * boards with global ids 2q and 2q+1 share Philox4x32-10({q lo, q hi, step, 0x2048}); the even
+ * board takes (x, y) = (w0, w1), the odd one (w2, w3). action = x >> 30, spawn a 4 iff
+ * (x & 0x3FFFFFFF) < 0x06666666, blank rank = mulhi(y, n_blank), auto-reset cell = y >> 28 with
+ * a 4 iff (y & 0x0FFFFFFF) < 0x0199999A. actions are read, or written in random-policy mode.
+ * Outputs may be NULL. Returns the number of boards with a bad action. */
 ORC_API int64_t orc_step_philox(int8_t *boards, int64_t n, uint64_t seed, int64_t board_offset,
                                 uint32_t step, uint32_t flags, int8_t *actions, uint8_t *done,
                                 uint8_t *changed, int32_t *reward, int32_t *score)
@@ -386,12 +390,14 @@ ORC_API int64_t orc_step_philox(int8_t *boards, int64_t n, uint64_t seed, int64_
     const uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
     for (int64_t i = 0; i < n; i++) {
         int8_t *b = boards + 16 * i;
-        uint64_t gid = (uint64_t)(board_offset + i);
-        uint32_t ctr[4] = {(uint32_t)gid, (uint32_t)(gid >> 32), step, 0x2048u}, w[4];
+        /* boards 2q and 2q+1 share one Philox call; the even one takes (w0, w1), the odd one (w2, w3) */
+        uint64_t gid = (uint64_t)(board_offset + i), q = gid >> 1;
+        uint32_t ctr[4] = {(uint32_t)q, (uint32_t)(q >> 32), step, 0x2048u}, w[4];
         orc_philox4x32_10(ctr, key, w);
+        const uint32_t x = w[2 * (gid & 1)], y = w[2 * (gid & 1) + 1];
         int a;
         if (flags & ORC_FLAG_RANDOM_POLICY) {
-            a = (int)(w[0] >> 30);
+            a = (int)(x >> 30);
             if (actions)
                 actions[i] = (int8_t)a;
         } else {
@@ -405,7 +411,7 @@ ORC_API int64_t orc_step_philox(int8_t *boards, int64_t n, uint64_t seed, int64_
         }
         if (c) {
             int nb = orc_blank_count(b);
-            orc_spawn(b, (int)mulhi32(w[1], (uint32_t)nb), w[2] < 0x1999999Au);
+            orc_spawn(b, (int)mulhi32(y, (uint32_t)nb), (x & 0x3FFFFFFFu) < 0x06666666u);
         }
         int d = orc_game_over(b);
         if (score) {
@@ -414,9 +420,9 @@ ORC_API int64_t orc_step_philox(int8_t *boards, int64_t n, uint64_t seed, int64_
                 sc += b[k] ? (1 << b[k]) : 0;
             score[i] = sc;
         }
-        if (d && (flags & ORC_FLAG_AUTO_RESET)) {
+        if (d && (flags & ORC_FLAG_AUTO_RESET)) {   /* y is unused by a step that ends done */
             memset(b, 0, 16);
-            b[w[3] >> 28] = ((w[3] & 0x0FFFFFFFu) < 0x0199999Au) ? 2 : 1;
+            b[y >> 28] = ((y & 0x0FFFFFFFu) < 0x0199999Au) ? 2 : 1;
         }
         if (done)
             done[i] = (uint8_t)d;

@@ -41,16 +41,19 @@ class _SplitKLinear(torch.autograd.Function):
         acc = torch.float64 if x.dtype == torch.float64 else torch.float32  # bf16 partials sum in fp32
         gx = gy @ w
         rows = x.shape[0]
+        # bf16 on the GPU: the per-chunk partial products come out of hipBLASLt in fp32
+        # (bmm out_dtype), so no bf16 rounding of partials and no cast pass
+        f32_out = gy.is_cuda and gy.dtype == torch.bfloat16
         if rows >= SPLITK_MIN_ROWS:
             s = min(1024, rows // 8192)
             main = (rows // s) * s
-            gw = torch.bmm(gy[:main].view(s, -1, gy.shape[1]).transpose(1, 2),
-                           x[:main].view(s, -1, x.shape[1])).to(acc).sum(0)
+            a, b = gy[:main].view(s, -1, gy.shape[1]).transpose(1, 2), x[:main].view(s, -1, x.shape[1])
+            gw = (torch.bmm(a, b, out_dtype=acc) if f32_out else torch.bmm(a, b).to(acc)).sum(0)
             if main < rows:
                 gw += (gy[main:].t() @ x[main:]).to(acc)
         else:
             gw = (gy.t() @ x).to(acc)
-        gb = gy.to(acc).sum(0) if ctx.has_bias else None
+        gb = gy.sum(0, dtype=acc) if ctx.has_bias else None     # fp32 accumulation, no cast copy
         return gx, gw.to(w.dtype), (gb.to(w.dtype) if gb is not None else None)
 
 

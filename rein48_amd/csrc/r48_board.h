@@ -315,6 +315,7 @@ static constexpr uint32_t kStepTag = 0x2048u;
 static constexpr uint32_t kResetTag = 0x5E7u;
 static constexpr uint32_t kFillTag = 0xF111u;   // synthetic start boards (r48_env_fill_random)
 static constexpr uint32_t kFourThresh = 0x1999999Au;     // P(4) = 0.1   (GameClient.py:125)
+static constexpr uint32_t kFourThresh30 = 0x06666666u;   // same on 30 bits (P = 0.1 - 4e-10)
 static constexpr uint32_t kFourThresh28 = 0x0199999Au;   // same on 28 bits
 
 struct StepOut {

@@ -58,33 +58,58 @@ __device__ __forceinline__ void count_bad(bool bad, unsigned long long *err)
 }
 
 // ---------------------------------------------------------------- Philox-mode step
+// Draw contract (oracle/r48_oracle.c orc_step_philox): boards 2q and 2q+1
+// (global ids) share one Philox4x32-10(key = seed, counter = {q lo, q hi, step, kStepTag});
+// board 2q takes (x, y) = (w0, w1), board 2q+1 takes (w2, w3). Per board: action = x >> 30
+// (random policy), spawn tile 4 iff (x & 0x3FFFFFFF) < kFourThresh30, blank rank =
+// mulhi(y, n_blank); auto-reset cell = y >> 28, 4 iff (y & 0x0FFFFFFF) < kFourThresh28. A board
+// is only done when its spawn had at most one blank (mulhi(y, n) = 0 for n <= 1) or no spawn,
+// so y carried no information into that step and its bits are free for the reset.
+struct Draw {
+    uint32_t x, y;
+};
+
+__device__ __forceinline__ void pair_draws(uint64_t q, uint32_t step, uint32_t k0, uint32_t k1, Draw &even,
+                                           Draw &odd)
+{
+    uint32_t w[4];
+    philox_words(w, q, step, r48::kStepTag, k0, k1);
+    even = Draw{w[0], w[1]};
+    odd = Draw{w[2], w[3]};
+}
+
+__device__ __forceinline__ Draw board_draw(uint64_t gid, uint32_t step, uint32_t k0, uint32_t k1)
+{
+    Draw e, o;
+    pair_draws(gid >> 1, step, k0, k1, e, o);
+    return (gid & 1u) ? o : e;
+}
+
 struct LaneOut {
     Board b;
     uint32_t a, done, changed, reward, score;
 };
 
 template <bool RANDOM, bool AUTO_RESET, bool REWARD, bool RESET_BRANCH = true>
-__device__ __forceinline__ LaneOut step_lane(Board b, int64_t i, int64_t gid0, uint32_t k0, uint32_t k1,
-                                             uint32_t step, const int8_t *actions, bool want_score,
+__device__ __forceinline__ LaneOut step_lane(Board b, int64_t i, Draw d, const int8_t *actions, bool want_score,
                                              unsigned long long *err)
 {
     LaneOut r;
-    uint32_t w[4];
-    philox_words(w, (uint64_t)(gid0 + i), step, r48::kStepTag, k0, k1);
     if (RANDOM) {
-        r.a = w[0] >> 30;  // uniform over {UP, DOWN, LEFT, RIGHT} (control/rand.py:9-11)
+        r.a = d.x >> 30;  // uniform over {UP, DOWN, LEFT, RIGHT} (control/rand.py:9-11)
     } else {
         r.a = (uint32_t)(uint8_t)actions[i];
         count_bad(r.a > 3u, err);
     }
-    const r48::StepOut o = r48::step_board<REWARD, false, RANDOM>(b, r.a, w[1], w[2] < r48::kFourThresh);
+    const r48::StepOut o =
+        r48::step_board<REWARD, false, RANDOM>(b, r.a, d.y, (d.x & 0x3FFFFFFFu) < r48::kFourThresh30);
     r.score = want_score ? r48::tile_sum(b) : 0u;
     // auto-reset: ~1 board-step in 140 is done, so most waves skip it (wave-uniform branch).
     // Inside a multi-board tile (RESET_BRANCH = false) the branch would split the straight-line
     // load/compute pipeline, so there it is a select.
     if (AUTO_RESET && (RESET_BRANCH ? __ballot(o.done) != 0 : true)) {
         Board z;
-        r48::reset_board(z, w[3] >> 28, (w[3] & 0x0FFFFFFFu) < r48::kFourThresh28);
+        r48::reset_board(z, d.y >> 28, (d.y & 0x0FFFFFFFu) < r48::kFourThresh28);
         b = Board{r48::sel(o.done, z.w0, b.w0), r48::sel(o.done, z.w1, b.w1), r48::sel(o.done, z.w2, b.w2),
                   r48::sel(o.done, z.w3, b.w3)};
     }
@@ -116,12 +141,13 @@ __device__ __forceinline__ void emit(const LaneOut &r, int64_t i, int8_t *boards
 // replays: node k of a captured chunk carries step_arg = k and the launch function sets
 // *d_ctr to the env's counter with a memset before each replay).
 //
-// B boards per lane: a block owns a tile of kBlock*B boards, lane t board j = tile + t +
-// kBlock*j (each load/store instruction stays one contiguous 1 KiB per wave). Full tiles take
-// a straight-line path -- all B loads issued back to back, board j computed as soon as its
-// own load has landed (counted vmcnt), all stores at the end -- so a lane's later loads
-// overlap its earlier boards' compute. Only the grid's last, partial tile is guarded.
-template <bool RANDOM, bool AUTO_RESET, bool REWARD, int B>
+// NP board pairs per lane: a block owns a tile of 2 * NP * kBlock boards, lane t's pair j is
+// boards tile + 2 * kBlock * j + 2t and +1 (each pair = 32 contiguous bytes, a wave's pair slot
+// one contiguous 2 KiB), and ONE Philox call serves both boards of a pair. Full, pair-aligned
+// tiles take a straight-line path -- all loads issued back to back, each pair computed as soon
+// as its loads have landed, all stores at the end. The grid's partial last tile and envs whose
+// global board ids start odd (pairs straddling the tile) take the guarded per-board path.
+template <bool RANDOM, bool AUTO_RESET, bool REWARD, int NP>
 __global__ __launch_bounds__(kBlock) void k_step(int8_t *__restrict__ boards, int64_t n, int64_t gid0,
                                                  uint32_t k0, uint32_t k1, const uint32_t *__restrict__ d_ctr,
                                                  uint32_t step_arg, int8_t *__restrict__ actions,
@@ -129,28 +155,40 @@ __global__ __launch_bounds__(kBlock) void k_step(int8_t *__restrict__ boards, in
                                                  int32_t *__restrict__ reward, int32_t *__restrict__ score,
                                                  unsigned long long *err)
 {
-    const int64_t base = (int64_t)blockIdx.x * kBlock * B + threadIdx.x;
+    constexpr int64_t kTile = (int64_t)kBlock * 2 * NP;
+    const int64_t base = (int64_t)blockIdx.x * kTile + 2 * (int64_t)threadIdx.x;
     const uint32_t step = (d_ctr ? *d_ctr : 0u) + step_arg;
     const bool want_score = score != nullptr;
-    if ((int64_t)(blockIdx.x + 1) * kBlock * B <= n) {
-        Board b[B];
+    if ((int64_t)(blockIdx.x + 1) * kTile <= n && (gid0 & 1) == 0) {
+        Board b[2 * NP];
 #pragma unroll
-        for (int j = 0; j < B; j++)
-            b[j] = load_board(boards, base + kBlock * j);
-        LaneOut r[B];
+        for (int j = 0; j < NP; j++) {
+            b[2 * j] = load_board(boards, base + 2 * kBlock * j);
+            b[2 * j + 1] = load_board(boards, base + 2 * kBlock * j + 1);
+        }
+        LaneOut r[2 * NP];
 #pragma unroll
-        for (int j = 0; j < B; j++)
-            r[j] = step_lane<RANDOM, AUTO_RESET, REWARD, (B == 1)>(b[j], base + kBlock * j, gid0, k0, k1, step,
-                                                                   actions, want_score, err);
+        for (int j = 0; j < NP; j++) {
+            const int64_t i = base + 2 * kBlock * j;
+            Draw de, dd;
+            pair_draws((uint64_t)(gid0 + i) >> 1, step, k0, k1, de, dd);
+            r[2 * j] = step_lane<RANDOM, AUTO_RESET, REWARD, NP == 1>(b[2 * j], i, de, actions, want_score, err);
+            r[2 * j + 1] =
+                step_lane<RANDOM, AUTO_RESET, REWARD, NP == 1>(b[2 * j + 1], i + 1, dd, actions, want_score, err);
+        }
 #pragma unroll
-        for (int j = 0; j < B; j++)
-            emit<RANDOM, REWARD>(r[j], base + kBlock * j, boards, actions, done, changed, reward, score);
+        for (int j = 0; j < NP; j++) {
+            emit<RANDOM, REWARD>(r[2 * j], base + 2 * kBlock * j, boards, actions, done, changed, reward, score);
+            emit<RANDOM, REWARD>(r[2 * j + 1], base + 2 * kBlock * j + 1, boards, actions, done, changed, reward,
+                                 score);
+        }
     } else {
-        for (int j = 0; j < B; j++) {
-            const int64_t i = base + kBlock * j;
+        for (int j = 0; j < 2 * NP; j++) {
+            const int64_t i = base + 2 * kBlock * (j >> 1) + (j & 1);
             if (i < n) {
-                const LaneOut r = step_lane<RANDOM, AUTO_RESET, REWARD>(load_board(boards, i), i, gid0, k0, k1,
-                                                                        step, actions, want_score, err);
+                const Draw d = board_draw((uint64_t)(gid0 + i), step, k0, k1);
+                const LaneOut r = step_lane<RANDOM, AUTO_RESET, REWARD, false>(load_board(boards, i), i, d, actions,
+                                                                               want_score, err);
                 emit<RANDOM, REWARD>(r, i, boards, actions, done, changed, reward, score);
             }
         }
@@ -299,12 +337,11 @@ __global__ __launch_bounds__(kBlock) void k_rollout(int8_t *__restrict__ boards,
     Board b = load_board(boards, i);
     const uint64_t gid = (uint64_t)(gid0 + i);
     for (int32_t t = 0; t < n_steps; t++) {
-        uint32_t w[4];
-        philox_words(w, gid, step0 + (uint32_t)t, r48::kStepTag, k0, k1);
-        const uint32_t a = w[0] >> 30;
-        const r48::StepOut o = r48::step_board<false, false>(b, a, w[1], w[2] < r48::kFourThresh);
+        const Draw d = board_draw(gid, step0 + (uint32_t)t, k0, k1);   // the k_step contract
+        const uint32_t a = d.x >> 30;
+        const r48::StepOut o = r48::step_board<false, false, true>(b, a, d.y, (d.x & 0x3FFFFFFFu) < r48::kFourThresh30);
         if (o.done)
-            r48::reset_board(b, w[3] >> 28, (w[3] & 0x0FFFFFFFu) < r48::kFourThresh28);
+            r48::reset_board(b, d.y >> 28, (d.y & 0x0FFFFFFFu) < r48::kFourThresh28);
         if (actions)
             actions[(int64_t)t * n + i] = (int8_t)a;
         if (done)
@@ -660,8 +697,9 @@ int validate_step(const r48_env *env, const int8_t *actions, uint32_t flags)
 }
 
 // one k_step launch over boards [off, off+cnt) of the env; step counter =
-// (d_ctr ? *d_ctr : 0) + step_arg. Past 4M boards a lane takes 4 boards (memory-level
-// parallelism for HBM-resident sweeps); below, one board per lane keeps every CU busy.
+// (d_ctr ? *d_ctr : 0) + step_arg. A lane takes one board pair (one Philox call per two boards)
+// at every size: two pairs per lane measured slower even on the HBM-bound 2^26-board sweep
+// (437 vs 428-432 us per step), so only NP = 1 is instantiated.
 void launch_step(r48_env *env, int64_t off, int64_t cnt, const uint32_t *d_ctr, uint32_t step_arg,
                  int8_t *actions, uint32_t flags, uint8_t *done, uint8_t *changed, int32_t *reward, int32_t *score,
                  hipStream_t stream)
@@ -669,14 +707,14 @@ void launch_step(r48_env *env, int64_t off, int64_t cnt, const uint32_t *d_ctr, 
     const bool rnd = flags & R48_RANDOM_POLICY, ar = flags & R48_AUTO_RESET, rw = flags & R48_MERGE_REWARD;
     const uint32_t k0 = (uint32_t)env->seed, k1 = (uint32_t)(env->seed >> 32);
     auto at = [off](auto *p) { return p ? p + off : p; };
-    const bool wide = cnt >= ((int64_t)1 << 22);
-    auto go = [&](auto kern, int B) {
-        const dim3 grid((unsigned)((cnt + (int64_t)kBlock * B - 1) / ((int64_t)kBlock * B)));
+    auto go = [&](auto kern, int NP) {
+        const int64_t tile = (int64_t)kBlock * 2 * NP;
+        const dim3 grid((unsigned)((cnt + tile - 1) / tile));
         hipLaunchKernelGGL(kern, grid, dim3(kBlock), 0, stream, env->boards + 16 * off, cnt, env->gid0 + off, k0,
                            k1, d_ctr, step_arg, at(actions), at(done), at(changed), at(reward), at(score), env->err);
     };
-#define R48_GO(RN, AR, RW) wide ? go(k_step<RN, AR, RW, 4>, 4) : go(k_step<RN, AR, RW, 1>, 1)
-    // 16 instantiations: policy source x auto-reset x reward mode x boards per lane
+#define R48_GO(RN, AR, RW) go(k_step<RN, AR, RW, 1>, 1)
+    // 8 instantiations: policy source x auto-reset x reward mode
     if (rnd) {
         if (ar) rw ? R48_GO(true, true, true) : R48_GO(true, true, false);
         else rw ? R48_GO(true, false, true) : R48_GO(true, false, false);
@@ -720,7 +758,10 @@ int chain_graphs(r48_env *env, int32_t n_steps, int8_t *actions, uint32_t flags,
             return fail(R48_EHIP, "hipEventCreate failed");
     }
     for (int c = 0; c < chains; c++) {
-        const int64_t off = env->n * c / chains, cnt = env->n * (c + 1) / chains - off;
+        // shard boundaries on even board ids: every board pair stays inside one shard
+        const int64_t off = (env->n * c / chains) & ~(int64_t)1;
+        const int64_t end = c + 1 == chains ? env->n : (env->n * (c + 1) / chains) & ~(int64_t)1;
+        const int64_t cnt = end - off;
         const GraphKey key{c, n_steps, flags, {env->boards, actions, done, changed, reward, score}};
         auto it = env->graphs.find(key);
         if (it == env->graphs.end()) {

@@ -143,15 +143,17 @@ int main()
         for (uint32_t step = 7; step < 10; step++) {
             orc_step_philox(ob, n, seed, off, step, 1u | 2u, act, done, chg, rw, sc);
             for (int i = 0; i < n; i++) {
-                const uint64_t gid = (uint64_t)(off + i);
-                uint32_t w[4] = {(uint32_t)gid, (uint32_t)(gid >> 32), step, r48::kStepTag};
+                // pair contract: boards 2q, 2q+1 share one Philox call; even takes (w0, w1), odd (w2, w3)
+                const uint64_t gid = (uint64_t)(off + i), q = gid >> 1;
+                uint32_t w[4] = {(uint32_t)q, (uint32_t)(q >> 32), step, r48::kStepTag};
                 r48::philox4x32_10(w, (uint32_t)seed, (uint32_t)(seed >> 32));
-                const uint32_t a = w[0] >> 30;
+                const uint32_t x = w[2 * (gid & 1)], y = w[2 * (gid & 1) + 1];
+                const uint32_t a = x >> 30;
                 CHECK((int8_t)a == act[i], "philox action i=%d", i);
                 Board r = load(boards + 16 * i);
-                r48::StepOut s = r48::step_board<false, false>(r, a, w[1], w[2] < r48::kFourThresh);
+                r48::StepOut s = r48::step_board<false, false>(r, a, y, (x & 0x3FFFFFFFu) < r48::kFourThresh30);
                 CHECK((int32_t)r48::tile_sum(r) == sc[i], "score i=%d", i);
-                if (s.done) r48::reset_board(r, w[3] >> 28, (w[3] & 0x0FFFFFFFu) < r48::kFourThresh28);
+                if (s.done) r48::reset_board(r, y >> 28, (y & 0x0FFFFFFFu) < r48::kFourThresh28);
                 store(boards + 16 * i, r);
                 CHECK(memcmp(boards + 16 * i, ob + 16 * i, 16) == 0, "philox board i=%d step=%u", i, step);
                 CHECK(s.done == done[i] && s.changed == chg[i], "philox flags i=%d", i);

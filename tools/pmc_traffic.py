@@ -28,8 +28,8 @@ def per_dispatch(path_glob, counter):
             name = r.get("Kernel_Name", "")
             if r.get("Counter_Name") != counter or "k_step<" not in name:
                 continue
-            b = int(re.search(r"k_step<[^>]*?(\d+)>", name).group(1))  # boards per lane (template B)
-            key = (r.get("Dispatch_Id"), int(r.get("Grid_Size", r.get("Grid_Size_X"))) * b)
+            np_ = int(re.search(r"k_step<[^>]*?(\d+)>", name).group(1))  # board pairs per lane (template NP)
+            key = (r.get("Dispatch_Id"), int(r.get("Grid_Size", r.get("Grid_Size_X"))) * 2 * np_)
             vals[key] = vals.get(key, 0.0) + float(r["Counter_Value"])
     return vals
 

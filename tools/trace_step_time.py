@@ -24,7 +24,8 @@ def main():
     iv = []
     with open(a.trace) as f:
         for row in csv.DictReader(f):
-            if "k_step<" in row["Kernel_Name"] and int(row["Grid_Size_X"]) in (lanes, lanes // 4):
+            # one board pair per lane: a launch over `lanes` boards has lanes / 2 threads
+            if "k_step<" in row["Kernel_Name"] and int(row["Grid_Size_X"]) * 2 == lanes:
                 iv.append((int(row["Start_Timestamp"]), int(row["End_Timestamp"])))
     iv.sort()
     iv = iv[a.skip:]
