@@ -225,13 +225,23 @@ def traffic_from_profile(n_boards):
     return d.get("hbm_bytes_per_step")
 
 
+SETTLE_S = 0.1   # minimum untimed stepping before a timed region: GPU clocks ramp over ~20 ms+
+
+
 def timed_steps(env, plan, W, chunk, world, dev):
     """W untimed warm-up steps through the same replay path (in chunks of the timed chunk
-    size, so the timed region replays graphs that have already run), then exactly sum(plan)
-    steps bracketed by barrier + synchronize. -> (slowest rank's wall seconds, device ms from
-    HIP events on the launch stream)."""
+    size, so the timed region replays graphs that have already run) -- continued, still untimed,
+    until at least SETTLE_S of stepping has run -- then exactly sum(plan) steps bracketed by
+    barrier + synchronize. -> (slowest rank's wall seconds, device ms from HIP events on the
+    launch stream)."""
+    t_w = time.perf_counter()
     for c in chunks(W, chunk) if W else []:
         env.step_n(c, auto_reset=True)
+    if W:
+        torch.cuda.synchronize(dev)
+        while time.perf_counter() - t_w < SETTLE_S:
+            env.step_n(chunk, auto_reset=True)
+            torch.cuda.synchronize(dev)
     for c in sorted(set(plan)):
         env.prepare_step_n(c, auto_reset=True)
     s = torch.cuda.current_stream(dev)
@@ -255,8 +265,9 @@ def main():
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3000)
-    ap.add_argument("--warmup", type=int, default=3000,
-                    help="untimed steps (the GPU clock needs ~20 ms of load to settle)")
+    ap.add_argument("--warmup", type=int, default=10000,
+                    help="untimed steps; stepping continues untimed until %.0f ms have run (GPU clock ramp)"
+                    % (SETTLE_S * 1e3))
     ap.add_argument("--boards", type=int, default=1 << 20, help="boards per GPU")
     ap.add_argument("--chunk", type=int, default=4096, help="max steps per r48_env_step_n call (<= 4096)")
     ap.add_argument("--seed", type=int, default=0x20485EED)
@@ -330,7 +341,7 @@ def main():
         ex = extras(dev, args.seed, n)
         # median of 5 repeats of the same K-step region, and the reference
         # reset-distribution start (one tile per board) instead of the synthetic fill
-        reps = [timed_steps(env, plan, 0, chunk, world, dev)[0] for _ in range(5)]
+        reps = [timed_steps(env, plan, chunk, chunk, world, dev)[0] for _ in range(5)]   # each re-warmed
         ex["repeat_5"] = {"values": [n * K / r for r in reps], "median": n * K / sorted(reps)[2]}
         env2 = VecGame(n, device=dev, seed=args.seed, board_offset=offset)
         env2.reset()
