@@ -183,11 +183,12 @@ def test_drop_in_game_surface():
 
 
 # ---------------------------------------------------------------- Philox mode vs oracle
+@pytest.mark.parametrize("off", [12345, 1 << 20])   # odd: guarded per-board path; even: pair fast path
 @pytest.mark.parametrize("flags", [O.RANDOM_POLICY, O.RANDOM_POLICY | O.AUTO_RESET,
                                    O.RANDOM_POLICY | O.AUTO_RESET | O.MERGE_REWARD])
-def test_philox_random_policy_matches_oracle(flags):
+def test_philox_random_policy_matches_oracle(flags, off):
     rng = np.random.default_rng(flags)
-    n, seed, off = 100_003, 0x2048_5EED, 12345
+    n, seed = 100_003, 0x2048_5EED
     b0 = rand_boards(rng, n)
     v = vec(n, seed=seed, offset=off)
     put(v, b0)
@@ -302,7 +303,7 @@ def test_rollout_equals_repeated_steps():
     n, K, seed = 30_000, 37, 4242
     rng = np.random.default_rng(3)
     b0 = rand_boards(rng, n, emax=6, p_empty=0.4)
-    a, b = vec(n, seed=seed, offset=99), vec(n, seed=seed, offset=99)
+    a, b = vec(n, seed=seed, offset=98), vec(n, seed=seed, offset=98)   # even: k_step's pair fast path
     put(a, b0)
     put(b, b0)
     acts = torch.empty((K, n), dtype=torch.int8, device=DEV)
@@ -434,15 +435,16 @@ def test_step_n_graph_equals_repeated_steps():
     assert a.counters == b.counters
 
 
+@pytest.mark.parametrize("off", [3, 0])               # odd: guarded per-board path; even: pair fast path
 @pytest.mark.parametrize("n", [300_001, 9_000_003])
-def test_step_n_chains_and_wide_tiles_match_oracle(n):
-    """Large envs: r48_env_step_n splits the boards into 2 shard chains (>= 2^18 boards) and
-    uses 4 boards per lane past 4M boards per launch; odd sizes exercise the partial tile.
-    Result == eager steps == the oracle."""
+def test_step_n_chains_and_wide_tiles_match_oracle(n, off):
+    """Large envs: r48_env_step_n splits the boards into 2 shard chains (>= 2^18 boards, split
+    on an even board id); odd sizes exercise the partial tile. Result == eager steps == the
+    oracle, on both the pair fast path (even offset) and the guarded path (odd offset)."""
     seed = 4040
     rng = np.random.default_rng(n)
     b0 = rand_boards(rng, n, emax=6)
-    a, b = vec(n, seed=seed, offset=3), vec(n, seed=seed, offset=3)
+    a, b = vec(n, seed=seed, offset=off), vec(n, seed=seed, offset=off)
     put(a, b0)
     put(b, b0)
     a.step_n(2, auto_reset=True)
@@ -453,7 +455,7 @@ def test_step_n_chains_and_wide_tiles_match_oracle(n):
     assert torch.equal(a.done, b.done) and torch.equal(a.actions, b.actions)
     want = b0
     for t in range(4):
-        want = O.step_philox(want, seed, t, O.RANDOM_POLICY | O.AUTO_RESET, board_offset=3)["boards"]
+        want = O.step_philox(want, seed, t, O.RANDOM_POLICY | O.AUTO_RESET, board_offset=off)["boards"]
     assert np.array_equal(host(a.boards), want)
 
 
