@@ -186,6 +186,22 @@ int r48_cnn_policy_forward(const int8_t *boards, int64_t n, const void *wfrag, c
                            int32_t mode, float *logits, float *value, int8_t *actions, uint64_t seed,
                            int64_t gid0, uint32_t ctr, void *stream);
 
+/* Fused A3C update for the CNN (configs 3-4; rein48_amd/a3c/losses.py restating a3c.py:99-123):
+ * the gradient of (actor + critic) over `rows` training states w.r.t. every ActorCriticCNN
+ * parameter, in one pass with no activation written to memory. boards int8[rows][16], actions
+ * int8[rows], targets / wn float[rows] (wn = mask / (segment length * n)); reference-mode actor
+ * loss when cm != NULL: cm float[rows] (= coef * mask / n) and counts float[n_boards][4] (row r
+ * belongs to board r % n_boards); textbook otherwise. wfrag: 65 x 64 x 8 bf16 fragments and bias
+ * 104 floats from rein48_amd/a3c/fused.py:pack_cnn_train. workspace: r48_cnn_train_workspace_floats()
+ * floats; grad: r48_cnn_train_grad_floats() floats = dW2[64][128] | db2[64] | dW1[32][5] (col 4 =
+ * bias) | dWh[5][257] (col 256 = bias) | actor loss | critic loss. Deterministic. */
+int r48_cnn_train_grad(const int8_t *boards, int64_t rows, int64_t n_boards, const int8_t *actions,
+                       const float *targets, const float *wn, const float *cm, const float *counts,
+                       float beta, int32_t mode, const void *wfrag, const float *bias, float *workspace,
+                       float *grad, void *stream);
+int64_t r48_cnn_train_workspace_floats(void);
+int64_t r48_cnn_train_grad_floats(void);
+
 /* ---- Transition store for replay-based training (config 5; algorithm/ddpg/replay.py) ----
  * HBM-resident, structure of arrays, 38 B per transition: state int8[16], action int8,
  * reward float, next_state int8[16], done uint8. State pointers must be 16-byte aligned. */

@@ -25,6 +25,9 @@ REPLAY_RING, REPLAY_FILL_DRAIN = 0, 1
 # name -> (restype, argtypes); mirrors include/rein48.h one to one
 _P, _I32, _I64, _U32, _U64 = C.c_void_p, C.c_int32, C.c_int64, C.c_uint32, C.c_uint64
 SIGNATURES = {
+    "r48_cnn_train_grad": (C.c_int, [_P, _I64, _I64, _P, _P, _P, _P, _P, C.c_float, _I32, _P, _P, _P, _P, _P]),
+    "r48_cnn_train_workspace_floats": (_I64, []),
+    "r48_cnn_train_grad_floats": (_I64, []),
     "r48_resnet_q_forward": (C.c_int, [_P, _I64, _P, _P, _P, _P, _P, C.c_float, _U64, _I64, _U32, _P]),
     "r48_resnet_q_blob_bytes": (_I64, []),
     "r48_board_onehot": (C.c_int, [_P, _I64, _I32, _P, _P]),

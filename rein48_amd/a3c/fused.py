@@ -30,7 +30,24 @@ def _index_maps():
     return w1, w2, wh
 
 
+def _index_maps_backward():
+    """A fragments of the fused update's backward-data GEMMs (r48_a3c_train.hip):
+    Wh^T fragment (p, g) (8):       heads.w[o = 8h + j][64p + 32g + r]          (o >= 5: 0)
+    W2^T fragment (kk, g, s) (16):  conv2.w[32g + f(s, j, h)][32kk + r]"""
+    lane = np.arange(64)
+    r, h = lane & 31, lane >> 5
+    j = np.arange(8)
+    f_perm = lambda s: 16 * s + 8 * (j[None, :] >> 2) + 4 * h[:, None] + (j[None, :] & 3)   # [64, 8]
+    o = 8 * h[:, None] + j[None, :]
+    wht = np.stack([np.where(o < 5, o * 256 + 64 * p + 32 * g + r[:, None], -1)
+                    for p in range(4) for g in range(2)])
+    w2t = np.stack([(32 * g + f_perm(s)) * 128 + 32 * kk + r[:, None]
+                    for kk in range(4) for g in range(2) for s in range(2)])
+    return wht, w2t
+
+
 _MAPS = None
+_MAPS_BWD = None
 
 
 @torch.no_grad()
@@ -52,6 +69,58 @@ def pack_cnn(net):
     bias[32:96] = net.conv2.bias
     bias[96:101] = net.heads.bias
     return wfrag, bias
+
+
+@torch.no_grad()
+def pack_cnn_train(net):
+    """-> (wfrag bf16 [65, 64, 8], bias f32 [104]): pack_cnn's 41 forward fragments followed by
+    the 8 Wh^T and 16 W2^T fragments of the fused update."""
+    global _MAPS_BWD
+    if _MAPS_BWD is None:
+        _MAPS_BWD = _index_maps_backward()
+    wfrag, bias = pack_cnn(net)
+    dev = net.conv1.weight.device
+    wht_idx, w2t_idx = (torch.as_tensor(m, device=dev) for m in _MAPS_BWD)
+    hw = torch.cat([net.heads.weight.reshape(-1), torch.zeros(1, device=dev)])
+    fwht = hw[torch.where(wht_idx < 0, hw.numel() - 1, wht_idx)]
+    fw2t = net.conv2.weight.reshape(-1)[w2t_idx]
+    return torch.cat([wfrag, torch.cat([fwht, fw2t]).to(torch.bfloat16)]).contiguous(), bias
+
+
+GRAD_FLOATS = 9703   # r48_cnn_train_grad's record: dW2 [64][128] | db2 [64] | dW1 [32][5] | dWh [5][257] | losses [2]
+
+
+def cnn_train_grad(net, boards, actions, targets, wn, cm=None, counts=None, beta=0.001, exponents=False,
+                   n_boards=None, packed=None, workspace=None):
+    """Gradient of the A3C loss (rein48_amd/a3c/losses.py) over `rows` training states in ONE fused
+    pass (r48_cnn_train_grad). boards int8 [rows, 16]; actions int8 [rows]; targets, wn (= mask /
+    (B * n)) f32 [rows]; reference mode: cm (= coef * mask / n) f32 [rows] and counts f32
+    [n_boards, 4] (row r belongs to board r % n_boards). Returns (grads in net.parameters()
+    order, actor loss, critic loss)."""
+    L = _lib.load()
+    rows = boards.numel() // 16
+    dev = boards.device
+    for name, t, dt in (("boards", boards, torch.int8), ("actions", actions, torch.int8),
+                        ("targets", targets, torch.float32), ("wn", wn, torch.float32)):
+        if not t.is_cuda or t.dtype != dt or not t.is_contiguous():
+            raise ValueError("%s must be a contiguous %s GPU tensor" % (name, dt))
+    if (cm is None) != (counts is None):
+        raise ValueError("reference mode needs both cm and counts")
+    wfrag, bias = packed if packed is not None else pack_cnn_train(net)
+    if workspace is None:
+        workspace = torch.empty(L.r48_cnn_train_workspace_floats(), dtype=torch.float32, device=dev)
+    out = torch.empty(GRAD_FLOATS, dtype=torch.float32, device=dev)
+    check(L.r48_cnn_train_grad(ptr(boards), rows, int(n_boards or rows), ptr(actions), ptr(targets), ptr(wn), ptr(cm),
+                               ptr(counts), float(beta), _lib.FEAT_EXPONENTS if exponents else _lib.FEAT_VALUES,
+                               ptr(wfrag), ptr(bias), ptr(workspace), ptr(out),
+                               C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)))
+    dw2 = out[:64 * 128].view(64, 128)
+    db2 = out[8192:8256]
+    dw1 = out[8256:8416].view(32, 5)
+    dwh = out[8416:8416 + 5 * 257].view(5, 257)
+    grads = [dw1[:, :4].contiguous(), dw1[:, 4].contiguous(), dw2, db2, dwh[:, :256].contiguous(),
+             dwh[:, 256].contiguous()]
+    return grads, out[-2], out[-1]
 
 
 def cnn_forward(boards, wfrag, bias, exponents=False, logits=True, value=True, actions=False, seed=0, ctr=0,

@@ -22,12 +22,18 @@ from dataclasses import dataclass
 import torch
 import torch.distributed as dist
 
+from .. import _lib
+
 from ..env import VecGame
 from . import kernels as K
 from .fused import cnn_forward, pack_cnn
 from .losses import chunk_loss, segment_stats
 from .nets import make_net
 from .optim import FlatParams, RMSPropTF1
+
+
+def _lib_workspace_floats():
+    return _lib.load().r48_cnn_train_workspace_floats()
 
 
 @dataclass
@@ -44,6 +50,7 @@ class A3CConfig:
     update_chunk: int = 25        # time steps per forward/backward chunk of the update
     bf16: bool = False            # run the net's GEMMs in bf16 (MFMA, fp32 accumulate)
     fused_policy: bool = True     # cnn + bf16: rollout inference in one fused MFMA kernel (r48_policy.hip)
+    fused_update: bool = True     # cnn + bf16: the whole update's gradient in one fused pass (r48_a3c_train.hip)
 
 
 class A3CTrainer:
@@ -140,6 +147,15 @@ class A3CTrainer:
             targets = K.discounted_returns(self.rewards, self.lengths, boot, cfg.gamma,
                                            drop_last=cfg.mode == "reference")
             stats = segment_stats(v_all, targets, self.actions, self.mask)
+        if fused and cfg.fused_update:
+            # pass 2 as ONE fused MFMA kernel over all T x n states (no activation hits HBM)
+            actor_total, critic_total = self._fused_gradient(states, targets, stats)
+            self.flat.allreduce_grad(self.group)
+            self.opt.step()
+            self.updates += 1
+            return {"actor_loss": actor_total, "critic_loss": critic_total,
+                    "mean_length": float(self.lengths.float().mean()),
+                    "finished": float(self.finished.float().mean())}
         # pass 2: chunked forward/backward, gradients accumulate in the flat buffer
         self.flat.zero_grad()
         actor_total, critic_total = 0.0, 0.0
@@ -157,6 +173,31 @@ class A3CTrainer:
         return {"actor_loss": actor_total, "critic_loss": critic_total,
                 "mean_length": float(self.lengths.float().mean()),
                 "finished": float(self.finished.float().mean())}
+
+    def _fused_gradient(self, states, targets, stats):
+        """Per-row weights of losses.chunk_loss for r48_cnn_train_grad: wn = mask / (B n) and, in
+        reference mode, cm = (td_sum / (4 B^2)) mask / n with the per-segment action counts;
+        the kernel's gradient lands in the flat gradient buffer (parameters() order)."""
+        from .fused import cnn_train_grad, pack_cnn_train
+        cfg = self.cfg
+        n = cfg.n_boards
+        m = self.mask.float()
+        wn = (m / stats["B"][None, :] / n).contiguous()
+        cm = counts = None
+        if cfg.mode == "reference":
+            cm = ((stats["td_sum"] / (4.0 * stats["B"] * stats["B"]))[None, :] * m / n).contiguous()
+            counts = stats["counts"].float().contiguous()
+        if getattr(self, "_train_ws", None) is None:
+            self._train_ws = torch.empty(_lib_workspace_floats(), dtype=torch.float32, device=self.device)
+        grads, actor, critic = cnn_train_grad(
+            self.net, states.reshape(-1, 16), self.actions.reshape(-1), targets.reshape(-1).contiguous(),
+            wn.view(-1), None if cm is None else cm.view(-1), counts, beta=cfg.beta,
+            exponents=cfg.features == "exponents", n_boards=n, packed=pack_cnn_train(self.net),
+            workspace=self._train_ws)
+        with torch.no_grad():
+            for p, g in zip(self.net.parameters(), grads):
+                p.grad.copy_(g.view_as(p))
+        return float(actor), float(critic)
 
     def train_step(self):
         self.rollout()

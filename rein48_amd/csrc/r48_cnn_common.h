@@ -1,0 +1,79 @@
+// r48_cnn_common.h -- MFMA building blocks shared by the fused CNN kernels (inference:
+// r48_policy.hip; training: r48_a3c_train.hip) for rein48_amd/a3c/nets.py:ActorCriticCNN.
+//
+// v_mfma_f32_32x32x16_bf16 lane maps: lane l (r = l & 31, h = l >> 5) holds A[row r][k = 8h + j]
+// and B[k = 8h + j][col r] in element j = 0..7 of its fragment; C/D register i holds
+// D[row 8(i>>2) + 4h + (i&3)][col r]. With boards on the column, a 32x32 accumulator feeds the
+// next layer as its B operand after acc_to_frag, in the permuted k order
+// f(s, j, h) = 16s + 8(j>>2) + 4h + (j&3) (host packing: rein48_amd/a3c/fused.py).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "../../include/rein48.h"
+
+namespace r48cnn {
+
+using bf16x8 = __attribute__((ext_vector_type(8))) short;
+using f32x16 = __attribute__((ext_vector_type(16))) float;
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+
+constexpr int kFragW1 = 9, kFragW2 = 16, kFragWh = 16, kFrags = kFragW1 + kFragW2 + kFragWh;
+// conv2's 2x2 patches over the 3x3 conv1 grid: input positions of output position p
+__device__ constexpr int kP2[4][4] = {{0, 1, 3, 4}, {1, 2, 4, 5}, {3, 4, 6, 7}, {4, 5, 7, 8}};
+
+__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi)
+{
+    // plain casts: hipcc emits one v_cvt_pk_bf16_f32 (round to nearest even)
+    const bf16x2_t v = {(__bf16)lo, (__bf16)hi};
+    return __builtin_bit_cast(uint32_t, v);
+}
+
+// accumulator registers 8s..8s+7 -> the B fragment of k-step s
+__device__ __forceinline__ bf16x8 acc_to_frag(const f32x16 &acc, int s)
+{
+    uint32_t p[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+        p[q] = pack_bf16x2(acc[8 * s + 2 * q], acc[8 * s + 2 * q + 1]);
+    bf16x8 f;
+    __builtin_memcpy(&f, p, 16);
+    return f;
+}
+
+// per-lane bias registers: C/D row of register r for lane half h is (r&3) + 8(r>>2) + 4h
+__device__ __forceinline__ f32x16 load_bias(const float *bias_lds, int h)
+{
+    f32x16 b;
+#pragma unroll
+    for (int r = 0; r < 16; r++)
+        b[r] = bias_lds[(r & 3) + 8 * (r >> 2) + 4 * h];
+    return b;
+}
+
+__device__ __forceinline__ f32x16 bias_relu(f32x16 acc, const f32x16 &b)
+{
+#pragma unroll
+    for (int r = 0; r < 16; r++)
+        acc[r] = fmaxf(acc[r] + b[r], 0.0f);
+    return acc;
+}
+
+// exponent e -> bf16 bits of the network input (raw value 2^e, or e itself)
+__device__ __forceinline__ uint32_t cell_bf16(uint32_t e, int mode)
+{
+    if (mode == R48_FEAT_VALUES)
+        return e ? ((e + 127u) << 7) : 0u;                     // 2^e is exact in bf16
+    return __float_as_uint((float)e) >> 16;                    // small integers are exact
+}
+
+__device__ __forceinline__ bf16x8 frag_at(const uint4 *w, int frag, int lane)
+{
+    const uint4 v = w[frag * 64 + lane];
+    bf16x8 f;
+    __builtin_memcpy(&f, &v, 16);
+    return f;
+}
+
+}  // namespace r48cnn

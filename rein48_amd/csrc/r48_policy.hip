@@ -24,6 +24,7 @@
 
 #include "../../include/rein48.h"
 #include "r48_board.h"
+#include "r48_cnn_common.h"
 
 namespace r48 {
 void set_last_error(const std::string &msg);
@@ -31,62 +32,11 @@ void set_last_error(const std::string &msg);
 
 namespace {
 
-using bf16x8 = __attribute__((ext_vector_type(8))) short;
-using f32x16 = __attribute__((ext_vector_type(16))) float;
+using namespace r48cnn;
 
 constexpr int kWaves = 4;
 constexpr int kThreads = 64 * kWaves;
-constexpr int kFragW1 = 9, kFragW2 = 16, kFragWh = 16, kFrags = kFragW1 + kFragW2 + kFragWh;
 constexpr uint32_t kSampleTag = 0xA3Cu;
-// conv2's 2x2 patches over the 3x3 conv1 grid: input positions of output position p
-__device__ constexpr int kP2[4][4] = {{0, 1, 3, 4}, {1, 2, 4, 5}, {3, 4, 6, 7}, {4, 5, 7, 8}};
-
-typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi)
-{
-    // plain casts: hipcc emits one v_cvt_pk_bf16_f32 (round to nearest even)
-    const bf16x2_t v = {(__bf16)lo, (__bf16)hi};
-    return __builtin_bit_cast(uint32_t, v);
-}
-
-// accumulator registers 8s..8s+7 (after bias + ReLU) -> the B fragment of k-step s
-__device__ __forceinline__ bf16x8 acc_to_frag(const f32x16 &acc, int s)
-{
-    uint32_t p[4];
-#pragma unroll
-    for (int q = 0; q < 4; q++)
-        p[q] = pack_bf16x2(acc[8 * s + 2 * q], acc[8 * s + 2 * q + 1]);
-    bf16x8 f;
-    __builtin_memcpy(&f, p, 16);
-    return f;
-}
-
-// per-lane bias registers: C/D row of register r for lane half h is (r&3) + 8(r>>2) + 4h
-__device__ __forceinline__ f32x16 load_bias(const float *bias_lds, int h)
-{
-    f32x16 b;
-#pragma unroll
-    for (int r = 0; r < 16; r++)
-        b[r] = bias_lds[(r & 3) + 8 * (r >> 2) + 4 * h];
-    return b;
-}
-
-__device__ __forceinline__ f32x16 bias_relu(f32x16 acc, const f32x16 &b)
-{
-#pragma unroll
-    for (int r = 0; r < 16; r++)
-        acc[r] = fmaxf(acc[r] + b[r], 0.0f);
-    return acc;
-}
-
-// exponent e -> bf16 bits of the network input (raw value 2^e, or e itself)
-__device__ __forceinline__ uint32_t cell_bf16(uint32_t e, int mode)
-{
-    if (mode == R48_FEAT_VALUES)
-        return e ? ((e + 127u) << 7) : 0u;                     // 2^e is exact in bf16
-    return __float_as_uint((float)e) >> 16;                    // small integers are exact
-}
 
 __global__ __launch_bounds__(kThreads, 1) void k_cnn_forward(const int8_t *__restrict__ boards, int64_t n,
                                                              const uint4 *__restrict__ wfrag,
