@@ -21,6 +21,12 @@ asm: $(SRC) $(DEPS)
 	$(HIPCC) $(HIPFLAGS) --cuda-device-only -c -o /dev/null -Rpass-analysis=kernel-resource-usage rein48_amd/csrc/r48_policy.hip 2> build/resource_usage_policy.txt
 	$(HIPCC) $(HIPFLAGS) --cuda-device-only -c -o /dev/null -Rpass-analysis=kernel-resource-usage rein48_amd/csrc/r48_env.hip 2> build/resource_usage.txt
 
+# k_cnn_train phase ablations for tools/exp_train_ablate.py (timing only; wrong gradients)
+ABLATE := 1 2 4 6 7
+ablate: $(SRC) $(DEPS)
+	@mkdir -p build/ablate_train
+	for m in $(ABLATE); do $(HIPCC) $(HIPFLAGS) -DR48_TRAIN_SKIP=$$m -shared -o build/ablate_train/librein48_skip$$m.so $(SRC) || exit 1; done
+
 oracle:
 	$(MAKE) -s -C oracle
 
@@ -28,4 +34,4 @@ clean:
 	rm -rf $(LIBDIR) build
 	$(MAKE) -s -C oracle clean
 
-.PHONY: all asm oracle clean
+.PHONY: all asm ablate oracle clean

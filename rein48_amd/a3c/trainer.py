@@ -135,10 +135,15 @@ class A3CTrainer:
                                               logits=False, value=True)[1]
             else:
                 value = lambda b: self._net(self._features(b))[1]
-            v_all = torch.empty((T, n), dtype=torch.float32, device=self.device)
-            for t0 in range(0, T, T if fused else cfg.update_chunk):
-                t1 = min(T, t0 + (T if fused else cfg.update_chunk))
-                v_all[t0:t1] = value(states[t0:t1].contiguous()).view(t1 - t0, n)
+            # the fused textbook update computes td = target - V(s) in-kernel and needs no
+            # per-segment td_sum, so only the reference loss (or the unfused path) pays this pass
+            need_values = not (fused and cfg.fused_update and cfg.mode == "textbook")
+            v_all = None
+            if need_values:
+                v_all = torch.empty((T, n), dtype=torch.float32, device=self.device)
+                for t0 in range(0, T, T if fused else cfg.update_chunk):
+                    t1 = min(T, t0 + (T if fused else cfg.update_chunk))
+                    v_all[t0:t1] = value(states[t0:t1].contiguous()).view(t1 - t0, n)
             # last post-step state of each segment = boards[len]
             idx = self.lengths.long().view(1, n, 1).expand(1, n, 16)
             last = self.boards.gather(0, idx)[0].contiguous()
@@ -146,7 +151,10 @@ class A3CTrainer:
             boot = torch.where(self.finished, torch.zeros_like(v_last), v_last.view(n)).float().contiguous()
             targets = K.discounted_returns(self.rewards, self.lengths, boot, cfg.gamma,
                                            drop_last=cfg.mode == "reference")
-            stats = segment_stats(v_all, targets, self.actions, self.mask)
+            if v_all is not None:
+                stats = segment_stats(v_all, targets, self.actions, self.mask)
+            else:
+                stats = {"B": self.mask.float().sum(0).clamp(min=1.0)}
         if fused and cfg.fused_update:
             # pass 2 as ONE fused MFMA kernel over all T x n states (no activation hits HBM)
             actor_total, critic_total = self._fused_gradient(states, targets, stats)

@@ -56,6 +56,12 @@ constexpr int kAccWhCols = 288;                               // dWh accumulator
 constexpr int kOffDb2 = 64 * 128, kOffDw1 = kOffDb2 + 64, kOffDwh = kOffDw1 + 32 * 5, kOffLoss = kOffDwh + 5 * 257;
 constexpr int kPartial = kOffLoss + 2;                        // 9703
 constexpr float kEntropyEps = 1e-5f;                          // a3c.py:114
+// ablation knob for tools/exp_train_ablate.py (wrong gradients when nonzero; never in the product
+// build): bit 0 drops phase A, bit 1 phase B, bit 2 dh1 + phase C (7 leaves forward + loss)
+#ifndef R48_TRAIN_SKIP
+#define R48_TRAIN_SKIP 0
+#endif
+constexpr int kSkip = R48_TRAIN_SKIP;
 
 // conv1's 2x2 patches over the 4x4 board: cell of tap t (row-major dr, dc) at output position R
 __device__ __forceinline__ int cell_of(int R, int t) { return (R / 3 + (t >> 1)) * 4 + (R % 3) + (t & 1); }
@@ -261,7 +267,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
         }
         // ---------------- phase A: dWh (+ bias) = dout h2^T over the tile's rows
 #pragma unroll
-        for (int u = 0; u < 2; u++) {
+        for (int u = 0; u < ((kSkip & 1) ? 0 : 2); u++) {
             if ((col >> 4) == u) {
                 const int rowi = col & 15;
 #pragma unroll
@@ -314,7 +320,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
             }
         // ---------------- phase B: dW2 = sum_p dh2[p] h1[patch p]^T, db2 = sum_p dh2[p] 1^T
 #pragma unroll
-        for (int u = 0; u < 2; u++) {
+        for (int u = 0; u < ((kSkip & 2) ? 0 : 2); u++) {
             uint16_t *img_dh2 = img, *img_h1 = img + 16 * kStrideDh2;
             if ((col >> 4) == u) {
                 const int rowi = col & 15;
@@ -351,7 +357,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
         // whose patch contains it)
         bf16x8 dh1[9][2];
 #pragma unroll
-        for (int R = 0; R < 9; R++) {
+        for (int R = 0; R < ((kSkip & 4) ? 0 : 9); R++) {
             f32x16 a = zero;
 #pragma unroll
             for (int p = 0; p < 4; p++)
@@ -372,6 +378,8 @@ __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
         // ---------------- phase C: dW1 (+ bias) = sum_R dh1[R] x[patch R]^T
 #pragma unroll
         for (int u = 0; u < 2; u++) {
+            if (kSkip & 4)
+                break;
             uint16_t *img_dh1 = img, *img_x = img + 16 * kStrideH1;              // img_x: [16 cells][16 rows]
             if ((col >> 4) == u) {
                 const int rowi = col & 15;

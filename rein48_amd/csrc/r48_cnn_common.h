@@ -42,13 +42,19 @@ __device__ __forceinline__ bf16x8 acc_to_frag(const f32x16 &acc, int s)
     return f;
 }
 
-// per-lane bias registers: C/D row of register r for lane half h is (r&3) + 8(r>>2) + 4h
+// per-lane bias registers: C/D row of register r for lane half h is (r&3) + 8(r>>2) + 4h, so
+// registers 4u..4u+3 are the 4 contiguous floats at 8u + 4h (four 16-byte LDS reads)
 __device__ __forceinline__ f32x16 load_bias(const float *bias_lds, int h)
 {
     f32x16 b;
 #pragma unroll
-    for (int r = 0; r < 16; r++)
-        b[r] = bias_lds[(r & 3) + 8 * (r >> 2) + 4 * h];
+    for (int u = 0; u < 4; u++) {
+        const float4 v = *reinterpret_cast<const float4 *>(bias_lds + 8 * u + 4 * h);
+        b[4 * u] = v.x;
+        b[4 * u + 1] = v.y;
+        b[4 * u + 2] = v.z;
+        b[4 * u + 3] = v.w;
+    }
     return b;
 }
 

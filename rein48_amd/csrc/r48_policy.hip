@@ -46,7 +46,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_cnn_forward(const int8_t *__res
                                                              uint32_t k1, uint32_t ctr)
 {
     __shared__ uint4 w_lds[kFrags * 64];
-    __shared__ float b_lds[32 + 64 + 8];
+    __shared__ __attribute__((aligned(16))) float b_lds[32 + 64 + 8];   // float4 reads (load_bias)
     for (int i = threadIdx.x; i < kFrags * 64; i += kThreads)
         w_lds[i] = wfrag[i];
     for (int i = threadIdx.x; i < 32 + 64 + 8; i += kThreads)

@@ -1,0 +1,47 @@
+"""GPU experiment: where k_cnn_train's time goes. Times r48_cnn_train_grad over `rows` synthetic
+states for the product library and for ablation builds (R48_TRAIN_SKIP, see r48_a3c_train.hip)
+made by `make ablate`; the ablated gradients are wrong by construction, only their time counts.
+
+    python tools/exp_train_ablate.py [rows]
+"""
+import glob
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, ".")
+from rein48_amd import _lib  # noqa: E402
+from rein48_amd.a3c.fused import cnn_train_grad, pack_cnn_train  # noqa: E402
+from rein48_amd.a3c.nets import ActorCriticCNN  # noqa: E402
+
+rows = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 24
+dev = torch.device("cuda:0")
+n = 1 << 20
+libs = [_lib.LIB_PATH] + sorted(glob.glob("build/ablate_train/librein48_skip*.so"))
+g = torch.Generator(device="cpu").manual_seed(0)
+boards = torch.randint(0, 12, (rows, 16), generator=g, dtype=torch.int8).to(dev)
+actions = torch.randint(0, 4, (rows,), generator=g, dtype=torch.int8).to(dev)
+targets = torch.randn(rows, generator=g).to(dev)
+wn = torch.full((rows,), 1.0 / rows, device=dev)
+for path in libs:
+    _lib.LIB_PATH, _lib._lib = path, None
+    torch.manual_seed(0)
+    net = ActorCriticCNN(dtype=torch.bfloat16).to(dev)
+    packed = pack_cnn_train(net)
+    ws = torch.empty(_lib.load().r48_cnn_train_workspace_floats(), dtype=torch.float32, device=dev)
+    run = lambda: cnn_train_grad(net, boards, actions, targets, wn, None, None, beta=0.01, exponents=True,
+                                 n_boards=n, packed=packed, workspace=ws)
+    for _ in range(3):
+        run()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = 5
+    e0.record()
+    for _ in range(reps):
+        run()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    print("%-40s %8.2f ms per %d rows  (%.2f ms per 1e8)" % (os.path.basename(path), ms, rows, ms * 1e8 / rows),
+          flush=True)
