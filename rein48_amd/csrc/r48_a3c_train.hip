@@ -9,18 +9,24 @@
 //
 // Per 32-row tile and wave (rows on the MFMA column, as in r48_policy.hip):
 //   forward   x -> h1 (9 x 32) -> h2 (4 x 64) -> out (4 logits + value)        89 MFMAs
+//             (bias preloaded as the MFMA accumulator, ReLU as an int16 max on the packed bf16)
 //   loss      per row: d out = dL/d(logits, value)   (softmax, entropy, td; lane-local)
 //   backward  dh2 = Wh^T dout . [h2 > 0]                                          8 MFMAs
 //             dh1 = W2^T dh2 . [h1 > 0]      (conv2 transposed, shared over positions) 64 MFMAs
-//   weights   dWh = dout h2^T, dW2 = dh2 h1^T, dW1 = dh1 x^T (+ biases by a ones row/column):
-//             these contract over ROWS, so rows move to the MFMA K dimension: the lanes of one
-//             16-row half-tile store their activations / gradients as packed 8-byte chunks into a
-//             per-wave [row][feature] LDS image and the operands are read back transposed with
-//             ds_read_b64_tr_b16 (gfx950).                                       ~100 MFMAs
-// dW2 (+ its bias) and dW1 (+ bias) accumulate in AGPRs for the whole kernel; dWh (+ bias) in a
-// per-wave LDS block. Every wave owns its LDS images and accumulators, so after the weights are
-// staged no workgroup barrier is needed. Each wave writes one partial record; k_reduce sums
-// the records in a fixed order (deterministic).
+//             (ReLU' applied to the packed bf16 gradient: d * min(h, 1) per 16-bit half)
+//   weights   dWh = dout h2^T, dW2 = dh2 h1^T, dW1 = dh1 x^T (+ biases by a ones operand):
+//             these contract over ROWS, so rows move to the MFMA K dimension: every lane stores
+//             its row's activations / gradients as packed 8-byte chunks into its wave's LDS slot,
+//             a [row][feature] image read back transposed with ds_read_b64_tr_b16 (gfx950).
+//
+// The four waves of a workgroup SHARE their slots: after a barrier every wave contracts over all
+// 4 x 32 rows, but only for its own slice of the weight gradient (wave w: dW2 input block kk = w,
+// dWh features 64w..64w+63, one (patch, half) pair of db2), so each wave's accumulators are a
+// quarter of the full gradient and fit in registers next to the activations. dW1 is contracted
+// over the wave's own slot. Images are 32-row x 32-column blocks of 64-byte rows with the 8-byte
+// chunk XOR-swizzled by (row >> 1) & 7: the 16-row column stores (ds_write_b64) and the 4-row
+// transposed reads are both bank-conflict free. Each wave writes one partial record (staged in
+// LDS); k_reduce sums the records in a fixed order (deterministic).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -38,6 +44,8 @@ namespace {
 
 using namespace r48cnn;
 typedef short i16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
 #define R48_LDS __attribute__((address_space(3)))
 
 constexpr int kWaves = 4;
@@ -45,16 +53,20 @@ constexpr int kThreads = 64 * kWaves;
 constexpr int kFragWhT = 8, kFragW2T = 16;
 constexpr int kFragsTrain = kFrags + kFragWhT + kFragW2T;    // 65: forward 41 | Wh^T 8 | W2^T 16
 constexpr int kOffWhT = kFrags, kOffW2T = kFrags + kFragWhT;
-// per-wave LDS image region (bf16 elements), one 16-row half-tile at a time:
-//   phase A: img_h2 [16][288] (256 features + ones column) + img_dout [8][16]
-//   phase B: img_dh2 [16][256] + img_h1 [16][288]
-//   phase C: img_dh1 [16][288] + img_x [16 cells][16 rows]
-constexpr int kStrideH2 = 288, kStrideDh2 = 256, kStrideH1 = 288;
-constexpr int kImgElems = 16 * kStrideDh2 + 16 * kStrideH1;  // 8704 bf16 = 17 KiB (phase B, the largest)
-constexpr int kAccWhCols = 288;                               // dWh accumulator [5][288] f32 (col 256 = bias)
+// per-wave slot (bf16 elements): 10 image blocks of 32 rows x 32 columns
+//   phase A: h2 (blocks 0-7: feature 32b + c) | dout [5][32 rows] at kDoutOff
+//   phase B half ph: dh2 of patches 2ph, 2ph+1 (blocks 0-3) | h1 positions 3ph..3ph+5 (blocks 4-9)
+//   phase C: dh1 (blocks 0-8: position R) | x [16 cells][32 rows] at kXOff
+constexpr int kBlock = 32 * 32;
+constexpr int kSlot = 10 * kBlock;
+constexpr int kDoutOff = 8 * kBlock, kXOff = 9 * kBlock;
 // partial record per wave (floats): dW2 [64][128] | db2 [64] | dW1 [32][5] | dWh [5][257] | losses [2]
 constexpr int kOffDb2 = 64 * 128, kOffDw1 = kOffDb2 + 64, kOffDwh = kOffDw1 + 32 * 5, kOffLoss = kOffDwh + 5 * 257;
 constexpr int kPartial = kOffLoss + 2;                        // 9703
+constexpr size_t kLdsWeights = (size_t)(kFragsTrain * 64 + 32) * 16;
+constexpr size_t kLdsLoop = kLdsWeights + (size_t)kWaves * kSlot * 2;     // 148992 B
+constexpr size_t kLdsFlush = (size_t)kWaves * kPartial * 4;              // 155248 B (records staged)
+constexpr size_t kLds = kLdsLoop > kLdsFlush ? kLdsLoop : kLdsFlush;
 constexpr float kEntropyEps = 1e-5f;                          // a3c.py:114
 // ablation knob for tools/exp_train_ablate.py (wrong gradients when nonzero; never in the product
 // build): bit 0 drops phase A, bit 1 phase B, bit 2 dh1 + phase C (7 leaves forward + loss)
@@ -62,55 +74,89 @@ constexpr float kEntropyEps = 1e-5f;                          // a3c.py:114
 #define R48_TRAIN_SKIP 0
 #endif
 constexpr int kSkip = R48_TRAIN_SKIP;
+// scheduling fence: the machine scheduler may not move instructions across it (keeps the
+// transposed operand reads of one slot from being hoisted over the previous slot's MFMAs)
+#define R48_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
 
 // conv1's 2x2 patches over the 4x4 board: cell of tap t (row-major dr, dc) at output position R
 __device__ __forceinline__ int cell_of(int R, int t) { return (R / 3 + (t >> 1)) * 4 + (R % 3) + (t & 1); }
 
-// 32x32x16 operand with k = row of a 16-row half-tile (k = 8h + j) and the operand's row/column
-// index = image column c0 + (lane & 31), from a [row][column] bf16 image: two transposed reads
-// (lane 4q + p of each 16-lane group addresses image row q, columns 4p..4p+3 of its block).
-__device__ __forceinline__ bf16x8 tr_operand(const uint16_t *img, int stride, int c0, int lane)
+// element offset of image (row r, column c) inside a slot: block c >> 5, 64-byte rows, the
+// 8-byte chunk index XOR (r >> 1) & 7
+__device__ __forceinline__ int img_at(int r, int c)
 {
-    const int g = lane >> 4, i = lane & 15, h = g >> 1;
-    const int col = c0 + 16 * (g & 1) + 4 * (i & 3);
-    const uint16_t *a0 = img + (8 * h + (i >> 2)) * stride + col;
-    const uint16_t *a1 = a0 + 4 * stride;
-    const i16x4 r0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((R48_LDS i16x4 *)(a0));
-    const i16x4 r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((R48_LDS i16x4 *)(a1));
+    return (c >> 5) * kBlock + r * 32 + ((((c >> 2) & 7) ^ ((r >> 1) & 7)) << 2) + (c & 3);
+}
+
+// The swizzle is not additive in the column, so every image access is written as a per-lane base
+// (computed once, 10 VGPRs) plus a compile-time block / row offset that folds into the DS
+// instruction's offset field; otherwise each call site gets its own hoisted address register.
+struct LaneAddr {
+    int st[4];       // stores of row `col`: chunk 2k + h of a block
+    int t32[2];      // 32x32x16 transposed read, rows 8h + (i >> 2) + 4u, chunk 4(g & 1) + (i & 3)
+    int t16[2][2];   // 16x16x32 transposed read, rows 8G + (i >> 2) + 4u, chunk 4v + (i & 3)
+};
+
+__device__ __forceinline__ LaneAddr lane_addr(int lane)
+{
+    LaneAddr a;
+    const int h = lane >> 5, col = lane & 31, g = lane >> 4, i = lane & 15;
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+        a.st[k] = img_at(col, 4 * (2 * k + h));
+#pragma unroll
+    for (int u = 0; u < 2; u++) {
+        a.t32[u] = img_at(8 * (g >> 1) + (i >> 2) + 4 * u, 16 * (g & 1) + 4 * (i & 3));
+#pragma unroll
+        for (int v = 0; v < 2; v++)
+            a.t16[v][u] = img_at(8 * g + (i >> 2) + 4 * u, 16 * v + 4 * (i & 3));
+    }
+    return a;
+}
+
+__device__ __forceinline__ bf16x8 tr_pair(const uint16_t *p0, const uint16_t *p1)
+{
+    const i16x4 r0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((R48_LDS i16x4 *)(p0));
+    const i16x4 r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((R48_LDS i16x4 *)(p1));
     bf16x8 f;
     __builtin_memcpy(&f, &r0, 8);
     __builtin_memcpy(reinterpret_cast<char *>(&f) + 8, &r1, 8);
     return f;
 }
 
-// store a B-layout fragment (elements j = channel cbase + 8(j>>2) + 4h + (j&3)) of image row
-// `row` as two packed 8-byte chunks
-__device__ __forceinline__ void store_frag(uint16_t *img, int stride, int row, int cbase, int h, const bf16x8 &f)
+// 32x32x16 operand: index 32 blk + (lane & 31), k = image row r0 + 8h + j (r0 = 0 or 16; the
+// swizzle of row + 16 equals that of row). Per 16-lane group, lane 4q + p addresses row q of the
+// group's 4-row block, columns 4p..4p+3.
+__device__ __forceinline__ bf16x8 tr32(const uint16_t *slot, const LaneAddr &la, int blk, int r0)
+{
+    const uint16_t *b = slot + blk * kBlock + r0 * 32;
+    return tr_pair(b + la.t32[0], b + la.t32[1]);
+}
+
+// 16x16x32 operand: index 32 blk + 16 v + (lane & 15), k = image row 8(lane >> 4) + j
+__device__ __forceinline__ bf16x8 tr16(const uint16_t *slot, const LaneAddr &la, int blk, int v)
+{
+    const uint16_t *b = slot + blk * kBlock;
+    return tr_pair(b + la.t16[v][0], b + la.t16[v][1]);
+}
+
+// store a B-layout fragment (elements j = feature cbase + 8(j>>2) + 4h + (j&3), cbase a multiple
+// of 16) as image row `col`: two packed 8-byte chunks
+__device__ __forceinline__ void store_frag(uint16_t *slot, const LaneAddr &la, int cbase, const bf16x8 &f)
 {
     uint4 v;
     __builtin_memcpy(&v, &f, 16);
-    *reinterpret_cast<uint2 *>(img + row * stride + cbase + 4 * h) = make_uint2(v.x, v.y);
-    *reinterpret_cast<uint2 *>(img + row * stride + cbase + 8 + 4 * h) = make_uint2(v.z, v.w);
+    uint16_t *b = slot + (cbase >> 5) * kBlock;
+    const int s = (cbase >> 4) & 1;
+    *reinterpret_cast<uint2 *>(b + la.st[2 * s]) = make_uint2(v.x, v.y);
+    *reinterpret_cast<uint2 *>(b + la.st[2 * s + 1]) = make_uint2(v.z, v.w);
 }
 
-// ReLU'(activation) of one 32-row accumulator tile as 16 bits: bit i <-> accumulator register i =
-// element i & 7 of fragment i >> 3 (activations are >= 0 post-ReLU bf16, so "> 0" as int16).
-// Keeping the masks as bits lets the activations themselves die early (register pressure).
-__device__ __forceinline__ uint32_t relu_bits(const bf16x8 &a0, const bf16x8 &a1)
+// ReLU' on packed bf16: d where the (post-ReLU, >= 0) activation is nonzero, else +0
+__device__ __forceinline__ bf16x8 mask_pk(const bf16x8 &d, const bf16x8 &act)
 {
-    uint32_t m = 0;
-#pragma unroll
-    for (int i = 0; i < 16; i++)
-        m |= ((i < 8 ? a0[i] : a1[i - 8]) > 0 ? 1u : 0u) << i;
-    return m;
-}
-
-__device__ __forceinline__ f32x16 relu_mask(f32x16 acc, uint32_t bits)
-{
-#pragma unroll
-    for (int i = 0; i < 16; i++)
-        acc[i] = ((bits >> i) & 1u) ? acc[i] : 0.0f;
-    return acc;
+    const u16x8 m = __builtin_elementwise_min(__builtin_bit_cast(u16x8, act), (u16x8)1);
+    return __builtin_bit_cast(bf16x8, (u16x8)(__builtin_bit_cast(u16x8, d) * m));
 }
 
 __device__ __forceinline__ bf16x8 ones_frag()
@@ -122,6 +168,14 @@ __device__ __forceinline__ bf16x8 ones_frag()
     return f;
 }
 
+__device__ __forceinline__ bf16x8 lds_frag(const uint16_t *p)
+{
+    const uint4 v = *reinterpret_cast<const uint4 *>(p);
+    bf16x8 f;
+    __builtin_memcpy(&f, &v, 16);
+    return f;
+}
+
 __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
     const int8_t *__restrict__ boards, int64_t rows, int64_t n_boards, const int8_t *__restrict__ actions,
     const float *__restrict__ targets, const float *__restrict__ wn, const float *__restrict__ cm,
@@ -129,35 +183,51 @@ __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
     const float *__restrict__ bias, float *__restrict__ partials)
 {
     extern __shared__ uint4 lds[];
-    uint4 *w_lds = lds;                                                   // kFragsTrain x 1 KiB
-    float *b_lds = reinterpret_cast<float *>(lds + kFragsTrain * 64);     // 104 floats in 32 x 16 B
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, col = lane & 31;
-    uint16_t *img = reinterpret_cast<uint16_t *>(lds + kFragsTrain * 64 + 32) + wave * kImgElems;
-    float *acc_wh = reinterpret_cast<float *>(reinterpret_cast<uint16_t *>(lds + kFragsTrain * 64 + 32) +
-                                              kWaves * kImgElems) + wave * 5 * kAccWhCols;
+    // LDS: the 4 wave slots first (small DS offsets), then the weight fragments and biases
+    uint16_t *slots = reinterpret_cast<uint16_t *>(lds);
+    uint4 *w_lds_base = lds + kWaves * kSlot / 8;                         // kFragsTrain x 1 KiB
+    float *b_lds_base = reinterpret_cast<float *>(w_lds_base + kFragsTrain * 64);  // 104 floats
+    const int lane = threadIdx.x & 63, h = lane >> 5, col = lane & 31;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint16_t *my = slots + wave * kSlot;
+    const LaneAddr la = lane_addr(lane);
     for (int i = threadIdx.x; i < kFragsTrain * 64; i += kThreads)
-        w_lds[i] = wfrag[i];
+        w_lds_base[i] = wfrag[i];
     for (int i = threadIdx.x; i < 104; i += kThreads)
-        b_lds[i] = bias[i];
-    for (int i = lane; i < 5 * kAccWhCols; i += 64)
-        acc_wh[i] = 0.0f;
+        b_lds_base[i] = bias[i];
     __syncthreads();
 
     const f32x16 zero = {};
+    const f32x4 zero4 = {};
     const bf16x8 ones = ones_frag();
-    f32x16 dw2[2][4], db2[2], dw1;
-#pragma unroll
-    for (int g = 0; g < 2; g++) {
-        db2[g] = zero;
-#pragma unroll
-        for (int kk = 0; kk < 4; kk++)
-            dw2[g][kk] = zero;
-    }
-    dw1 = zero;
+    // this wave's slice of the weight gradient
+    f32x16 dw2[2] = {zero, zero};                  // dW2[32 (g_mine ^ u) + i][32 wave + j], u = 0, 1
+    f32x16 db2 = zero;                             // db2[32 (wave & 1) + i], patches wave >> 1 and 2 + (wave >> 1)
+    f32x4 dwh[4] = {zero4, zero4, zero4, zero4};   // dWh[o][64 wave + 16 ft + i]
+    f32x4 dbh = zero4;                             // heads bias (wave 0)
+    f32x4 dw1[2] = {zero4, zero4};                 // dW1[16 ct + i][t] (t = 4: conv1 bias), own rows
     float loss_actor = 0.0f, loss_critic = 0.0f;
+    // conv1 input position of dW2 block kk = wave relative to the phase-B half:
+    // kP2[2 ph + pl][kk] - 3 ph = pl + 3 (kk >> 1) + (kk & 1)
+    const int pos_kk = 3 * (wave >> 1) + (wave & 1);
+    // ones/zero operands that select this wave's bias-gradient work without a branch (a
+    // conditional MFMA on a loop-carried accumulator makes the register allocator copy it)
+    const bf16x8 nil = {};
+    const bf16x8 ones_w0 = wave == 0 ? ones : nil;                    // heads bias: wave 0 only
+    const bf16x8 ones_pl0 = (wave >> 1) == 0 ? ones : nil, ones_pl1 = (wave >> 1) == 1 ? ones : nil;
+    const int g_mine = wave & 1;                                      // db2 half of this wave
 
     const int64_t n_tiles = (rows + 31) / 32;
-    for (int64_t tile = (int64_t)blockIdx.x * kWaves + wave; tile < n_tiles; tile += (int64_t)gridDim.x * kWaves) {
+    const int64_t per_round = (int64_t)gridDim.x * kWaves;
+    const int64_t rounds = (n_tiles + per_round - 1) / per_round;   // every wave runs every round (barriers)
+    for (int64_t round = 0; round < rounds; round++) {
+        // weights and biases are re-read from LDS every tile: an opaque zero offset keeps the
+        // compiler from hoisting ~300 registers of loop-invariant fragments out of the loop
+        int wofs = 0;
+        asm volatile("" : "+s"(wofs));
+        const uint4 *w_lds = w_lds_base + wofs;
+        const float *b_lds = b_lds_base + wofs;
+        const int64_t tile = round * per_round + (int64_t)blockIdx.x * kWaves + wave;
         const int64_t r = tile * 32 + col;
         const bool live = r < rows;
         const int64_t rr = live ? r : rows - 1;          // padding lanes compute on a valid row, weight 0
@@ -173,43 +243,38 @@ __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
         bf16x8 x;
         __builtin_memcpy(&x, xp, 16);
         bf16x8 h1[9][2];
+        // h1 = ReLU(conv1 x + b1); computed again before phase B rather than kept live (72 VGPRs)
+        // across the loss, dh2 and phase A
+        auto conv1 = [&](const uint4 *wl, const float *bl) {
+            const f32x16 b1 = load_bias(bl, h);
 #pragma unroll
-        for (int R = 0; R < 9; R++) {
-            f32x16 a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_at(w_lds, R, lane), x, zero, 0, 0, 0);
-            a = bias_relu(a, load_bias(b_lds, h));
-            h1[R][0] = acc_to_frag(a, 0);
-            h1[R][1] = acc_to_frag(a, 1);
-        }
+            for (int R = 0; R < 9; R++) {
+                const f32x16 a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_at(wl, R, lane), x, b1, 0, 0, 0);
+                h1[R][0] = acc_to_frag_relu(a, 0);
+                h1[R][1] = acc_to_frag_relu(a, 1);
+            }
+        };
+        conv1(w_lds, b_lds);
         bf16x8 h2[4][2][2];
         f32x16 out = zero;
 #pragma unroll
         for (int p = 0; p < 4; p++)
 #pragma unroll
             for (int g = 0; g < 2; g++) {
-                f32x16 a = zero;
+                f32x16 a = load_bias(b_lds + 32 + 32 * g, h);
 #pragma unroll
                 for (int kk = 0; kk < 4; kk++)
 #pragma unroll
                     for (int s = 0; s < 2; s++)
                         a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_at(w_lds, kFragW1 + (g * 4 + kk) * 2 + s, lane),
                                                                     h1[kP2[p][kk]][s], a, 0, 0, 0);
-                a = bias_relu(a, load_bias(b_lds + 32 + 32 * g, h));
 #pragma unroll
                 for (int s = 0; s < 2; s++) {
-                    h2[p][g][s] = acc_to_frag(a, s);
+                    h2[p][g][s] = acc_to_frag_relu(a, s);
                     out = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
                         frag_at(w_lds, kFragW1 + kFragW2 + (p * 2 + g) * 2 + s, lane), h2[p][g][s], out, 0, 0, 0);
                 }
             }
-        uint32_t m1[9], m2[8];
-#pragma unroll
-        for (int R = 0; R < 9; R++)
-            m1[R] = relu_bits(h1[R][0], h1[R][1]);
-#pragma unroll
-        for (int p = 0; p < 4; p++)
-#pragma unroll
-            for (int g = 0; g < 2; g++)
-                m2[2 * p + g] = relu_bits(h2[p][g][0], h2[p][g][1]);
         // ---------------- loss gradient per row (lane half 0: logits rows 0..3; value in lane + 32)
         const float v = __shfl(out[0], col + 32) + b_lds[100];
         float dz[4] = {0.f, 0.f, 0.f, 0.f}, dv = 0.f;
@@ -265,182 +330,197 @@ __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
             uint32_t pk[4] = {h == 0 ? d0 : 0u, h == 0 ? d1 : 0u, h == 0 ? d2 : 0u, 0u};
             __builtin_memcpy(&dout, pk, 16);
         }
-        // ---------------- phase A: dWh (+ bias) = dout h2^T over the tile's rows
+        // ---------------- phase A stores: h2 and dout of the tile's 32 rows into the own slot
+        if (!(kSkip & 1)) {
 #pragma unroll
-        for (int u = 0; u < ((kSkip & 1) ? 0 : 2); u++) {
-            if ((col >> 4) == u) {
-                const int rowi = col & 15;
+            for (int p = 0; p < 4; p++)
 #pragma unroll
-                for (int p = 0; p < 4; p++)
+                for (int g = 0; g < 2; g++)
 #pragma unroll
-                    for (int g = 0; g < 2; g++)
+                    for (int s = 0; s < 2; s++)
+                        store_frag(my, la, 64 * p + 32 * g + 16 * s, h2[p][g][s]);
+            if (h == 0) {
+                const float dd[5] = {dz[0], dz[1], dz[2], dz[3], dv};
 #pragma unroll
-                        for (int s = 0; s < 2; s++)
-                            store_frag(img, kStrideH2, rowi, 64 * p + 32 * g + 16 * s, h, h2[p][g][s]);
-                if (h == 0) {
-                    *reinterpret_cast<uint2 *>(img + rowi * kStrideH2 + 256) = make_uint2(0x3F80u, 0u);   // ones column
-                    uint16_t *dimg = img + 16 * kStrideH2;                                              // [o][16 rows]
-                    const float dd[5] = {dz[0], dz[1], dz[2], dz[3], dv};
-#pragma unroll
-                    for (int o = 0; o < 5; o++)
-                        dimg[o * 16 + rowi] = __builtin_bit_cast(uint16_t, (__bf16)dd[o]);
-                }
-            }
-            // A[row o][k = row]: lanes with o < 5 read their 8 rows of img_dout
-            bf16x8 aout = {};
-            if (col < 5) {
-                const uint4 v4 = *reinterpret_cast<const uint4 *>(img + 16 * kStrideH2 + col * 16 + 8 * h);
-                __builtin_memcpy(&aout, &v4, 16);
-            }
-#pragma unroll
-            for (int T = 0; T < 9; T++) {
-                const f32x16 d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aout, tr_operand(img, kStrideH2, 32 * T, lane),
-                                                                         zero, 0, 0, 0);
-                // D rows o: half 0 registers 0..3 = o 0..3, half 1 register 0 = o 4
-                if (h == 0) {
-#pragma unroll
-                    for (int o = 0; o < 4; o++)
-                        acc_wh[o * kAccWhCols + 32 * T + col] += d[o];
-                } else {
-                    acc_wh[4 * kAccWhCols + 32 * T + col] += d[0];
-                }
+                for (int o = 0; o < 5; o++)
+                    my[kDoutOff + o * 32 + col] = __builtin_bit_cast(uint16_t, (__bf16)dd[o]);
             }
         }
-        // ---------------- dh2 = Wh^T dout . [h2 > 0]
+        // ---------------- dh2 = Wh^T dout . [h2 > 0]   (h2 dies here)
         bf16x8 dh2[4][2][2];
 #pragma unroll
         for (int p = 0; p < 4; p++)
 #pragma unroll
             for (int g = 0; g < 2; g++) {
-                f32x16 a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_at(w_lds, kOffWhT + p * 2 + g, lane), dout,
-                                                                   zero, 0, 0, 0);
-                a = relu_mask(a, m2[2 * p + g]);
-                dh2[p][g][0] = acc_to_frag(a, 0);
-                dh2[p][g][1] = acc_to_frag(a, 1);
+                const f32x16 a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_at(w_lds, kOffWhT + p * 2 + g, lane),
+                                                                         dout, zero, 0, 0, 0);
+                dh2[p][g][0] = mask_pk(acc_to_frag(a, 0), h2[p][g][0]);
+                dh2[p][g][1] = mask_pk(acc_to_frag(a, 1), h2[p][g][1]);
             }
-        // ---------------- phase B: dW2 = sum_p dh2[p] h1[patch p]^T, db2 = sum_p dh2[p] 1^T
+        // ---------------- phase A: dWh[o][f] (f in the wave's 64 features) = sum over the 4 x 32 rows
+        // of the workgroup of dout[o] h2[f]; 16x16x32 with A = h2^T (features x rows), B = dout
+        if (!(kSkip & 1)) {
+            __syncthreads();
 #pragma unroll
-        for (int u = 0; u < ((kSkip & 2) ? 0 : 2); u++) {
-            uint16_t *img_dh2 = img, *img_h1 = img + 16 * kStrideDh2;
-            if ((col >> 4) == u) {
-                const int rowi = col & 15;
+            for (int sl = 0; sl < kWaves; sl++) {
+                R48_SCHED_FENCE();
+                const uint16_t *slot = slots + sl * kSlot;
+                const int o = lane & 15;
+                bf16x8 bd = {};
+                if (o < 5)
+                    bd = lds_frag(slot + kDoutOff + o * 32 + 8 * (lane >> 4));
 #pragma unroll
-                for (int p = 0; p < 4; p++)
+                for (int ft = 0; ft < 4; ft++)
+                    dwh[ft] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr16(slot, la, 2 * wave + (ft >> 1), ft & 1), bd,
+                                                                      dwh[ft], 0, 0, 0);
+                dbh = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones_w0, bd, dbh, 0, 0, 0);
+            }
+            __syncthreads();
+        }
+        // ---------------- phase B: dW2[:, 32 wave ..] = sum_p dh2[p] h1[kP2[p][wave]]^T, in two
+        // halves of two patches each (the slot holds one half); dh1 is formed between the halves
+        bf16x8 dh1[9][2];
+        {
+            int ofs = 0;
+            asm volatile("" : "+s"(ofs));     // a fresh read of the weights, not the forward's values
+            conv1(w_lds + ofs, b_lds + ofs);
+        }
+#pragma unroll
+        for (int ph = 0; ph < 2; ph++) {
+            if (!(kSkip & 2)) {
+#pragma unroll
+                for (int pl = 0; pl < 2; pl++)
 #pragma unroll
                     for (int g = 0; g < 2; g++)
 #pragma unroll
                         for (int s = 0; s < 2; s++)
-                            store_frag(img_dh2, kStrideDh2, rowi, 64 * p + 32 * g + 16 * s, h, dh2[p][g][s]);
+                            store_frag(my, la, 64 * pl + 32 * g + 16 * s, dh2[2 * ph + pl][g][s]);
 #pragma unroll
-                for (int R = 0; R < 9; R++)
+                for (int q = 0; q < 6; q++)
 #pragma unroll
                     for (int s = 0; s < 2; s++)
-                        store_frag(img_h1, kStrideH1, rowi, 32 * R + 16 * s, h, h1[R][s]);
+                        store_frag(my, la, 128 + 32 * q + 16 * s, h1[3 * ph + q][s]);
             }
+            if (ph == 1 && !(kSkip & 4)) {
+                // dh1 = W2^T dh2 . [h1 > 0]: each conv1 position gathers the conv2 outputs whose
+                // patch contains it (h1 and dh2 die here)
 #pragma unroll
-            for (int p = 0; p < 4; p++) {
-                bf16x8 B[4];
+                for (int R = 0; R < 9; R++) {
+                    f32x16 a = zero;
 #pragma unroll
-                for (int kk = 0; kk < 4; kk++)
-                    B[kk] = tr_operand(img_h1, kStrideH1, 32 * kP2[p][kk], lane);
+                    for (int p = 0; p < 4; p++)
 #pragma unroll
-                for (int g = 0; g < 2; g++) {
-                    const bf16x8 A = tr_operand(img_dh2, kStrideDh2, 64 * p + 32 * g, lane);
+                        for (int kk = 0; kk < 4; kk++)
+                            if (kP2[p][kk] == R) {
 #pragma unroll
-                    for (int kk = 0; kk < 4; kk++)
-                        dw2[g][kk] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A, B[kk], dw2[g][kk], 0, 0, 0);
-                    db2[g] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A, ones, db2[g], 0, 0, 0);
+                                for (int g = 0; g < 2; g++)
+#pragma unroll
+                                    for (int s = 0; s < 2; s++)
+                                        a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                                            frag_at(w_lds, kOffW2T + (kk * 2 + g) * 2 + s, lane), dh2[p][g][s], a, 0, 0,
+                                            0);
+                            }
+                    dh1[R][0] = mask_pk(acc_to_frag(a, 0), h1[R][0]);
+                    dh1[R][1] = mask_pk(acc_to_frag(a, 1), h1[R][1]);
                 }
             }
-        }
-        // ---------------- dh1 = W2^T dh2 . [h1 > 0] (each conv1 position gathers the conv2 outputs
-        // whose patch contains it)
-        bf16x8 dh1[9][2];
+            if (!(kSkip & 2)) {
+                __syncthreads();
 #pragma unroll
-        for (int R = 0; R < ((kSkip & 4) ? 0 : 9); R++) {
-            f32x16 a = zero;
+                for (int sl = 0; sl < kWaves; sl++) {
+                    R48_SCHED_FENCE();
+                    const uint16_t *slot = slots + sl * kSlot;
 #pragma unroll
-            for (int p = 0; p < 4; p++)
+                    for (int pl = 0; pl < 2; pl++)
 #pragma unroll
-                for (int kk = 0; kk < 4; kk++)
-                    if (kP2[p][kk] == R) {
-#pragma unroll
-                        for (int g = 0; g < 2; g++)
-#pragma unroll
-                            for (int s = 0; s < 2; s++)
-                                a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-                                    frag_at(w_lds, kOffW2T + (kk * 2 + g) * 2 + s, lane), dh2[p][g][s], a, 0, 0, 0);
-                    }
-            a = relu_mask(a, m1[R]);
-            dh1[R][0] = acc_to_frag(a, 0);
-            dh1[R][1] = acc_to_frag(a, 1);
-        }
-        // ---------------- phase C: dW1 (+ bias) = sum_R dh1[R] x[patch R]^T
-#pragma unroll
-        for (int u = 0; u < 2; u++) {
-            if (kSkip & 4)
-                break;
-            uint16_t *img_dh1 = img, *img_x = img + 16 * kStrideH1;              // img_x: [16 cells][16 rows]
-            if ((col >> 4) == u) {
-                const int rowi = col & 15;
-#pragma unroll
-                for (int R = 0; R < 9; R++)
-#pragma unroll
-                    for (int s = 0; s < 2; s++)
-                        store_frag(img_dh1, kStrideH1, rowi, 32 * R + 16 * s, h, dh1[R][s]);
-                // cells 8h..8h+7 of this row (the x fragment: element j = cell 8h + j)
-#pragma unroll
-                for (int j = 0; j < 8; j++)
-                    img_x[(8 * h + j) * 16 + rowi] = (uint16_t)x[j];
+                        for (int ks = 0; ks < 2; ks++) {
+                            // dw2[0] holds output half g_mine, dw2[1] the other one
+                            const bf16x8 B = tr32(slot, la, 4 + pl + pos_kk, 16 * ks);
+                            const bf16x8 Am = tr32(slot, la, 2 * pl + g_mine, 16 * ks);
+                            const bf16x8 Ao = tr32(slot, la, 2 * pl + (g_mine ^ 1), 16 * ks);
+                            dw2[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Am, B, dw2[0], 0, 0, 0);
+                            dw2[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Ao, B, dw2[1], 0, 0, 0);
+                            db2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Am, pl == 0 ? ones_pl0 : ones_pl1, db2, 0, 0,
+                                                                          0);
+                        }
+                }
+                __syncthreads();
             }
+        }
+        // ---------------- phase C: dW1[co][t] (+ bias t = 4) = sum over the own 32 rows of
+        // dh1[R][co] x[cell(R, t)]; 16x16x32 with A = dh1^T (channels x rows), B = x patch
+        if (!(kSkip & 4)) {
+#pragma unroll
+            for (int R = 0; R < 9; R++)
+#pragma unroll
+                for (int s = 0; s < 2; s++)
+                    store_frag(my, la, 32 * R + 16 * s, dh1[R][s]);
+#pragma unroll
+            for (int j = 0; j < 8; j++)
+                my[kXOff + (8 * h + j) * 32 + col] = (uint16_t)x[j];
+            const int t = lane & 15;
 #pragma unroll
             for (int R = 0; R < 9; R++) {
-                // B[k = row][col t]: t < 4 -> x[cell(R, t)], t == 4 -> 1 (bias), else 0
                 bf16x8 b = {};
-                if (col < 4) {
-                    const uint4 v4 = *reinterpret_cast<const uint4 *>(img_x + cell_of(R, col) * 16 + 8 * h);
-                    __builtin_memcpy(&b, &v4, 16);
-                } else if (col == 4) {
+                if (t < 4)
+                    b = lds_frag(my + kXOff + cell_of(R, t) * 32 + 8 * (lane >> 4));
+                else if (t == 4)
                     b = ones;
-                }
-                dw1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_operand(img_dh1, kStrideH1, 32 * R, lane), b, dw1,
-                                                              0, 0, 0);
+#pragma unroll
+                for (int ct = 0; ct < 2; ct++)
+                    dw1[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr16(my, la, R, ct), b, dw1[ct], 0, 0, 0);
             }
         }
     }
 
-    // ---------------- flush this wave's partial record
-    float *rec = partials + ((int64_t)blockIdx.x * kWaves + wave) * kPartial;
+    // ---------------- flush: stage this wave's partial record in LDS (zeros outside its slice),
+    // then one coalesced copy to HBM
+    __syncthreads();
+    float *rec = reinterpret_cast<float *>(lds) + wave * kPartial;
+    for (int i = lane; i < kPartial; i += 64)
+        rec[i] = 0.0f;
+    __syncthreads();
 #pragma unroll
     for (int g = 0; g < 2; g++)
 #pragma unroll
-        for (int i = 0; i < 16; i++) {
-            const int row = 32 * g + 8 * (i >> 2) + 4 * h + (i & 3);
+        for (int i = 0; i < 16; i++)
+            rec[(32 * (g ^ (wave & 1)) + 8 * (i >> 2) + 4 * h + (i & 3)) * 128 + 32 * wave + col] = dw2[g][i];
+    if (col == 0) {
 #pragma unroll
-            for (int kk = 0; kk < 4; kk++)
-                rec[row * 128 + 32 * kk + col] = dw2[g][kk][i];
-            if (col == 0)
-                rec[kOffDb2 + row] = db2[g][i];
-        }
-#pragma unroll
-    for (int i = 0; i < 16; i++) {
-        const int row = 8 * (i >> 2) + 4 * h + (i & 3);
-        if (col < 5)
-            rec[kOffDw1 + row * 5 + col] = dw1[i];
+        for (int i = 0; i < 16; i++)
+            rec[kOffDb2 + 32 * (wave & 1) + 8 * (i >> 2) + 4 * h + (i & 3)] = db2[i];
     }
-    for (int i = lane; i < 5 * 257; i += 64)
-        rec[kOffDwh + i] = acc_wh[(i / 257) * kAccWhCols + (i % 257)];
-    // losses: sum over the wave's half-0 lanes
-    float la = loss_actor, lc = loss_critic;
+    {
+        const int j = lane & 15, G = lane >> 4;            // 16x16 D: column j, rows 4G + reg
+        if (j < 5) {
+#pragma unroll
+            for (int ct = 0; ct < 2; ct++)
+#pragma unroll
+                for (int i = 0; i < 4; i++)
+                    rec[kOffDw1 + (16 * ct + 4 * G + i) * 5 + j] = dw1[ct][i];
+#pragma unroll
+            for (int ft = 0; ft < 4; ft++)
+#pragma unroll
+                for (int i = 0; i < 4; i++)
+                    rec[kOffDwh + j * 257 + 64 * wave + 16 * ft + 4 * G + i] = dwh[ft][i];
+            if (wave == 0 && G == 0)
+                rec[kOffDwh + j * 257 + 256] = dbh[0];     // every row of D is the same column sum
+        }
+    }
+    float lsa = loss_actor, lsc = loss_critic;
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
-        la += __shfl_xor(la, off);
-        lc += __shfl_xor(lc, off);
+        lsa += __shfl_xor(lsa, off);
+        lsc += __shfl_xor(lsc, off);
     }
     if (lane == 0) {
-        rec[kOffLoss] = la;
-        rec[kOffLoss + 1] = lc;
+        rec[kOffLoss] = lsa;
+        rec[kOffLoss + 1] = lsc;
     }
+    __syncthreads();
+    float *dst = partials + ((int64_t)blockIdx.x * kWaves + wave) * kPartial;
+    for (int i = lane; i < kPartial; i += 64)
+        dst[i] = rec[i];
 }
 
 // deterministic sum of the per-wave records: out[k] = sum_w partials[w][k]
@@ -490,8 +570,7 @@ int r48_cnn_train_grad(const int8_t *boards, int64_t rows, int64_t n_boards, con
          reinterpret_cast<uintptr_t>(counts)) & 15u)
         return fail(R48_EINVAL, "boards, wfrag and counts must be 16-byte aligned");
     const int grid = grid_size();
-    const size_t lds = (size_t)(kFragsTrain * 64 + 32) * 16 + (size_t)kWaves * kImgElems * 2 +
-                       (size_t)kWaves * 5 * kAccWhCols * 4;
+    const size_t lds = kLds;
     static bool attr_set = false;
     if (!attr_set) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_cnn_train),

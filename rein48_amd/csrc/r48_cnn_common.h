@@ -30,13 +30,34 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi)
     return __builtin_bit_cast(uint32_t, v);
 }
 
-// accumulator registers 8s..8s+7 -> the B fragment of k-step s
+// accumulator registers 8s..8s+7 -> the B fragment of k-step s: four v_cvt_pk_bf16_f32 (round to
+// nearest even). Converted as 2-vectors: a wider conversion is split into single converts + perm.
 __device__ __forceinline__ bf16x8 acc_to_frag(const f32x16 &acc, int s)
 {
+    typedef float f32x2 __attribute__((ext_vector_type(2)));
     uint32_t p[4];
 #pragma unroll
     for (int q = 0; q < 4; q++)
-        p[q] = pack_bf16x2(acc[8 * s + 2 * q], acc[8 * s + 2 * q + 1]);
+        p[q] = __builtin_bit_cast(uint32_t, __builtin_convertvector(
+                                                (f32x2{acc[8 * s + 2 * q], acc[8 * s + 2 * q + 1]}), bf16x2_t));
+    bf16x8 f;
+    __builtin_memcpy(&f, p, 16);
+    return f;
+}
+
+// the same with ReLU: as int16 a negative bf16 (sign bit set) is below 0, so a packed int16
+// max(v, 0) maps it (and -0) to +0 and keeps every positive value; = bf16(max(a, 0)) bit for bit
+__device__ __forceinline__ bf16x8 acc_to_frag_relu(const f32x16 &acc, int s)
+{
+    typedef float f32x2 __attribute__((ext_vector_type(2)));
+    typedef short i16x2 __attribute__((ext_vector_type(2)));
+    uint32_t p[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const i16x2 v = __builtin_bit_cast(
+            i16x2, __builtin_convertvector((f32x2{acc[8 * s + 2 * q], acc[8 * s + 2 * q + 1]}), bf16x2_t));
+        p[q] = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(v, i16x2{0, 0}));
+    }
     bf16x8 f;
     __builtin_memcpy(&f, p, 16);
     return f;
