@@ -8,9 +8,19 @@ DEPS := rein48_amd/csrc/r48_board.h rein48_amd/csrc/r48_cnn_common.h include/rei
 
 all: $(LIBDIR)/librein48.so oracle
 
-$(LIBDIR)/librein48.so: $(SRC) $(DEPS)
+OBJDIR := build/obj
+OBJ := $(patsubst rein48_amd/csrc/%.hip,$(OBJDIR)/%.o,$(SRC))
+# the fused A3C update keeps its loop-carried gradient slices in AGPRs and its MFMA results in
+# VGPRs (no accumulator round trips through v_accvgpr_read before each epilogue)
+FLAGS_r48_a3c_train := -mllvm -amdgpu-mfma-vgpr-form=1
+
+$(LIBDIR)/librein48.so: $(OBJ)
 	@mkdir -p $(LIBDIR)
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(SRC)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJ)
+
+$(OBJDIR)/%.o: rein48_amd/csrc/%.hip $(DEPS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) $(FLAGS_$*) -c -o $@ $<
 
 # assembly + register report for the hot kernels (not needed for the build)
 asm: $(SRC) $(DEPS)
@@ -23,9 +33,9 @@ asm: $(SRC) $(DEPS)
 
 # k_cnn_train phase ablations for tools/exp_train_ablate.py (timing only; wrong gradients)
 ABLATE := 1 2 4 6 7
-ablate: $(SRC) $(DEPS)
+ablate: $(OBJ)
 	@mkdir -p build/ablate_train
-	for m in $(ABLATE); do $(HIPCC) $(HIPFLAGS) -DR48_TRAIN_SKIP=$$m -shared -o build/ablate_train/librein48_skip$$m.so $(SRC) || exit 1; done
+	for m in $(ABLATE); do $(HIPCC) $(HIPFLAGS) $(FLAGS_r48_a3c_train) -DR48_TRAIN_SKIP=$$m -c -o build/ablate_train/train_skip$$m.o rein48_amd/csrc/r48_a3c_train.hip && $(HIPCC) $(HIPFLAGS) -shared -o build/ablate_train/librein48_skip$$m.so $(filter-out $(OBJDIR)/r48_a3c_train.o,$(OBJ)) build/ablate_train/train_skip$$m.o || exit 1; done
 
 oracle:
 	$(MAKE) -s -C oracle

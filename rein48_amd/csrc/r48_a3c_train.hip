@@ -45,7 +45,6 @@ namespace {
 using namespace r48cnn;
 typedef short i16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
 #define R48_LDS __attribute__((address_space(3)))
 
 constexpr int kWaves = 4;
@@ -74,9 +73,6 @@ constexpr float kEntropyEps = 1e-5f;                          // a3c.py:114
 #define R48_TRAIN_SKIP 0
 #endif
 constexpr int kSkip = R48_TRAIN_SKIP;
-// scheduling fence: the machine scheduler may not move instructions across it (keeps the
-// transposed operand reads of one slot from being hoisted over the previous slot's MFMAs)
-#define R48_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
 
 // conv1's 2x2 patches over the 4x4 board: cell of tap t (row-major dr, dc) at output position R
 __device__ __forceinline__ int cell_of(int R, int t) { return (R / 3 + (t >> 1)) * 4 + (R % 3) + (t & 1); }
@@ -152,11 +148,25 @@ __device__ __forceinline__ void store_frag(uint16_t *slot, const LaneAddr &la, i
     *reinterpret_cast<uint2 *>(b + la.st[2 * s + 1]) = make_uint2(v.z, v.w);
 }
 
-// ReLU' on packed bf16: d where the (post-ReLU, >= 0) activation is nonzero, else +0
+// ReLU' on packed bf16: d where the (post-ReLU, >= 0) activation is nonzero, else +0, as
+// d * min(act, 1) per 16-bit half: one v_pk_min_u16 + one v_pk_mul_lo_u16 per word. The min is
+// written in asm: as plain code its 0/1 range lets the compiler rewrite min and product as
+// per-element compares + selects (4-5 instructions per word).
 __device__ __forceinline__ bf16x8 mask_pk(const bf16x8 &d, const bf16x8 &act)
 {
-    const u16x8 m = __builtin_elementwise_min(__builtin_bit_cast(u16x8, act), (u16x8)1);
-    return __builtin_bit_cast(bf16x8, (u16x8)(__builtin_bit_cast(u16x8, d) * m));
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    uint32_t dw[4], aw[4];
+    __builtin_memcpy(dw, &d, 16);
+    __builtin_memcpy(aw, &act, 16);
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        uint32_t m;
+        asm volatile("v_pk_min_u16 %0, %1, %2" : "=v"(m) : "v"(aw[q]), "s"(0x00010001u));   // 1 in both halves
+        dw[q] = __builtin_bit_cast(uint32_t, (u16x2)(__builtin_bit_cast(u16x2, dw[q]) * __builtin_bit_cast(u16x2, m)));
+    }
+    bf16x8 f;
+    __builtin_memcpy(&f, dw, 16);
+    return f;
 }
 
 __device__ __forceinline__ bf16x8 ones_frag()
@@ -176,10 +186,11 @@ __device__ __forceinline__ bf16x8 lds_frag(const uint16_t *p)
     return f;
 }
 
+template <int MODE>
 __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
     const int8_t *__restrict__ boards, int64_t rows, int64_t n_boards, const int8_t *__restrict__ actions,
     const float *__restrict__ targets, const float *__restrict__ wn, const float *__restrict__ cm,
-    const float *__restrict__ counts, float beta, int32_t mode, const uint4 *__restrict__ wfrag,
+    const float *__restrict__ counts, float beta, const uint4 *__restrict__ wfrag,
     const float *__restrict__ bias, float *__restrict__ partials)
 {
     extern __shared__ uint4 lds[];
@@ -220,25 +231,51 @@ __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
     const int64_t n_tiles = (rows + 31) / 32;
     const int64_t per_round = (int64_t)gridDim.x * kWaves;
     const int64_t rounds = (n_tiles + per_round - 1) / per_round;   // every wave runs every round (barriers)
+    // per-row inputs of tile `round`, loaded one tile ahead so their HBM latency hides behind the
+    // previous tile's work (wt = 0 on padding rows; loss inputs only in lane half 0)
+    struct RowIn {
+        uint2 raw;
+        float wt, tgt, c;
+        int act;
+        float4 cnt;
+    };
+    auto fetch = [&](int64_t round) {
+        RowIn in;
+        const int64_t r = (round * per_round + (int64_t)blockIdx.x * kWaves + wave) * 32 + col;
+        const bool live = r < rows;
+        const int64_t rr = live ? r : rows - 1;          // padding lanes compute on a valid row, weight 0
+        in.raw = *reinterpret_cast<const uint2 *>(boards + 16 * rr + 8 * h);
+        in.wt = 0.f, in.tgt = 0.f, in.c = 0.f, in.act = 0, in.cnt = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (h == 0) {
+            in.wt = live ? wn[rr] : 0.0f;
+            in.tgt = targets[rr];
+            in.act = actions[rr] & 3;
+            if (cm) {
+                in.c = live ? cm[rr] : 0.0f;
+                in.cnt = *reinterpret_cast<const float4 *>(counts + 4 * (rr % n_boards));
+            }
+        }
+        return in;
+    };
+    RowIn next = fetch(0);
     for (int64_t round = 0; round < rounds; round++) {
+        const RowIn in = next;
+        if (round + 1 < rounds)
+            next = fetch(round + 1);
         // weights and biases are re-read from LDS every tile: an opaque zero offset keeps the
         // compiler from hoisting ~300 registers of loop-invariant fragments out of the loop
         int wofs = 0;
         asm volatile("" : "+s"(wofs));
         const uint4 *w_lds = w_lds_base + wofs;
         const float *b_lds = b_lds_base + wofs;
-        const int64_t tile = round * per_round + (int64_t)blockIdx.x * kWaves + wave;
-        const int64_t r = tile * 32 + col;
-        const bool live = r < rows;
-        const int64_t rr = live ? r : rows - 1;          // padding lanes compute on a valid row, weight 0
         // ---------------- forward (r48_policy.hip k_cnn_forward)
-        const uint2 raw = *reinterpret_cast<const uint2 *>(boards + 16 * rr + 8 * h);
+        const uint2 raw = in.raw;
         uint32_t xp[4];
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             const uint32_t w = q < 2 ? raw.x : raw.y;
             const int sh = 16 * (q & 1);
-            xp[q] = cell_bf16((w >> sh) & 0xffu, mode) | (cell_bf16((w >> (sh + 8)) & 0xffu, mode) << 16);
+            xp[q] = cell_bf16((w >> sh) & 0xffu, MODE) | (cell_bf16((w >> (sh + 8)) & 0xffu, MODE) << 16);
         }
         bf16x8 x;
         __builtin_memcpy(&x, xp, 16);
@@ -279,7 +316,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
         const float v = __shfl(out[0], col + 32) + b_lds[100];
         float dz[4] = {0.f, 0.f, 0.f, 0.f}, dv = 0.f;
         if (h == 0) {
-            const float wt = live ? wn[rr] : 0.0f;
+            const float wt = in.wt;
             float z[4], p[4], g[4];
 #pragma unroll
             for (int k = 0; k < 4; k++)
@@ -291,21 +328,21 @@ __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
                 p[k] = __expf(z[k] - m);
                 se += p[k];
             }
-            const float inv = 1.0f / se, lse = m + __logf(se);
+            const float inv = __builtin_amdgcn_rcpf(se), lse = m + __logf(se);
             float H = 0.f, gbar = 0.f;
 #pragma unroll
             for (int k = 0; k < 4; k++) {
                 p[k] *= inv;
                 const float lq = __logf(p[k] + kEntropyEps);
                 H -= p[k] * lq;
-                g[k] = -(lq + p[k] / (p[k] + kEntropyEps));     // dH/dp_k
+                g[k] = -(lq + p[k] * __builtin_amdgcn_rcpf(p[k] + kEntropyEps));     // dH/dp_k
                 gbar += p[k] * g[k];
             }
-            const float td = targets[rr] - v;
-            const int a = actions[rr] & 3;
+            const float td = in.tgt - v;
+            const int a = in.act;
             if (cm) {   // reference: -beta wn H - cm sum_k c_k log p_k  (losses.py, a3c.py:110-116)
-                const float c = live ? cm[rr] : 0.0f;
-                const float4 cnt = *reinterpret_cast<const float4 *>(counts + 4 * (rr % n_boards));
+                const float c = in.c;
+                const float4 cnt = in.cnt;
                 const float ck[4] = {cnt.x, cnt.y, cnt.z, cnt.w}, C = cnt.x + cnt.y + cnt.z + cnt.w;
                 float sa = 0.f;
 #pragma unroll
@@ -363,7 +400,6 @@ __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
             __syncthreads();
 #pragma unroll
             for (int sl = 0; sl < kWaves; sl++) {
-                R48_SCHED_FENCE();
                 const uint16_t *slot = slots + sl * kSlot;
                 const int o = lane & 15;
                 bf16x8 bd = {};
@@ -428,7 +464,6 @@ __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
                 __syncthreads();
 #pragma unroll
                 for (int sl = 0; sl < kWaves; sl++) {
-                    R48_SCHED_FENCE();
                     const uint16_t *slot = slots + sl * kSlot;
 #pragma unroll
                     for (int pl = 0; pl < 2; pl++)
@@ -571,14 +606,16 @@ int r48_cnn_train_grad(const int8_t *boards, int64_t rows, int64_t n_boards, con
         return fail(R48_EINVAL, "boards, wfrag and counts must be 16-byte aligned");
     const int grid = grid_size();
     const size_t lds = kLds;
-    static bool attr_set = false;
-    if (!attr_set) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_cnn_train),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        attr_set = true;
+    // one instantiation per input encoding (no per-cell branch); each needs the LDS opt-in once
+    auto kern = mode == R48_FEAT_VALUES ? k_cnn_train<R48_FEAT_VALUES> : k_cnn_train<R48_FEAT_EXPONENTS>;
+    static bool attr_set[2] = {false, false};
+    if (!attr_set[mode == R48_FEAT_VALUES]) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds);
+        attr_set[mode == R48_FEAT_VALUES] = true;
     }
-    hipLaunchKernelGGL(k_cnn_train, dim3(grid), dim3(kThreads), lds, (hipStream_t)stream, boards, rows, n_boards,
-                       actions, targets, wn, cm, counts, beta, mode, (const uint4 *)wfrag, bias, workspace);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), lds, (hipStream_t)stream, boards, rows, n_boards, actions,
+                       targets, wn, cm, counts, beta, (const uint4 *)wfrag, bias, workspace);
     hipLaunchKernelGGL(k_reduce, dim3((kPartial + 255) / 256), dim3(256), 0, (hipStream_t)stream, workspace,
                        (int64_t)grid * kWaves, grad);
     const hipError_t e = hipGetLastError();
