@@ -74,6 +74,11 @@ constexpr float kEntropyEps = 1e-5f;                          // a3c.py:114
 #endif
 constexpr int kSkip = R48_TRAIN_SKIP;
 
+// dh1's (conv2 output p, input block kk) pairs grouped by the conv1 position R = kP2[p][kk]
+__device__ constexpr int kDh1P[16] = {0, 0, 1, 1, 0, 2, 0, 1, 2, 3, 1, 3, 2, 2, 3, 3};
+__device__ constexpr int kDh1K[16] = {0, 1, 0, 1, 2, 0, 3, 2, 1, 0, 3, 1, 2, 3, 2, 3};
+__device__ constexpr int kDh1R[16] = {0, 1, 1, 2, 3, 3, 4, 4, 4, 4, 5, 5, 6, 7, 7, 8};
+
 // conv1's 2x2 patches over the 4x4 board: cell of tap t (row-major dr, dc) at output position R
 __device__ __forceinline__ int cell_of(int R, int t) { return (R / 3 + (t >> 1)) * 4 + (R % 3) + (t & 1); }
 
@@ -167,6 +172,22 @@ __device__ __forceinline__ bf16x8 mask_pk(const bf16x8 &d, const bf16x8 &act)
     bf16x8 f;
     __builtin_memcpy(&f, dw, 16);
     return f;
+}
+
+// Gradient-slice accumulation: acc += A B with the accumulator pinned in AGPRs ("+a") while the
+// activation MFMAs (builtins, VGPR form: FLAGS_r48_a3c_train) keep their results in VGPRs for the
+// epilogues. Wait states, as hipcc pads nothing inside asm: s_nop 1 first (an operand may be a
+// just-written VGPR, e.g. a rematerialised ones fragment); D -> the next MFMA of the same chain
+// taking it whole as C needs none; D -> any other reader: the s_nop fence after the loop. Not
+// volatile: a volatile asm is a scheduling barrier for the LDS reads that feed the next step.
+__device__ __forceinline__ void mfma_acc32(f32x16 &acc, const bf16x8 &a, const bf16x8 &b)
+{
+    asm("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+
+__device__ __forceinline__ void mfma_acc16(f32x4 &acc, const bf16x8 &a, const bf16x8 &b)
+{
+    asm("s_nop 1\n\tv_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
 }
 
 __device__ __forceinline__ bf16x8 ones_frag()
@@ -280,38 +301,16 @@ __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
         bf16x8 x;
         __builtin_memcpy(&x, xp, 16);
         bf16x8 h1[9][2];
-        // h1 = ReLU(conv1 x + b1); computed again before phase B rather than kept live (72 VGPRs)
-        // across the loss, dh2 and phase A
-        auto conv1 = [&](const uint4 *wl, const float *bl) {
-            const f32x16 b1 = load_bias(bl, h);
-#pragma unroll
-            for (int R = 0; R < 9; R++) {
-                const f32x16 a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_at(wl, R, lane), x, b1, 0, 0, 0);
-                h1[R][0] = acc_to_frag_relu(a, 0);
-                h1[R][1] = acc_to_frag_relu(a, 1);
-            }
-        };
-        conv1(w_lds, b_lds);
         bf16x8 h2[4][2][2];
-        f32x16 out = zero;
-#pragma unroll
-        for (int p = 0; p < 4; p++)
-#pragma unroll
-            for (int g = 0; g < 2; g++) {
-                f32x16 a = load_bias(b_lds + 32 + 32 * g, h);
-#pragma unroll
-                for (int kk = 0; kk < 4; kk++)
-#pragma unroll
-                    for (int s = 0; s < 2; s++)
-                        a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_at(w_lds, kFragW1 + (g * 4 + kk) * 2 + s, lane),
-                                                                    h1[kP2[p][kk]][s], a, 0, 0, 0);
-#pragma unroll
-                for (int s = 0; s < 2; s++) {
-                    h2[p][g][s] = acc_to_frag_relu(a, s);
-                    out = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-                        frag_at(w_lds, kFragW1 + kFragW2 + (p * 2 + g) * 2 + s, lane), h2[p][g][s], out, 0, 0, 0);
-                }
-            }
+        f32x16 out;
+        {
+            // h1 is computed again before phase B rather than kept live (72 VGPRs) across the
+            // loss, dh2 and phase A
+            WStream ws;
+            ws.start(w_lds, fwd_frag(0), fwd_frag(1), lane);
+            cnn_conv1(w_lds, b_lds, lane, h, x, ws, h1);
+            cnn_conv2_heads(w_lds, b_lds, lane, h, h1, ws, h2, out);
+        }
         // ---------------- loss gradient per row (lane half 0: logits rows 0..3; value in lane + 32)
         const float v = __shfl(out[0], col + 32) + b_lds[100];
         float dz[4] = {0.f, 0.f, 0.f, 0.f}, dv = 0.f;
@@ -385,31 +384,43 @@ __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
         }
         // ---------------- dh2 = Wh^T dout . [h2 > 0]   (h2 dies here)
         bf16x8 dh2[4][2][2];
+        {
+            WStream ws;
+            ws.start(w_lds, kOffWhT, kOffWhT + 1, lane);
 #pragma unroll
-        for (int p = 0; p < 4; p++)
-#pragma unroll
-            for (int g = 0; g < 2; g++) {
-                const f32x16 a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_at(w_lds, kOffWhT + p * 2 + g, lane),
-                                                                         dout, zero, 0, 0, 0);
-                dh2[p][g][0] = mask_pk(acc_to_frag(a, 0), h2[p][g][0]);
-                dh2[p][g][1] = mask_pk(acc_to_frag(a, 1), h2[p][g][1]);
+            for (int m = 0; m < 8; m++) {               // m = 2p + g
+                const bf16x8 wa = ws.step(w_lds, kOffWhT + (m + 2) % 8, lane);
+                wfence();
+                const f32x16 a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, dout, zero, 0, 0, 0);
+                wfence();
+                dh2[m >> 1][m & 1][0] = mask_pk(acc_to_frag(a, 0), h2[m >> 1][m & 1][0]);
+                dh2[m >> 1][m & 1][1] = mask_pk(acc_to_frag(a, 1), h2[m >> 1][m & 1][1]);
             }
+        }
         // ---------------- phase A: dWh[o][f] (f in the wave's 64 features) = sum over the 4 x 32 rows
         // of the workgroup of dout[o] h2[f]; 16x16x32 with A = h2^T (features x rows), B = dout
         if (!(kSkip & 1)) {
             __syncthreads();
+            // the 4 dout operands up front, the h2^T operands one (slot, ft) step ahead
+            const int o = lane & 15;
+            bf16x8 bd[kWaves];
 #pragma unroll
             for (int sl = 0; sl < kWaves; sl++) {
-                const uint16_t *slot = slots + sl * kSlot;
-                const int o = lane & 15;
-                bf16x8 bd = {};
+                bd[sl] = bf16x8{};
                 if (o < 5)
-                    bd = lds_frag(slot + kDoutOff + o * 32 + 8 * (lane >> 4));
+                    bd[sl] = lds_frag(slots + sl * kSlot + kDoutOff + o * 32 + 8 * (lane >> 4));
+            }
+            bf16x8 A = tr16(slots, la, 2 * wave, 0);
 #pragma unroll
-                for (int ft = 0; ft < 4; ft++)
-                    dwh[ft] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr16(slot, la, 2 * wave + (ft >> 1), ft & 1), bd,
-                                                                      dwh[ft], 0, 0, 0);
-                dbh = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones_w0, bd, dbh, 0, 0, 0);
+            for (int k = 0; k < 4 * kWaves; k++) {
+                const int sl = k >> 2, ft = k & 3, k1 = (k + 1) & 15;
+                const bf16x8 An = tr16(slots + (k1 >> 2) * kSlot, la, 2 * wave + ((k1 & 3) >> 1), k1 & 1);
+                wfence();
+                mfma_acc16(dwh[ft], A, bd[sl]);
+                if (ft == 3)
+                    mfma_acc16(dbh, ones_w0, bd[sl]);
+                wfence();
+                A = An;
             }
             __syncthreads();
         }
@@ -419,7 +430,9 @@ __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
         {
             int ofs = 0;
             asm volatile("" : "+s"(ofs));     // a fresh read of the weights, not the forward's values
-            conv1(w_lds + ofs, b_lds + ofs);
+            WStream ws;
+            ws.start(w_lds + ofs, 0, 1, lane);
+            cnn_conv1(w_lds + ofs, b_lds + ofs, lane, h, x, ws, h1, 0, 0);
         }
 #pragma unroll
         for (int ph = 0; ph < 2; ph++) {
@@ -438,46 +451,54 @@ __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
                         store_frag(my, la, 128 + 32 * q + 16 * s, h1[3 * ph + q][s]);
             }
             if (ph == 1 && !(kSkip & 4)) {
-                // dh1 = W2^T dh2 . [h1 > 0]: each conv1 position gathers the conv2 outputs whose
-                // patch contains it (h1 and dh2 die here)
+                // dh1 = W2^T dh2 . [h1 > 0]: each conv1 position R gathers the conv2 outputs (p, kk)
+                // whose patch contains it (kDh1*: the 16 pairs in R order); one stream of 64
+                // MFMAs, each A fragment read one MFMA ahead (h1 and dh2 die here)
+                f32x16 a = zero;
+                auto w2t = [](int m) { return kOffW2T + (kDh1K[(m & 63) >> 2] * 2 + ((m >> 1) & 1)) * 2 + (m & 1); };
+                WStream ws;
+                ws.start(w_lds, w2t(0), w2t(1), lane);
 #pragma unroll
-                for (int R = 0; R < 9; R++) {
-                    f32x16 a = zero;
-#pragma unroll
-                    for (int p = 0; p < 4; p++)
-#pragma unroll
-                        for (int kk = 0; kk < 4; kk++)
-                            if (kP2[p][kk] == R) {
-#pragma unroll
-                                for (int g = 0; g < 2; g++)
-#pragma unroll
-                                    for (int s = 0; s < 2; s++)
-                                        a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-                                            frag_at(w_lds, kOffW2T + (kk * 2 + g) * 2 + s, lane), dh2[p][g][s], a, 0, 0,
-                                            0);
-                            }
-                    dh1[R][0] = mask_pk(acc_to_frag(a, 0), h1[R][0]);
-                    dh1[R][1] = mask_pk(acc_to_frag(a, 1), h1[R][1]);
+                for (int m = 0; m < 64; m++) {
+                    const int n = m >> 2, g = (m >> 1) & 1, sk = m & 1;
+                    const bf16x8 wa = ws.step(w_lds, w2t(m + 2), lane);
+                    wfence();
+                    a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, dh2[kDh1P[n]][g][sk], a, 0, 0, 0);
+                    wfence();
+                    if ((m & 3) == 3 && (n == 15 || kDh1R[n + 1] != kDh1R[n])) {
+                        const int R = kDh1R[n];
+                        dh1[R][0] = mask_pk(acc_to_frag(a, 0), h1[R][0]);
+                        dh1[R][1] = mask_pk(acc_to_frag(a, 1), h1[R][1]);
+                        a = zero;
+                    }
                 }
             }
             if (!(kSkip & 2)) {
                 __syncthreads();
+                // 16 K-steps (slot sl, patch pl of the half, 16-row block ks), software-pipelined:
+                // the operands of step k + 1 are read before the MFMAs of step k issue
+                // (dw2[0] holds output half g_mine, dw2[1] the other one)
+                auto ld = [&](int st, bf16x8 *op) {
+                    const uint16_t *slot = slots + (st >> 2) * kSlot;
+                    const int pl = (st >> 1) & 1, ks = st & 1;
+                    op[0] = tr32(slot, la, 4 + pl + pos_kk, 16 * ks);
+                    op[1] = tr32(slot, la, 2 * pl + g_mine, 16 * ks);
+                    op[2] = tr32(slot, la, 2 * pl + (g_mine ^ 1), 16 * ks);
+                };
+                bf16x8 cur[3], nxt[3];
+                ld(0, cur);
 #pragma unroll
-                for (int sl = 0; sl < kWaves; sl++) {
-                    const uint16_t *slot = slots + sl * kSlot;
+                for (int st = 0; st < 16; st++) {
+                    if (st + 1 < 16)
+                        ld(st + 1, nxt);
+                    __builtin_amdgcn_sched_barrier(0);
+                    mfma_acc32(dw2[0], cur[1], cur[0]);
+                    mfma_acc32(dw2[1], cur[2], cur[0]);
+                    mfma_acc32(db2, cur[1], ((st >> 1) & 1) == 0 ? ones_pl0 : ones_pl1);
+                    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-                    for (int pl = 0; pl < 2; pl++)
-#pragma unroll
-                        for (int ks = 0; ks < 2; ks++) {
-                            // dw2[0] holds output half g_mine, dw2[1] the other one
-                            const bf16x8 B = tr32(slot, la, 4 + pl + pos_kk, 16 * ks);
-                            const bf16x8 Am = tr32(slot, la, 2 * pl + g_mine, 16 * ks);
-                            const bf16x8 Ao = tr32(slot, la, 2 * pl + (g_mine ^ 1), 16 * ks);
-                            dw2[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Am, B, dw2[0], 0, 0, 0);
-                            dw2[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Ao, B, dw2[1], 0, 0, 0);
-                            db2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Am, pl == 0 ? ones_pl0 : ones_pl1, db2, 0, 0,
-                                                                          0);
-                        }
+                    for (int k = 0; k < 3; k++)
+                        cur[k] = nxt[k];
                 }
                 __syncthreads();
             }
@@ -494,22 +515,40 @@ __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
             for (int j = 0; j < 8; j++)
                 my[kXOff + (8 * h + j) * 32 + col] = (uint16_t)x[j];
             const int t = lane & 15;
-#pragma unroll
-            for (int R = 0; R < 9; R++) {
+            // B[row][t]: t < 4 -> x[cell(R, t)], t == 4 -> 1 (conv1 bias), else 0
+            auto patch = [&](int R) {
                 bf16x8 b = {};
                 if (t < 4)
                     b = lds_frag(my + kXOff + cell_of(R, t) * 32 + 8 * (lane >> 4));
                 else if (t == 4)
                     b = ones;
+                return b;
+            };
+            // operands one (R, ct) step ahead
+            bf16x8 B = patch(0), A = tr16(my, la, 0, 0);
 #pragma unroll
-                for (int ct = 0; ct < 2; ct++)
-                    dw1[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr16(my, la, R, ct), b, dw1[ct], 0, 0, 0);
+            for (int k = 0; k < 18; k++) {
+                const int R = k >> 1, ct = k & 1, k1 = (k + 1) % 18;
+                const bf16x8 An = tr16(my, la, k1 >> 1, k1 & 1);
+                bf16x8 Bn = B;
+                if (ct == 1)
+                    Bn = patch(k1 >> 1);
+                wfence();
+                mfma_acc16(dw1[ct], A, B);
+                wfence();
+                A = An;
+                B = Bn;
+                (void)R;
             }
         }
     }
 
     // ---------------- flush: stage this wave's partial record in LDS (zeros outside its slice),
-    // then one coalesced copy to HBM
+    // then one coalesced copy to HBM. acc fence: 24 wait states between the last accumulating MFMA
+    // and any other reader of its AGPRs (16-pass XDL write -> read)
+    asm volatile("s_nop 15\n\ts_nop 7"
+                 : "+a"(dw2[0]), "+a"(dw2[1]), "+a"(db2), "+a"(dwh[0]), "+a"(dwh[1]), "+a"(dwh[2]), "+a"(dwh[3]),
+                   "+a"(dbh), "+a"(dw1[0]), "+a"(dw1[1]));
     __syncthreads();
     float *rec = reinterpret_cast<float *>(lds) + wave * kPartial;
     for (int i = lane; i < kPartial; i += 64)

@@ -103,4 +103,87 @@ __device__ __forceinline__ bf16x8 frag_at(const uint4 *w, int frag, int lane)
     return f;
 }
 
+// ---- weight-fragment pipelining: with one wave per SIMD an MFMA that waits on its own A-fragment
+// LDS read exposes the read's latency, so the fragment of the next MFMA is read before the current
+// one issues. wfence() keeps that order (DS reads and MFMAs may not cross it; VALU, SALU and
+// transcendental work may, so epilogues still interleave with the MFMA stream).
+__device__ __forceinline__ void wfence() { __builtin_amdgcn_sched_barrier(0x406); }
+
+// A fragment of forward MFMA i (0..88) in issue order: conv1 positions R = 0..8, then per conv2
+// output (p, g) its 8 W2 fragments (kk, s) and its 2 head fragments (s)
+constexpr int kFwdMfmas = 9 + 8 * 10;
+__host__ __device__ constexpr int fwd_frag(int i)
+{
+    if (i < 9)
+        return i;
+    const int t = i - 9, pg = t / 10, u = t % 10;
+    return u < 8 ? kFragW1 + ((pg & 1) * 4 + (u >> 1)) * 2 + (u & 1) : kFragW1 + kFragW2 + pg * 2 + (u - 8);
+}
+
+// A-fragment stream two MFMAs deep: q0 feeds the next MFMA, q1 the one after; step() returns q0
+// and issues the read of fragment `ahead` (the MFMA after q1's)
+struct WStream {
+    bf16x8 q0, q1;
+    __device__ __forceinline__ void start(const uint4 *w, int f0, int f1, int lane)
+    {
+        q0 = frag_at(w, f0, lane);
+        q1 = frag_at(w, f1, lane);
+    }
+    __device__ __forceinline__ bf16x8 step(const uint4 *w, int ahead, int lane)
+    {
+        const bf16x8 cur = q0;
+        q0 = q1;
+        q1 = frag_at(w, ahead, lane);
+        return cur;
+    }
+};
+
+// ReLU(conv1 x + b1) for the 9 positions; the stream holds fragments 0 and 1 on entry and
+// `after0`, `after1` (default: fwd_frag(9), fwd_frag(10)) on exit
+__device__ __forceinline__ void cnn_conv1(const uint4 *w, const float *b, int lane, int h, const bf16x8 &x,
+                                          WStream &ws, bf16x8 (&h1)[9][2], int after0 = fwd_frag(9),
+                                          int after1 = fwd_frag(10))
+{
+    const f32x16 b1 = load_bias(b, h);
+#pragma unroll
+    for (int R = 0; R < 9; R++) {
+        const bf16x8 wa = ws.step(w, R + 2 < 9 ? R + 2 : (R + 2 == 9 ? after0 : after1), lane);
+        wfence();
+        const f32x16 a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, x, b1, 0, 0, 0);
+        wfence();
+        h1[R][0] = acc_to_frag_relu(a, 0);
+        h1[R][1] = acc_to_frag_relu(a, 1);
+    }
+}
+
+// conv2 + heads: h2[p][g][s] = ReLU(conv2 h1 + b2) fragments and out (rows 0..3 logits, row 4
+// value, without the head bias); the stream holds fwd_frag(9), fwd_frag(10) on entry
+__device__ __forceinline__ void cnn_conv2_heads(const uint4 *w, const float *b, int lane, int h,
+                                                const bf16x8 (&h1)[9][2], WStream &ws, bf16x8 (&h2)[4][2][2],
+                                                f32x16 &out)
+{
+    const f32x16 b2[2] = {load_bias(b + 32, h), load_bias(b + 64, h)};
+    out = f32x16{};
+#pragma unroll
+    for (int p = 0; p < 4; p++)
+#pragma unroll
+        for (int g = 0; g < 2; g++) {
+            f32x16 a = b2[g];
+#pragma unroll
+            for (int u = 0; u < 10; u++) {
+                const int i = 9 + (p * 2 + g) * 10 + u;
+                const bf16x8 wa = ws.step(w, fwd_frag(i + 2 < kFwdMfmas ? i + 2 : 0), lane);
+                wfence();
+                if (u < 8) {
+                    a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, h1[kP2[p][u >> 1]][u & 1], a, 0, 0, 0);
+                } else {
+                    const int s = u - 8;
+                    h2[p][g][s] = acc_to_frag_relu(a, s);
+                    out = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, h2[p][g][s], out, 0, 0, 0);
+                }
+                wfence();
+            }
+        }
+}
+
 }  // namespace r48cnn
