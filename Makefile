@@ -13,6 +13,7 @@ OBJ := $(patsubst rein48_amd/csrc/%.hip,$(OBJDIR)/%.o,$(SRC))
 # the fused A3C update keeps its loop-carried gradient slices in AGPRs and its MFMA results in
 # VGPRs (no accumulator round trips through v_accvgpr_read before each epilogue)
 FLAGS_r48_a3c_train := -mllvm -amdgpu-mfma-vgpr-form=1
+FLAGS_r48_policy ?=
 
 $(LIBDIR)/librein48.so: $(OBJ)
 	@mkdir -p $(LIBDIR)

@@ -16,6 +16,7 @@
 // packs the weight (A) fragments in exactly that order, once per parameter update
 // (rein48_amd/a3c/fused.py). Per 32 boards: 9 + 64 + 16 = 89 MFMAs (~70 kFLOP per board).
 // Weights (41 fragments x 1 KiB) are staged in LDS once per workgroup; waves loop over tiles.
+// Biases enter as the MFMA accumulator, ReLU is an int16 max on the packed bf16 pairs.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -38,9 +39,10 @@ constexpr int kWaves = 4;
 constexpr int kThreads = 64 * kWaves;
 constexpr uint32_t kSampleTag = 0xA3Cu;
 
-__global__ __launch_bounds__(kThreads, 1) void k_cnn_forward(const int8_t *__restrict__ boards, int64_t n,
+template <int MODE>
+__global__ __launch_bounds__(kThreads, 2) void k_cnn_forward(const int8_t *__restrict__ boards, int64_t n,
                                                              const uint4 *__restrict__ wfrag,
-                                                             const float *__restrict__ bias, int32_t mode,
+                                                             const float *__restrict__ bias,
                                                              float *__restrict__ logits, float *__restrict__ value,
                                                              int8_t *__restrict__ actions, int64_t gid0, uint32_t k0,
                                                              uint32_t k1, uint32_t ctr)
@@ -55,8 +57,6 @@ __global__ __launch_bounds__(kThreads, 1) void k_cnn_forward(const int8_t *__res
 
     const int lane = threadIdx.x & 63, h = lane >> 5, col = lane & 31;
     const int64_t n_tiles = (n + 31) / 32;
-    const f32x16 bias1 = load_bias(b_lds, h), bias2a = load_bias(b_lds + 32, h), bias2b = load_bias(b_lds + 64, h);
-    const f32x16 zero = {};
     const int64_t stride = (int64_t)gridDim.x * kWaves;
     int64_t tile = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
     // board bytes are prefetched one tile ahead (clamped index: always a valid address)
@@ -76,50 +76,19 @@ __global__ __launch_bounds__(kThreads, 1) void k_cnn_forward(const int8_t *__res
         for (int q = 0; q < 4; q++) {
             const uint32_t w = q < 2 ? raw.x : raw.y;
             const int sh = 16 * (q & 1);
-            xp[q] = cell_bf16((w >> sh) & 0xffu, mode) | (cell_bf16((w >> (sh + 8)) & 0xffu, mode) << 16);
+            xp[q] = cell_bf16((w >> sh) & 0xffu, MODE) | (cell_bf16((w >> (sh + 8)) & 0xffu, MODE) << 16);
         }
         bf16x8 x;
         __builtin_memcpy(&x, xp, 16);
-
-        // layer 1: 9 row tiles (one per conv1 output position, rows = 32 filters)
-        bf16x8 h1[9][2];
-#pragma unroll
-        for (int R = 0; R < 9; R++) {
-            const uint4 af = w_lds[R * 64 + lane];
-            bf16x8 a;
-            __builtin_memcpy(&a, &af, 16);
-            f32x16 acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, x, zero, 0, 0, 0);
-            acc = bias_relu(acc, bias1);
-            h1[R][0] = acc_to_frag(acc, 0);
-            h1[R][1] = acc_to_frag(acc, 1);
-        }
-        // layer 2 (conv2: weights shared by the 4 output positions) fused with the heads
-        f32x16 out = zero;
-#pragma unroll
-        for (int p = 0; p < 4; p++) {
-#pragma unroll
-            for (int g = 0; g < 2; g++) {
-                f32x16 acc = zero;
-#pragma unroll
-                for (int kk = 0; kk < 4; kk++) {
-#pragma unroll
-                    for (int s = 0; s < 2; s++) {
-                        const uint4 af = w_lds[(kFragW1 + (g * 4 + kk) * 2 + s) * 64 + lane];
-                        bf16x8 a;
-                        __builtin_memcpy(&a, &af, 16);
-                        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, h1[kP2[p][kk]][s], acc, 0, 0, 0);
-                    }
-                }
-                acc = bias_relu(acc, g == 0 ? bias2a : bias2b);
-#pragma unroll
-                for (int s = 0; s < 2; s++) {
-                    const uint4 af = w_lds[(kFragW1 + kFragW2 + (p * 2 + g) * 2 + s) * 64 + lane];
-                    bf16x8 a;
-                    __builtin_memcpy(&a, &af, 16);
-                    out = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, acc_to_frag(acc, s), out, 0, 0, 0);
-                }
-            }
-        }
+        // layer 1 (9 row tiles: one per conv1 output position, rows = 32 filters), then layer 2
+        // (conv2: weights shared by the 4 output positions) fused with the heads; weight
+        // fragments stream from LDS two MFMAs ahead (r48_cnn_common.h)
+        bf16x8 h1[9][2], h2[4][2][2];
+        f32x16 out;
+        WStream ws;
+        ws.start(w_lds, fwd_frag(0), fwd_frag(1), lane);
+        cnn_conv1(w_lds, b_lds, lane, h, x, ws, h1);
+        cnn_conv2_heads(w_lds, b_lds, lane, h, h1, ws, h2, out);
         if (!live)
             continue;  // padding lanes of the last tile computed on a clamped duplicate board
         // head rows: lane half 0 registers 0..3 = logits 0..3, lane half 1 register 0 = value
@@ -170,8 +139,10 @@ int r48_cnn_policy_forward(const int8_t *boards, int64_t n, const void *wfrag, c
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     const int64_t tiles = (n + 31) / 32;
     const int64_t blocks = std::min<int64_t>((tiles + kWaves - 1) / kWaves, (int64_t)cus * 2);
-    hipLaunchKernelGGL(k_cnn_forward, dim3((unsigned)blocks), dim3(kThreads), 0, (hipStream_t)stream, boards, n,
-                       (const uint4 *)wfrag, bias, mode, logits, value, actions, gid0, (uint32_t)seed,
+    // one instantiation per input encoding (no per-cell branch)
+    auto kern = mode == R48_FEAT_VALUES ? k_cnn_forward<R48_FEAT_VALUES> : k_cnn_forward<R48_FEAT_EXPONENTS>;
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kThreads), 0, (hipStream_t)stream, boards, n,
+                       (const uint4 *)wfrag, bias, logits, value, actions, gid0, (uint32_t)seed,
                        (uint32_t)(seed >> 32), ctr);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess)
