@@ -109,15 +109,23 @@ __device__ __forceinline__ bf16x8 frag_at(const uint4 *w, int frag, int lane)
 // transcendental work may, so epilogues still interleave with the MFMA stream).
 __device__ __forceinline__ void wfence() { __builtin_amdgcn_sched_barrier(0x406); }
 
-// A fragment of forward MFMA i (0..88) in issue order: conv1 positions R = 0..8, then per conv2
-// output (p, g) its 8 W2 fragments (kk, s) and its 2 head fragments (s)
+// A fragment of forward MFMA i (0..88) in issue order: conv1 positions R = 0..8, then the 8 conv2
+// chains c = 2p + g (8 W2 fragments (kk, s) each) with the 2 head MFMAs of chain c issued after
+// chain c + 1, so the head MFMAs never wait on their chain's epilogue (bf16 pack + ReLU)
 constexpr int kFwdMfmas = 9 + 8 * 10;
 __host__ __device__ constexpr int fwd_frag(int i)
 {
     if (i < 9)
         return i;
-    const int t = i - 9, pg = t / 10, u = t % 10;
-    return u < 8 ? kFragW1 + ((pg & 1) * 4 + (u >> 1)) * 2 + (u & 1) : kFragW1 + kFragW2 + pg * 2 + (u - 8);
+    const int t = i - 9;
+    if (t < 8)                                                       // chain 0
+        return kFragW1 + (t >> 1) * 2 + (t & 1);
+    const int t2 = t - 8;
+    if (t2 >= 70)                                                    // heads of chain 7
+        return kFragW1 + kFragW2 + 7 * 2 + (t2 - 70);
+    const int b = t2 / 10, u = t2 % 10;
+    return u < 8 ? kFragW1 + (((b + 1) & 1) * 4 + (u >> 1)) * 2 + (u & 1)   // chain b + 1
+                 : kFragW1 + kFragW2 + b * 2 + (u - 8);                     // heads of chain b
 }
 
 // A-fragment stream two MFMAs deep: q0 feeds the next MFMA, q1 the one after; step() returns q0
@@ -157,33 +165,42 @@ __device__ __forceinline__ void cnn_conv1(const uint4 *w, const float *b, int la
 }
 
 // conv2 + heads: h2[p][g][s] = ReLU(conv2 h1 + b2) fragments and out (rows 0..3 logits, row 4
-// value, without the head bias); the stream holds fwd_frag(9), fwd_frag(10) on entry
+// value, without the head bias); the stream holds fwd_frag(9), fwd_frag(10) on entry. Issue order
+// as fwd_frag: chain c (c = 2p + g), then the heads of chain c - 1.
 __device__ __forceinline__ void cnn_conv2_heads(const uint4 *w, const float *b, int lane, int h,
                                                 const bf16x8 (&h1)[9][2], WStream &ws, bf16x8 (&h2)[4][2][2],
                                                 f32x16 &out)
 {
     const f32x16 b2[2] = {load_bias(b + 32, h), load_bias(b + 64, h)};
     out = f32x16{};
+    f32x16 acc[2];
+    int i = 9;
 #pragma unroll
-    for (int p = 0; p < 4; p++)
+    for (int c = 0; c <= 8; c++) {
+        if (c < 8) {
+            const int p = c >> 1;
+            f32x16 a = b2[c & 1];
 #pragma unroll
-        for (int g = 0; g < 2; g++) {
-            f32x16 a = b2[g];
-#pragma unroll
-            for (int u = 0; u < 10; u++) {
-                const int i = 9 + (p * 2 + g) * 10 + u;
+            for (int u = 0; u < 8; u++, i++) {
                 const bf16x8 wa = ws.step(w, fwd_frag(i + 2 < kFwdMfmas ? i + 2 : 0), lane);
                 wfence();
-                if (u < 8) {
-                    a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, h1[kP2[p][u >> 1]][u & 1], a, 0, 0, 0);
-                } else {
-                    const int s = u - 8;
-                    h2[p][g][s] = acc_to_frag_relu(a, s);
-                    out = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, h2[p][g][s], out, 0, 0, 0);
-                }
+                a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, h1[kP2[p][u >> 1]][u & 1], a, 0, 0, 0);
+                wfence();
+            }
+            acc[c & 1] = a;
+        }
+        if (c >= 1) {
+            const int cp = c - 1, p = cp >> 1, g = cp & 1;
+#pragma unroll
+            for (int s = 0; s < 2; s++, i++) {
+                h2[p][g][s] = acc_to_frag_relu(acc[cp & 1], s);
+                const bf16x8 wa = ws.step(w, fwd_frag(i + 2 < kFwdMfmas ? i + 2 : 0), lane);
+                wfence();
+                out = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, h2[p][g][s], out, 0, 0, 0);
                 wfence();
             }
         }
+    }
 }
 
 }  // namespace r48cnn

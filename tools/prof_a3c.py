@@ -1,14 +1,21 @@
-"""Profile target: A3C (CNN, bf16) rollout + update at 2^20 boards, short segments."""
-import sys
-import torch
-sys.path.insert(0, ".")
-from rein48_amd.a3c import A3CConfig, A3CTrainer
+"""Profile target: A3C config 3 (2^20 boards, CNN bf16, fused policy and update, 100-step
+segments): `iters` train steps after one warm-up step.
 
-net = sys.argv[1] if len(sys.argv) > 1 else "cnn"
-cfg = A3CConfig(n_boards=1 << 20, max_steps=10, mode="textbook", net=net, bf16=(net == "cnn"),
-                features="exponents", seed=1, update_chunk=10)
+    rocprofv3 --kernel-trace --stats -d gpurun_out/prof_a3c -- python tools/prof_a3c.py [iters]
+"""
+import sys
+
+import torch
+
+sys.path.insert(0, ".")
+from rein48_amd.a3c import A3CConfig, A3CTrainer  # noqa: E402
+
+iters = int(sys.argv[1]) if len(sys.argv) > 1 else 2
+cfg = A3CConfig(n_boards=1 << 20, max_steps=100, mode="textbook", net="cnn", bf16=True, features="exponents",
+                seed=1, update_chunk=10)
 tr = A3CTrainer(cfg, device="cuda:0")
-for _ in range(3):
+tr.train_step()
+for _ in range(iters):
     tr.train_step()
 torch.cuda.synchronize()
 print("ok")
