@@ -2,7 +2,7 @@
 states for the product library and for ablation builds (R48_TRAIN_SKIP, see r48_a3c_train.hip)
 made by `make ablate`; the ablated gradients are wrong by construction, only their time counts.
 
-    python tools/exp_train_ablate.py [rows]
+    python tools/exp_train_ablate.py [rows] [lib.so ...]   (explicit libraries instead of the ablations)
 """
 import glob
 import os
@@ -18,7 +18,7 @@ from rein48_amd.a3c.nets import ActorCriticCNN  # noqa: E402
 rows = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 24
 dev = torch.device("cuda:0")
 n = 1 << 20
-libs = [_lib.LIB_PATH] + sorted(glob.glob("build/ablate_train/librein48_skip*.so"))
+libs = sys.argv[2:] or [_lib.LIB_PATH] + sorted(glob.glob("build/ablate_train/librein48_skip*.so"))
 g = torch.Generator(device="cpu").manual_seed(0)
 boards = torch.randint(0, 12, (rows, 16), generator=g, dtype=torch.int8).to(dev)
 actions = torch.randint(0, 4, (rows,), generator=g, dtype=torch.int8).to(dev)
