@@ -185,6 +185,19 @@ __device__ __forceinline__ void mfma_acc32(f32x16 &acc, const bf16x8 &a, const b
     asm("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
 }
 
+// the same without the leading pad, for operands that come straight from LDS reads (the s_waitcnt
+// orders those; only a VALU write needs the wait states). tools/check_asm_hazards.py verifies on
+// the compiled code that no VALU write reaches these within 2 states.
+__device__ __forceinline__ void mfma_acc32_lds(f32x16 &acc, const bf16x8 &a, const bf16x8 &b)
+{
+    asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+
+__device__ __forceinline__ void mfma_acc16_lds(f32x4 &acc, const bf16x8 &a, const bf16x8 &b)
+{
+    asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+
 __device__ __forceinline__ void mfma_acc16(f32x4 &acc, const bf16x8 &a, const bf16x8 &b)
 {
     asm("s_nop 1\n\tv_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
@@ -416,7 +429,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
                 const int sl = k >> 2, ft = k & 3, k1 = (k + 1) & 15;
                 const bf16x8 An = tr16(slots + (k1 >> 2) * kSlot, la, 2 * wave + ((k1 & 3) >> 1), k1 & 1);
                 wfence();
-                mfma_acc16(dwh[ft], A, bd[sl]);
+                mfma_acc16_lds(dwh[ft], A, bd[sl]);
                 if (ft == 3)
                     mfma_acc16(dbh, ones_w0, bd[sl]);
                 wfence();
@@ -485,8 +498,8 @@ __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
                     if (st + 1 < 16)
                         ld(st + 1, nxt);
                     __builtin_amdgcn_sched_barrier(0);
-                    mfma_acc32(dw2[0], cur[1], cur[0]);
-                    mfma_acc32(dw2[1], cur[2], cur[0]);
+                    mfma_acc32_lds(dw2[0], cur[1], cur[0]);
+                    mfma_acc32_lds(dw2[1], cur[2], cur[0]);
                     mfma_acc32(db2, cur[1], ((st >> 1) & 1) == 0 ? ones_pl0 : ones_pl1);
                     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll

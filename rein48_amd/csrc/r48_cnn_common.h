@@ -107,7 +107,14 @@ __device__ __forceinline__ bf16x8 frag_at(const uint4 *w, int frag, int lane)
 // LDS read exposes the read's latency, so the fragment of the next MFMA is read before the current
 // one issues. wfence() keeps that order (DS reads and MFMAs may not cross it; VALU, SALU and
 // transcendental work may, so epilogues still interleave with the MFMA stream).
-__device__ __forceinline__ void wfence() { __builtin_amdgcn_sched_barrier(0x406); }
+#ifndef R48_WFENCE
+#define R48_WFENCE 0x406
+#endif
+__device__ __forceinline__ void wfence()
+{
+    if (R48_WFENCE >= 0)
+        __builtin_amdgcn_sched_barrier(R48_WFENCE);
+}
 
 // A fragment of forward MFMA i (0..88) in issue order: conv1 positions R = 0..8, then the 8 conv2
 // chains c = 2p + g (8 W2 fragments (kk, s) each) with the 2 head MFMAs of chain c issued after
