@@ -23,8 +23,11 @@ Extra objects on the JSON line:
                 Game + Rand, calibrated against the reference in BASELINE.md) on one process
                 per available host CPU (at most 16, the box's share) for a bounded sample,
                 plus the 1-process figure; rank 0, N=1 only (oracle/port_bench.py).
-  extras        HBM-honest point (2^26 boards/GPU, past the 256 MiB Infinity Cache), the
-                fused random-policy rollout kernel, and the C oracle as a strong CPU line.
+  extras        N=1: HBM-honest point (2^26 boards/GPU, past the 256 MiB Infinity Cache), the
+                fused random-policy rollout kernel, config 3 (A3C + CNN), config 5 per GPU (DQN
+                + ResNet-10 + HBM replay) and the C oracle as a strong CPU line. N>1: config 4
+                (A3C, 2^20 boards per GPU) and config 5 (DQN, 2^21 boards per GPU) on all ranks
+                with the RCCL gradient all-reduce (--no-extras skips them).
 """
 import argparse
 import json
@@ -142,31 +145,44 @@ def extras(dev, seed, n_small):
     return out
 
 
-def a3c_config3(dev, seed, n_boards, updates=2):
-    """BASELINE configs[2]: 2^20 boards + 2-layer CNN policy (bf16 MFMA via hipBLASLt), A3C
-    rollout (MAX_STEP_NUM = 100 steps: features kernel -> CNN -> fused softmax/Philox sampling
-    -> env kernel) and the synchronous update (chunked forward/backward, TF1 RMSProp kernel)."""
+def _sync_max(ms_list, dev, world):
+    """Per-phase mean device time (ms), max over ranks (the slowest replica sets the pace)."""
+    return max_over_ranks(sum(ms_list) / len(ms_list), dev, world)
+
+
+def a3c_config3(dev, seed, n_boards, updates=2, world=1):
+    """BASELINE configs[2] (world 1: 2^20 boards + 2-layer CNN policy on 1 MI355X) and configs[3]
+    (world > 1: 2^20 boards per GPU, 8M boards on 8 GPUs, one RCCL all-reduce of the flat fp32
+    gradient per update): A3C rollout (MAX_STEP_NUM = 100 steps: fused CNN inference + softmax +
+    Philox sampling -> env kernel) and the synchronous update (fused MFMA gradient pass,
+    all-reduce, TF1 RMSProp kernel)."""
     from rein48_amd.a3c import A3CConfig, A3CTrainer
     cfg = A3CConfig(n_boards=n_boards, max_steps=100, mode="textbook", net="cnn", bf16=True,
                     features="exponents", seed=seed, update_chunk=10)
     tr = A3CTrainer(cfg, device=dev)
-    tr.train_step()                                   # warm-up (allocator, hipBLASLt heuristics)
+    tr.train_step()                                   # warm-up (allocator, kernels, first collective)
     s = torch.cuda.current_stream(dev)
     roll_ms, upd_ms, steps = [], [], 0
     for _ in range(updates):
         a, b, c = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
         a.record(s)
         tr.rollout()
         b.record(s)
-        out = tr.update()
+        out = tr.update()                             # includes the gradient all-reduce when world > 1
         c.record(s)
         torch.cuda.synchronize(dev)
         roll_ms.append(a.elapsed_time(b))
         upd_ms.append(b.elapsed_time(c))
         steps += int(tr.lengths.sum())
-    r, u = sum(roll_ms) / updates, sum(upd_ms) / updates
-    board_steps = n_boards * cfg.max_steps          # every board is stepped every rollout step
-    return {"boards": n_boards, "net": "cnn (conv2x2x32, conv2x2x64, heads 256->4/1), bf16 autocast",
+    r, u = _sync_max(roll_ms, dev, world), _sync_max(upd_ms, dev, world)
+    board_steps = world * n_boards * cfg.max_steps  # every board is stepped every rollout step
+    return {"boards": world * n_boards, "boards_per_gpu": n_boards, "n_gpus": world,
+            "net": "cnn (conv2x2x32, conv2x2x64, heads 256->4/1), bf16",
+            "gradient_allreduce": ("RCCL all_reduce(SUM)/world of %d fp32 per update" % tr.flat.grad.numel())
+            if world > 1 else None,
             "rollout_ms": r, "update_ms": u,
             "rollout_env_steps_per_s": board_steps / (r * 1e-3),
             "train_env_steps_per_s": board_steps / ((r + u) * 1e-3),
@@ -174,11 +190,12 @@ def a3c_config3(dev, seed, n_boards, updates=2):
             "last_losses": {k: out[k] for k in ("actor_loss", "critic_loss")}}
 
 
-def dqn_config5(dev, seed, n_boards, steps=3):
-    """BASELINE configs[4] per GPU (16M boards over 8 GPUs = 2^21 per GPU): ResNet-10 Q-network
-    in bf16 (structured-GEMM convs on hipBLASLt), epsilon-greedy acting on every board, env step
-    with merge reward + auto-reset, (s, a, r, s', done) of every board into the HBM replay ring,
-    one 64K-transition double-DQN update per env step."""
+def dqn_config5(dev, seed, n_boards, steps=3, world=1):
+    """BASELINE configs[4] (16M boards over 8 GPUs = 2^21 per GPU): ResNet-10 Q-network in bf16
+    (fused MFMA inference kernel for acting, structured-GEMM training path), epsilon-greedy acting
+    on every board, env step with merge reward + auto-reset, (s, a, r, s', done) of every board
+    into the HBM replay ring, one 64K-transition double-DQN update per env step (gradient
+    all-reduced over RCCL when world > 1; each rank samples its own ring shard)."""
     from rein48_amd.dqn import DQNConfig, DQNTrainer
     cfg = DQNConfig(n_boards=n_boards, replay_capacity=1 << 25, batch=1 << 16, learn_start=1, seed=seed,
                     act_chunk=1 << 18)
@@ -188,6 +205,9 @@ def dqn_config5(dev, seed, n_boards, steps=3):
     act, env, upd = [], [], []
     for _ in range(steps):
         e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
         e[0].record(s)
         st = tr.env.boards.clone()
         a = tr.act()
@@ -202,14 +222,16 @@ def dqn_config5(dev, seed, n_boards, steps=3):
         act.append(e[0].elapsed_time(e[1]))
         env.append(e[1].elapsed_time(e[2]))
         upd.append(e[2].elapsed_time(e[3]))
-    a_ms, e_ms, u_ms = (sum(x) / steps for x in (act, env, upd))
-    from rein48_amd.dqn.nets import ResNet10Q
+    a_ms, e_ms, u_ms = (_sync_max(x, dev, world) for x in (act, env, upd))
     C = cfg.channels
     useful = 2 * 100 * (18 * C + 2 * cfg.blocks * C * C) + 2 * 16 * C * 4     # valid taps only
-    return {"boards": n_boards, "net": "ResNet-10 (stem + 4 basic blocks, C=%d, BN) bf16" % C,
-            "replay_capacity": cfg.replay_capacity, "batch": cfg.batch,
+    return {"boards": world * n_boards, "boards_per_gpu": n_boards, "n_gpus": world,
+            "net": "ResNet-10 (stem + 4 basic blocks, C=%d, BN) bf16" % C,
+            "replay_capacity_per_gpu": cfg.replay_capacity, "batch_per_gpu": cfg.batch,
+            "gradient_allreduce": ("RCCL all_reduce(SUM)/world of %d fp32 per update" % tr.flat.grad.numel())
+            if world > 1 else None,
             "act_ms": a_ms, "env_step_store_ms": e_ms, "update_ms": u_ms,
-            "env_steps_per_s": n_boards / ((a_ms + e_ms + u_ms) * 1e-3),
+            "env_steps_per_s": world * n_boards / ((a_ms + e_ms + u_ms) * 1e-3),
             "act_useful_TFLOPs": n_boards * useful / (a_ms * 1e-3) / 1e12,
             "act_frac_of_bf16_dense_peak": n_boards * useful / (a_ms * 1e-3) / 2.5e15,
             "loss": out["loss"]}
@@ -284,10 +306,15 @@ def main():
     cpu_line = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu_line = cpu_baseline(args.cpu_seconds)          # before this process touches the GPU
+    # R48_DIST_BACKEND=gloo only rehearses several ranks sharing one GPU (RCCL refuses two ranks
+    # on one device); the product path is RCCL ("nccl" on ROCm), one rank per GPU
+    backend = os.environ.get("R48_DIST_BACKEND", "nccl")
+    if backend != "nccl":
+        local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        dist.init_process_group(backend, device_id=dev if backend == "nccl" else None)
 
     from rein48_amd import VecGame
 
@@ -358,6 +385,16 @@ def main():
             ex["dqn_config5"] = {"error": repr(e)}
         if not args.no_cpu_baseline:
             ex["cpu_strong_line"] = strong_cpu_line()
+        line["extras"] = ex
+    if world > 1 and not args.no_extras:
+        # BASELINE configs[3] (A3C, 2^20 boards per GPU: 8M on 8 GPUs) and configs[4] (DQN,
+        # 2^21 boards per GPU: 16M on 8 GPUs), every rank stepping its own shard, gradients
+        # all-reduced over RCCL. Every rank issues the same collective sequence (barriers, one
+        # broadcast per trainer, one all-reduce per update, max-reductions of the phase times).
+        ex = {}
+        for key, fn in (("a3c_config4", lambda: a3c_config3(dev, args.seed, n, world=world)),
+                        ("dqn_config5", lambda: dqn_config5(dev, args.seed, 1 << 21, world=world))):
+            ex[key] = fn()
         line["extras"] = ex
     if rank == 0:
         print(json.dumps(line), flush=True)

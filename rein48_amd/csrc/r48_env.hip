@@ -28,15 +28,27 @@ constexpr int kBlock = 256;
 constexpr int kMaxChains = 2;
 constexpr int64_t kChainMin = (int64_t)1 << 18;
 
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+#ifndef R48_NT_BOARDS
+#define R48_NT_BOARDS 0   // experiments: 1 = nontemporal board loads, 2 = stores, 3 = both
+#endif
+
 __device__ __forceinline__ Board load_board(const int8_t *boards, int64_t i)
 {
-    const uint4 v = *reinterpret_cast<const uint4 *>(boards + 16 * i);
+    const u32x4 *p = reinterpret_cast<const u32x4 *>(boards + 16 * i);
+    const u32x4 v = (R48_NT_BOARDS & 1) ? __builtin_nontemporal_load(p) : *p;
     return Board{v.x, v.y, v.z, v.w};
 }
 
 __device__ __forceinline__ void store_board(int8_t *boards, int64_t i, const Board &b)
 {
-    *reinterpret_cast<uint4 *>(boards + 16 * i) = make_uint4(b.w0, b.w1, b.w2, b.w3);
+    u32x4 *p = reinterpret_cast<u32x4 *>(boards + 16 * i);
+    const u32x4 v = {b.w0, b.w1, b.w2, b.w3};
+    if (R48_NT_BOARDS & 2)
+        __builtin_nontemporal_store(v, p);
+    else
+        *p = v;
 }
 
 __device__ __forceinline__ void philox_words(uint32_t w[4], uint64_t gid, uint32_t ctr, uint32_t tag,
@@ -137,6 +149,28 @@ __device__ __forceinline__ void emit(const LaneOut &r, int64_t i, int8_t *boards
         score[i] = (int32_t)r.score;
 }
 
+// both boards of a pair (i even): one 2-byte store per byte plane, so a wave's action / done /
+// changed stores are each one contiguous 128-byte run
+template <bool RANDOM, bool REWARD>
+__device__ __forceinline__ void emit_pair(const LaneOut &e, const LaneOut &o, int64_t i, int8_t *boards,
+                                          int8_t *actions, uint8_t *done, uint8_t *changed, int32_t *reward,
+                                          int32_t *score)
+{
+    store_board(boards, i, e.b);
+    store_board(boards, i + 1, o.b);
+    if (RANDOM && actions)
+        *reinterpret_cast<uint16_t *>(actions + i) = (uint16_t)((e.a & 0xffu) | (o.a << 8));
+    if (done)
+        *reinterpret_cast<uint16_t *>(done + i) = (uint16_t)(e.done | (o.done << 8));
+    if (changed)
+        *reinterpret_cast<uint16_t *>(changed + i) = (uint16_t)(e.changed | (o.changed << 8));
+    if (reward)
+        *reinterpret_cast<uint2 *>(reward + i) =
+            make_uint2(REWARD ? e.reward : 0u, REWARD ? o.reward : 0u);
+    if (score)
+        *reinterpret_cast<uint2 *>(score + i) = make_uint2(e.score, o.score);
+}
+
 // The Philox step counter is `step_arg` (eager launches) or `*d_ctr + step_arg` (graph
 // replays: node k of a captured chunk carries step_arg = k and the launch function sets
 // *d_ctr to the env's counter with a memset before each replay).
@@ -159,7 +193,10 @@ __global__ __launch_bounds__(kBlock) void k_step(int8_t *__restrict__ boards, in
     const int64_t base = (int64_t)blockIdx.x * kTile + 2 * (int64_t)threadIdx.x;
     const uint32_t step = (d_ctr ? *d_ctr : 0u) + step_arg;
     const bool want_score = score != nullptr;
-    if ((int64_t)(blockIdx.x + 1) * kTile <= n && (gid0 & 1) == 0) {
+    // the pair path stores 2-byte / 8-byte pairs: caller planes must be aligned for that
+    const bool aligned = ((((uintptr_t)actions | (uintptr_t)done | (uintptr_t)changed) & 1u) |
+                          (((uintptr_t)reward | (uintptr_t)score) & 7u)) == 0;
+    if ((int64_t)(blockIdx.x + 1) * kTile <= n && (gid0 & 1) == 0 && aligned) {
         Board b[2 * NP];
 #pragma unroll
         for (int j = 0; j < NP; j++) {
@@ -171,17 +208,22 @@ __global__ __launch_bounds__(kBlock) void k_step(int8_t *__restrict__ boards, in
         for (int j = 0; j < NP; j++) {
             const int64_t i = base + 2 * kBlock * j;
             Draw de, dd;
+#if defined(R48_ABLATE_STEP_COPY)
+            // timing floor only (tools/exp_step_variants.py): same launches and I/O, no compute
+            r[2 * j] = LaneOut{Board{b[2 * j].w0 ^ step, b[2 * j].w1, b[2 * j].w2, b[2 * j].w3}, step & 3u, 0u, 0u, 0u, 0u};
+            r[2 * j + 1] = LaneOut{Board{b[2 * j + 1].w0 ^ step, b[2 * j + 1].w1, b[2 * j + 1].w2, b[2 * j + 1].w3},
+                                   step & 3u, 0u, 0u, 0u, 0u};
+            continue;
+#endif
             pair_draws((uint64_t)(gid0 + i) >> 1, step, k0, k1, de, dd);
             r[2 * j] = step_lane<RANDOM, AUTO_RESET, REWARD, NP == 1>(b[2 * j], i, de, actions, want_score, err);
             r[2 * j + 1] =
                 step_lane<RANDOM, AUTO_RESET, REWARD, NP == 1>(b[2 * j + 1], i + 1, dd, actions, want_score, err);
         }
 #pragma unroll
-        for (int j = 0; j < NP; j++) {
-            emit<RANDOM, REWARD>(r[2 * j], base + 2 * kBlock * j, boards, actions, done, changed, reward, score);
-            emit<RANDOM, REWARD>(r[2 * j + 1], base + 2 * kBlock * j + 1, boards, actions, done, changed, reward,
-                                 score);
-        }
+        for (int j = 0; j < NP; j++)
+            emit_pair<RANDOM, REWARD>(r[2 * j], r[2 * j + 1], base + 2 * kBlock * j, boards, actions, done, changed,
+                                      reward, score);
     } else {
         for (int j = 0; j < 2 * NP; j++) {
             const int64_t i = base + 2 * kBlock * (j >> 1) + (j & 1);
