@@ -268,6 +268,24 @@ int r48_resnet_q_forward(const int8_t *boards, int64_t n, const void *wblob, con
                          int64_t gid0, uint32_t ctr, void *stream);
 int64_t r48_resnet_q_blob_bytes(void);
 
+/* Training-mode BatchNorm fused with ReLU and the basic block's identity add, for the ResNet-10
+ * update (rein48_amd/dqn/nets.py, bn.py; replaces torch.nn.BatchNorm1d + F.relu + add on
+ * channels-last bf16 activations). x, residual, y, dy, dx, dresidual: bf16 [rows][C], 16-byte
+ * aligned, C in {32, 64, 128}; gamma, beta, running statistics, dgamma, dbeta: float[C].
+ * Forward: y = relu?(gamma (x - mean) invstd + beta (+ residual)) with the batch statistics over
+ * rows (biased variance), running_mean/var (nullable together) updated with `momentum` and the
+ * unbiased variance, save = float[2 C] {mean, invstd} for the backward. Backward: given dy
+ * (gradient of y) and the saved y (ReLU mask, when relu) -> dx, dgamma, dbeta (nullable) and
+ * dresidual (nullable: the gradient reaching the residual input). workspace: float[
+ * r48_bn_workspace_floats(rows, C)], not shared between calls in flight. Deterministic. */
+int64_t r48_bn_workspace_floats(int64_t rows, int32_t C);
+int r48_bn_forward(const void *x, const void *residual, int64_t rows, int32_t C, const float *gamma,
+                   const float *beta, float *running_mean, float *running_var, float momentum, float eps,
+                   int32_t relu, float *save, float *workspace, void *y, void *stream);
+int r48_bn_backward(const void *dy, const void *y, const void *x, int64_t rows, int32_t C, const float *gamma,
+                    const float *save, int32_t relu, float *workspace, void *dx, void *dresidual, float *dgamma,
+                    float *dbeta, void *stream);
+
 /* Thread-local message of the last failed call on this thread ("" if none). */
 const char *r48_last_error(void);
 /* "rein48 <version> gfx950" */

@@ -80,6 +80,7 @@ class ResNet10Q(nn.Module):
         super().__init__()
         self.dtype = dtype
         self.channels, self.n_blocks, self.use_bn = channels, blocks, bn
+        self.fused_bn = True          # training-mode BN + ReLU (+ add) via r48_bn_* on bf16 GPU tensors
         C = channels
         self.stem = nn.Conv2d(PLANES, C, 3, padding=1)
         self.convs = nn.ModuleList([nn.Conv2d(C, C, 3, padding=1) for _ in range(2 * blocks)])
@@ -109,14 +110,30 @@ class ResNet10Q(nn.Module):
     def _conv(self, conv, h):
         return linear(h, dense_conv_weight(conv), conv.bias.repeat(16), self.dtype)
 
+    def _fused_bn(self, h):
+        return (self.use_bn and self.fused_bn and self.training and h.is_cuda and h.dtype == torch.bfloat16
+                and self.channels in (32, 64, 128))
+
+    def _bn_relu(self, k, h, residual=None):
+        """relu(BN_k(h) (+ residual)): on bf16 GPU activations in training mode one fused HIP pass
+        forward and backward (bn.py), else torch's BatchNorm1d + ReLU."""
+        if self._fused_bn(h):
+            from .bn import bn_act
+            B = h.shape[0]
+            r = None if residual is None else residual.reshape(B * 16, self.channels)
+            return bn_act(h.reshape(B * 16, self.channels), self.bns[k], r).view(B, 16 * self.channels)
+        z = self._bn(k, h)
+        if residual is not None:
+            z = z + residual.to(z.dtype)
+        return F.relu(z).to(self.dtype)
+
     def forward(self, x):
         d = self.dtype
-        h = F.relu(self._bn(0, self._conv(self.stem, x))).to(d)
+        h = self._bn_relu(0, self._conv(self.stem, x))
         for b in range(self.n_blocks):
             c1, c2 = self.convs[2 * b], self.convs[2 * b + 1]
-            y = F.relu(self._bn(1 + 2 * b, self._conv(c1, h))).to(d)
-            z = self._bn(2 + 2 * b, self._conv(c2, y))
-            h = F.relu(z + h.to(z.dtype)).to(d)
+            y = self._bn_relu(1 + 2 * b, self._conv(c1, h))
+            h = self._bn_relu(2 + 2 * b, self._conv(c2, y), residual=h)
         return linear(h, self.head.weight, self.head.bias, d).float()
 
     @torch.no_grad()

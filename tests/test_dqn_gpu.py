@@ -168,3 +168,109 @@ def test_fused_resnet_matches_torch(empty_frac):
     assert e_k <= 1.5 * e_t + 1e-3 and e_k <= 5e-2, (e_k, e_t)
     _, act = resnet_q_forward(bt, packed, q=False, actions=True, eps=0.25, seed=11, ctr=3, gid0=40)
     assert torch.equal(act, egreedy_actions(q, 0.25, 11, 3, gid0=40))
+
+
+def _bn_case(rows, C, res, relu, seed):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    x = torch.randn(rows, C, generator=g) * (torch.rand(C, generator=g) * 2 + 0.5) + torch.randn(C, generator=g) * 3
+    r = torch.randn(rows, C, generator=g) if res else None
+    gamma = torch.rand(C, generator=g) + 0.5
+    beta = torch.randn(C, generator=g) * 0.3
+    dy = torch.randn(rows, C, generator=g).to(torch.bfloat16).float()
+    return x, r, gamma, beta, dy
+
+
+def _torch_bn_act(x, r, gamma, beta, rm, rv, relu, dtype):
+    """torch.nn.functional reference in `dtype` (fp32: the reference; bf16: torch's own rounding)."""
+    xs = x.to(DEV, dtype).requires_grad_(True)
+    gs, bs = gamma.to(DEV).requires_grad_(True), beta.to(DEV).requires_grad_(True)
+    z = torch.nn.functional.batch_norm(xs, rm, rv, gs, bs, training=True, momentum=0.1, eps=1e-5)
+    rs = None
+    if r is not None:
+        rs = r.to(DEV, dtype).requires_grad_(True)
+        z = z + rs
+    y = torch.relu(z) if relu else z
+    return xs, rs, gs, bs, y
+
+
+@pytest.mark.parametrize("rows,C,res,relu", [(1 << 16, 64, False, True), (1 << 16, 64, True, True),
+                                             (100_003, 64, True, False), (4099, 32, False, True),
+                                             (20_000, 128, True, True)])
+def test_fused_bn_act_matches_torch(rows, C, res, relu):
+    """r48_bn_forward / r48_bn_backward (bn.py) vs F.batch_norm (+ add, ReLU) in training mode.
+    Forward y and backward dx / d(residual) are bf16: their error vs the fp32 reference is within
+    1.5x (+1e-3) of PyTorch's own bf16 path's error; so are dgamma / dbeta (fp32 sums over all
+    rows; + 1e-3 of their mean magnitude); running statistics (fp32) within 1e-4. All paths see
+    the same bf16-representable x, residual and dy. Channel means are offset by up to ~3
+    std-devs (the shifted sums must not cancel)."""
+    from rein48_amd.dqn.bn import bn_act
+    x, r, gamma, beta, dy = _bn_case(rows, C, res, relu, seed=rows + C)
+    ref_rm, ref_rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+    x = x.to(torch.bfloat16).float()             # every path sees the same (bf16-representable) input
+    if res:
+        r = r.to(torch.bfloat16).float()
+    xs, rs, gs, bs, y32 = _torch_bn_act(x, r, gamma, beta, ref_rm, ref_rv, relu, torch.float32)
+    y32.backward(dy.to(DEV))
+    t_rm, t_rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+    xt, rt, gt, bt, y16 = _torch_bn_act(x, r, gamma, beta, t_rm, t_rv, relu, torch.bfloat16)
+    y16.backward(dy.to(DEV, torch.bfloat16))
+
+    bn = torch.nn.BatchNorm1d(C).to(DEV).train()
+    with torch.no_grad():
+        bn.weight.copy_(gamma)
+        bn.bias.copy_(beta)
+    xk = x.to(DEV, torch.bfloat16).requires_grad_(True)
+    rk = r.to(DEV, torch.bfloat16).requires_grad_(True) if res else None
+    yk = bn_act(xk, bn, rk, relu=relu)
+    yk.backward(dy.to(DEV, torch.bfloat16))
+
+    def worst(a, ref):
+        a, ref = a.detach().float(), ref.detach().float()
+        return float(((a - ref).abs() / (ref.abs() + ref.abs().mean())).max())
+
+    for got, torch16, ref in ((yk, y16, y32), (xk.grad, xt.grad, xs.grad)) + \
+            (((rk.grad, rt.grad, rs.grad),) if res else ()):
+        e_k, e_t = worst(got, ref), worst(torch16, ref)
+        assert e_k <= 1.5 * e_t + 1e-3, (e_k, e_t)
+    for got, torch16, ref in ((bn.weight.grad, gt.grad, gs.grad), (bn.bias.grad, bt.grad, bs.grad)):
+        e_k, e_t = float((got - ref).abs().max()), float((torch16 - ref).abs().max())
+        assert e_k <= 1.5 * e_t + 1e-3 * float(ref.abs().mean()), (e_k, e_t)
+    torch.testing.assert_close(bn.running_mean, ref_rm, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(bn.running_var, ref_rv, rtol=1e-4, atol=1e-4)
+    assert int(bn.num_batches_tracked) == 1
+    yk2 = bn_act(xk.detach(), bn, None if rk is None else rk.detach(), relu=relu)   # deterministic
+    assert torch.equal(bn_act(xk.detach(), bn, None if rk is None else rk.detach(), relu=relu), yk2)
+
+
+def test_resnet_update_fused_bn_matches_torch_bn():
+    """One training forward/backward of the bf16 ResNet10Q with the fused BN path vs the same
+    net through torch's BatchNorm1d: losses agree to bf16 precision and every parameter gradient
+    is close in relative norm (both are bf16 computations of the same fp32 function)."""
+    from rein48_amd.dqn.kernels import board_onehot
+    from rein48_amd.dqn.nets import ResNet10Q
+    torch.manual_seed(9)
+    net = ResNet10Q(dtype=torch.bfloat16).to(DEV).train()
+    with torch.no_grad():
+        net.head.weight.normal_(std=0.05)
+    b = torch.from_numpy(np.random.default_rng(9).integers(0, 12, size=(8192, 16)).astype(np.int8)).to(DEV)
+    x = board_onehot(b, dtype=torch.bfloat16)
+    tgt = torch.randn(8192, 4, device=DEV)
+    grads, losses, stats = [], [], []
+    for fused in (True, False):
+        net.fused_bn = fused
+        net.zero_grad()
+        for m in net.bns:
+            m.reset_running_stats()
+        loss = torch.nn.functional.smooth_l1_loss(net(x), tgt)
+        loss.backward()
+        losses.append(float(loss.detach()))
+        # conv biases feed a BN, which removes them: their exact gradient is 0 and both paths
+        # return rounding noise, so they are not compared
+        grads.append([p.grad.detach().float().clone() for k, p in net.named_parameters()
+                      if not (k.endswith(".bias") and (k.startswith("stem") or k.startswith("convs")))])
+        stats.append([m.running_var.clone() for m in net.bns])
+    assert abs(losses[0] - losses[1]) <= 1e-2 * abs(losses[1])
+    for ga, gb in zip(*grads):
+        assert float((ga - gb).norm()) <= 5e-2 * float(gb.norm()) + 1e-6
+    for sa, sb in zip(*stats):
+        torch.testing.assert_close(sa, sb, rtol=1e-2, atol=1e-3)
