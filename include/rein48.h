@@ -180,11 +180,13 @@ int r48_rmsprop_tf1(float *var, const float *grad, float *ms, float *mom, int64_
  * conv trunk of algorithm/ddpg/actor.py:51-85 with actor/critic heads) on bf16 MFMA:
  * boards int8[n][16] -> logits float[n][4] and value float[n] (each nullable), and, when
  * actions != NULL, the choose_action draw of r48_sample_actions (same Philox contract) into
- * actions int8[n]. wfrag: 41 x 64 x 8 bf16 weight fragments and bias: 104 floats, both packed
- * by rein48_amd/a3c/fused.py:pack_cnn (16-byte aligned). mode: R48_FEAT_VALUES/EXPONENTS. */
+ * actions int8[n]; boards_out (nullable, 16-byte aligned): a copy of the input boards (the
+ * rollout's trajectory snapshot, a3c.py:203-209). wfrag: 41 x 64 x 8 bf16 weight fragments and
+ * bias: 104 floats, both packed by rein48_amd/a3c/fused.py:pack_cnn (16-byte aligned). mode:
+ * R48_FEAT_VALUES/EXPONENTS. */
 int r48_cnn_policy_forward(const int8_t *boards, int64_t n, const void *wfrag, const float *bias,
-                           int32_t mode, float *logits, float *value, int8_t *actions, uint64_t seed,
-                           int64_t gid0, uint32_t ctr, void *stream);
+                           int32_t mode, float *logits, float *value, int8_t *actions, int8_t *boards_out,
+                           uint64_t seed, int64_t gid0, uint32_t ctr, void *stream);
 
 /* Fused A3C update for the CNN (configs 3-4; rein48_amd/a3c/losses.py restating a3c.py:99-123):
  * the gradient of (actor + critic) over `rows` training states w.r.t. every ActorCriticCNN

@@ -124,19 +124,24 @@ def cnn_train_grad(net, boards, actions, targets, wn, cm=None, counts=None, beta
 
 
 def cnn_forward(boards, wfrag, bias, exponents=False, logits=True, value=True, actions=False, seed=0, ctr=0,
-                gid0=0):
+                gid0=0, actions_out=None, boards_out=None):
     """Fused CNN inference over int8 boards [n, 16]. Returns (logits [n,4], value [n], actions [n])
-    with the unrequested ones None."""
+    with the unrequested ones None. actions_out: int8 [n] to draw into (implies actions);
+    boards_out: int8 [n, 16] that receives a copy of the boards (the rollout's snapshot)."""
     if not boards.is_cuda or boards.dtype != torch.int8 or not boards.is_contiguous():
         raise ValueError("boards must be a contiguous int8 GPU tensor")
     n = boards.numel() // 16
     dev = boards.device
+    for t, name, numel in ((actions_out, "actions_out", n), (boards_out, "boards_out", 16 * n)):
+        if t is not None and (not t.is_cuda or t.dtype != torch.int8 or not t.is_contiguous() or t.numel() != numel):
+            raise ValueError("%s must be a contiguous int8 GPU tensor of %d elements" % (name, numel))
     lg = torch.empty((n, 4), dtype=torch.float32, device=dev) if logits else None
     v = torch.empty(n, dtype=torch.float32, device=dev) if value else None
-    a = torch.empty(n, dtype=torch.int8, device=dev) if actions else None
+    a = actions_out if actions_out is not None else (torch.empty(n, dtype=torch.int8, device=dev) if actions else None)
     check(_lib.load().r48_cnn_policy_forward(ptr(boards), n, ptr(wfrag), ptr(bias),
                                              _lib.FEAT_EXPONENTS if exponents else _lib.FEAT_VALUES,
-                                             ptr(lg), ptr(v), ptr(a), int(seed) & (2 ** 64 - 1), int(gid0),
+                                             ptr(lg), ptr(v), ptr(a), ptr(boards_out), int(seed) & (2 ** 64 - 1),
+                                             int(gid0),
                                              int(ctr) & 0xFFFFFFFF,
                                              C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)))
     return lg, v, a

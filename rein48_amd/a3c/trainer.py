@@ -93,21 +93,22 @@ class A3CTrainer:
         fused = cfg.net == "cnn" and cfg.bf16 and cfg.fused_policy
         if fused:
             wfrag, bias = pack_cnn(self.net)   # weights are fixed for the whole rollout
-        for t in range(cfg.max_steps):
-            self.boards[t].copy_(env.boards)
-            if fused:   # board -> CNN -> softmax -> Philox draw in one kernel
-                _, _, act = cnn_forward(env.boards, wfrag, bias, exponents=cfg.features == "exponents",
-                                        logits=False, value=False, actions=True, seed=cfg.seed,
-                                        ctr=self.sample_ctr, gid0=self.gid0)
-            else:
+        if merge and getattr(self, "_rewards_i32", None) is None:
+            self._rewards_i32 = torch.zeros((cfg.max_steps, cfg.n_boards), dtype=torch.int32, device=self.device)
+        if fused:   # board -> CNN -> softmax -> Philox draw in one kernel, then the env kernel
+            self._rollout_fused(wfrag, bias, merge)
+        else:
+            for t in range(cfg.max_steps):
+                self.boards[t].copy_(env.boards)
                 logits, _ = self._net(self._features(env.boards))
                 act, _, _ = K.sample_actions(logits.contiguous(), cfg.seed, self.sample_ctr, gid0=self.gid0)
-            self.sample_ctr += 1
-            _, reward, done = env.step(act, merge_reward=merge)
-            self.actions[t].copy_(act)
-            self.done[t].copy_(done)
-            if merge:
-                self.rewards[t].copy_(reward)
+                self.actions[t].copy_(act)
+                self.sample_ctr += 1
+                # done (and the merge reward) land in the trajectory rows directly
+                env.step(act, merge_reward=merge, done_out=self.done[t],
+                         reward_out=self._rewards_i32[t] if merge else None)
+        if merge:
+            self.rewards.copy_(self._rewards_i32)     # one int32 -> fp32 pass for the whole rollout
         self.boards[cfg.max_steps].copy_(env.boards)
         # segment length: through the first done step, else max_steps (a3c.py:201)
         notdone = (self.done.cumsum(0) == 0)
@@ -116,6 +117,31 @@ class A3CTrainer:
         t = torch.arange(cfg.max_steps, device=self.device).unsqueeze(1)
         self.mask = t < self.lengths.unsqueeze(0)
         return self.lengths
+
+    def _rollout_fused(self, wfrag, bias, merge):
+        """The fused rollout's T steps as two raw C-ABI calls each: r48_cnn_policy_forward (CNN,
+        softmax, Philox draw; writes the board snapshot boards[t] and the action actions[t]) and
+        r48_env_step (reads actions[t]; writes done[t] and the merge reward). The buffers are the
+        trainer's own contiguous trajectory tensors, so the per-call tensor checks of
+        cnn_forward / VecGame.step are skipped: the host issues a step in a few microseconds and
+        never gates the GPU (through the checked wrappers the rollout was host-bound)."""
+        cfg, env = self.cfg, self.env
+        lib = _lib.load()
+        n = cfg.n_boards
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        mode = _lib.FEAT_EXPONENTS if cfg.features == "exponents" else _lib.FEAT_VALUES
+        flags = _lib.MERGE_REWARD if merge else 0
+        seed = int(cfg.seed) & (2 ** 64 - 1)
+        bp, wp, biasp = env.boards.data_ptr(), wfrag.data_ptr(), bias.data_ptr()
+        a0, b0, d0 = self.actions.data_ptr(), self.boards.data_ptr(), self.done.data_ptr()
+        r0 = self._rewards_i32.data_ptr() if merge else None
+        for t in range(cfg.max_steps):
+            at = a0 + t * n
+            _lib.check(lib.r48_cnn_policy_forward(bp, n, wp, biasp, mode, None, None, at, b0 + 16 * t * n, seed,
+                                                  self.gid0, self.sample_ctr & 0xFFFFFFFF, stream))
+            self.sample_ctr += 1
+            _lib.check(lib.r48_env_step(env._env, at, flags, d0 + t * n, None,
+                                        None if r0 is None else r0 + 4 * t * n, None, stream))
 
     # ------------------------------------------------------------------ update (a3c.py:218-234)
     def _states(self):

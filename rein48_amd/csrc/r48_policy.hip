@@ -44,8 +44,9 @@ __global__ __launch_bounds__(kThreads, 2) void k_cnn_forward(const int8_t *__res
                                                              const uint4 *__restrict__ wfrag,
                                                              const float *__restrict__ bias,
                                                              float *__restrict__ logits, float *__restrict__ value,
-                                                             int8_t *__restrict__ actions, int64_t gid0, uint32_t k0,
-                                                             uint32_t k1, uint32_t ctr)
+                                                             int8_t *__restrict__ actions,
+                                                             int8_t *__restrict__ boards_out, int64_t gid0,
+                                                             uint32_t k0, uint32_t k1, uint32_t ctr)
 {
     __shared__ uint4 w_lds[kFrags * 64];
     __shared__ __attribute__((aligned(16))) float b_lds[32 + 64 + 8];   // float4 reads (load_bias)
@@ -91,6 +92,8 @@ __global__ __launch_bounds__(kThreads, 2) void k_cnn_forward(const int8_t *__res
         cnn_conv2_heads(w_lds, b_lds, lane, h, h1, ws, h2, out);
         if (!live)
             continue;  // padding lanes of the last tile computed on a clamped duplicate board
+        if (boards_out)  // the rollout's trajectory snapshot of the input board (no separate copy)
+            *reinterpret_cast<uint2 *>(boards_out + 16 * b + 8 * h) = raw;
         // head rows: lane half 0 registers 0..3 = logits 0..3, lane half 1 register 0 = value
         if (h == 0) {
             const float z0 = out[0] + b_lds[96], z1 = out[1] + b_lds[97], z2 = out[2] + b_lds[98],
@@ -124,14 +127,15 @@ int fail(int code, const std::string &msg)
 extern "C" {
 
 int r48_cnn_policy_forward(const int8_t *boards, int64_t n, const void *wfrag, const float *bias, int32_t mode,
-                           float *logits, float *value, int8_t *actions, uint64_t seed, int64_t gid0, uint32_t ctr,
-                           void *stream)
+                           float *logits, float *value, int8_t *actions, int8_t *boards_out, uint64_t seed,
+                           int64_t gid0, uint32_t ctr, void *stream)
 {
     if (!boards || !wfrag || !bias || n < 0 || gid0 < 0 || (mode != R48_FEAT_VALUES && mode != R48_FEAT_EXPONENTS))
         return fail(R48_EINVAL, "NULL argument, n/gid0 < 0 or bad mode");
-    if ((reinterpret_cast<uintptr_t>(boards) | reinterpret_cast<uintptr_t>(wfrag)) & 15u ||
+    if ((reinterpret_cast<uintptr_t>(boards) | reinterpret_cast<uintptr_t>(wfrag) |
+         reinterpret_cast<uintptr_t>(boards_out)) & 15u ||
         (logits && (reinterpret_cast<uintptr_t>(logits) & 15u)))
-        return fail(R48_EINVAL, "boards, wfrag and logits must be 16-byte aligned");
+        return fail(R48_EINVAL, "boards, boards_out, wfrag and logits must be 16-byte aligned");
     if (n == 0)
         return R48_OK;
     int dev = 0, cus = 256;
@@ -142,7 +146,7 @@ int r48_cnn_policy_forward(const int8_t *boards, int64_t n, const void *wfrag, c
     // one instantiation per input encoding (no per-cell branch)
     auto kern = mode == R48_FEAT_VALUES ? k_cnn_forward<R48_FEAT_VALUES> : k_cnn_forward<R48_FEAT_EXPONENTS>;
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kThreads), 0, (hipStream_t)stream, boards, n,
-                       (const uint4 *)wfrag, bias, logits, value, actions, gid0, (uint32_t)seed,
+                       (const uint4 *)wfrag, bias, logits, value, actions, boards_out, gid0, (uint32_t)seed,
                        (uint32_t)(seed >> 32), ctr);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess)

@@ -113,13 +113,16 @@ class VecGame:
         return self.boards
 
     # ------------------------------------------------------------------ step
-    def step(self, actions=None, auto_reset=False, merge_reward=False, want_changed=False, score=None):
+    def step(self, actions=None, auto_reset=False, merge_reward=False, want_changed=False, score=None,
+             done_out=None, reward_out=None):
         """Game.step (GameClient.py:40-51) for every board.
 
         actions: int8[N] tensor of 0..3; None = in-kernel uniform random policy
         (control/rand.py:9-11), the drawn actions land in self.actions.
         Returns (boards, reward, done); reward is all-zero like the reference unless
-        merge_reward. done is evaluated before any auto-reset.
+        merge_reward. done is evaluated before any auto-reset. done_out (uint8[N]) /
+        reward_out (int32[N], with merge_reward) receive done / reward instead of the env's own
+        buffers (a rollout's trajectory rows, no copies).
         """
         flags = (AUTO_RESET if auto_reset else 0) | (MERGE_REWARD if merge_reward else 0)
         if actions is None:
@@ -128,10 +131,12 @@ class VecGame:
         else:
             act = self._t(actions, torch.int8, "actions")
         score = self._t(score, torch.int32, "score")
-        check(self._lib.r48_env_step(self._env, ptr(act), flags, ptr(self.done),
+        done = self.done if done_out is None else self._t(done_out, torch.uint8, "done_out")
+        rew = self.reward if reward_out is None else self._t(reward_out, torch.int32, "reward_out")
+        check(self._lib.r48_env_step(self._env, ptr(act), flags, ptr(done),
                                      ptr(self.changed) if want_changed else None,
-                                     ptr(self.reward) if merge_reward else None, ptr(score), self._s()))
-        return self.boards, (self.reward if merge_reward else self._zero_reward), self.done
+                                     ptr(rew) if merge_reward else None, ptr(score), self._s()))
+        return self.boards, (rew if merge_reward else self._zero_reward), done
 
     def _step_n_args(self, actions, auto_reset, merge_reward, want_changed, score):
         flags = (AUTO_RESET if auto_reset else 0) | (MERGE_REWARD if merge_reward else 0)

@@ -171,6 +171,12 @@ def test_fused_cnn_policy_matches_torch(exponents):
                             seed=9, ctr=4, gid0=17)
     want, _, _ = K.sample_actions(lg, 9, 4, gid0=17)
     assert torch.equal(act, want)
+    # the rollout form: the draw into a trajectory row and the board snapshot, same results
+    a_row = torch.full_like(act, -1)
+    snap = torch.full_like(boards, -1)
+    cnn_forward(boards, wfrag, bias, exponents=exponents, logits=False, value=False, actions=True, seed=9, ctr=4,
+                gid0=17, actions_out=a_row, boards_out=snap)
+    assert torch.equal(a_row, want) and torch.equal(snap, boards)
 
 
 @pytest.mark.parametrize("mode", ["textbook", "reference"])
@@ -249,3 +255,28 @@ def test_trainer_fused_update_matches_torch_update(mode):
                                [outs[1]["actor_loss"], outs[1]["critic_loss"]], rtol=1e-2, atol=1e-6)
     for df, dt in zip(*deltas):
         assert float((df - dt).abs().max()) <= 0.1 * float(dt.abs().max()) + 1e-9
+
+
+def test_fused_rollout_trajectory_replays_through_the_env():
+    """The fused rollout writes the board snapshot (policy kernel), the action and the done flag
+    and merge reward (env kernel) straight into the trajectory rows. Replaying boards[0] with the
+    recorded actions through a fresh env with the same seed and step counters reproduces every
+    boards[t + 1], done[t] and reward[t] bit-for-bit."""
+    from rein48_amd import VecGame
+    from rein48_amd.a3c import A3CConfig, A3CTrainer
+    cfg = A3CConfig(n_boards=4099, max_steps=30, mode="textbook", net="cnn", bf16=True, features="exponents",
+                    seed=21)
+    tr = A3CTrainer(cfg, device=DEV)
+    tr.train_step()
+    before = tr.env.counters
+    tr.rollout()
+    T = cfg.max_steps
+    env = VecGame(cfg.n_boards, device=DEV, seed=cfg.seed)
+    env.counters = before
+    env.reset()                                   # the rollout starts with a reset
+    assert torch.equal(env.boards, tr.boards[0])
+    for t in range(T):
+        _, rew, done = env.step(tr.actions[t], merge_reward=True)
+        assert torch.equal(env.boards, tr.boards[t + 1]), t
+        assert torch.equal(done, tr.done[t]), t
+        assert torch.equal(rew.float(), tr.rewards[t]), t
