@@ -59,6 +59,7 @@ SIGNATURES = {
     "r48_env_reset_with_draws": (C.c_int, [_P, _P, _P, _P, _P]),
     "r48_env_fill_random": (C.c_int, [_P, _U32, _P]),
     "r48_env_step": (C.c_int, [_P, _P, _U32, _P, _P, _P, _P, _P]),
+    "r48_env_set_pingpong_min": (C.c_int, [_P, _I64]),
     "r48_env_step_n": (C.c_int, [_P, _I32, _P, _U32, _P, _P, _P, _P, _P]),
     "r48_env_prepare_step_n": (C.c_int, [_P, _I32, _P, _U32, _P, _P, _P, _P]),
     "r48_env_step_with_draws": (C.c_int, [_P, _P, _P, _P, _U32, _P, _P, _P, _P]),

@@ -27,6 +27,10 @@ constexpr int kBlock = 256;
 // shard's load latency / store drain with the other's compute (1M boards: 10.3 -> 7.2 us).
 constexpr int kMaxChains = 2;
 constexpr int64_t kChainMin = (int64_t)1 << 18;
+// 2^24 boards = 256 MiB, the Infinity Cache: above it both patterns stream from HBM and
+// ping-pong wins (2^26: 384 vs 425 us per step, tools/pingpong_bw.hip); at 2^24 the in-place
+// array still fits the cache and in-place wins (85 vs 101 us)
+constexpr int64_t kPingPongMin = ((int64_t)1 << 24) + 1;
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -171,6 +175,8 @@ __device__ __forceinline__ void emit_pair(const LaneOut &e, const LaneOut &o, in
         *reinterpret_cast<uint2 *>(score + i) = make_uint2(e.score, o.score);
 }
 
+// Boards are read from `src` and written to `boards` (the same array for an in-place step; two
+// arrays when r48_env_step_n ping-pongs a large env through its scratch copy, see launch_step).
 // The Philox step counter is `step_arg` (eager launches) or `*d_ctr + step_arg` (graph
 // replays: node k of a captured chunk carries step_arg = k and the launch function sets
 // *d_ctr to the env's counter with a memset before each replay).
@@ -182,7 +188,7 @@ __device__ __forceinline__ void emit_pair(const LaneOut &e, const LaneOut &o, in
 // as its loads have landed, all stores at the end. The grid's partial last tile and envs whose
 // global board ids start odd (pairs straddling the tile) take the guarded per-board path.
 template <bool RANDOM, bool AUTO_RESET, bool REWARD, int NP>
-__global__ __launch_bounds__(kBlock) void k_step(int8_t *__restrict__ boards, int64_t n, int64_t gid0,
+__global__ __launch_bounds__(kBlock) void k_step(const int8_t *src, int8_t *boards, int64_t n, int64_t gid0,
                                                  uint32_t k0, uint32_t k1, const uint32_t *__restrict__ d_ctr,
                                                  uint32_t step_arg, int8_t *__restrict__ actions,
                                                  uint8_t *__restrict__ done, uint8_t *__restrict__ changed,
@@ -200,8 +206,8 @@ __global__ __launch_bounds__(kBlock) void k_step(int8_t *__restrict__ boards, in
         Board b[2 * NP];
 #pragma unroll
         for (int j = 0; j < NP; j++) {
-            b[2 * j] = load_board(boards, base + 2 * kBlock * j);
-            b[2 * j + 1] = load_board(boards, base + 2 * kBlock * j + 1);
+            b[2 * j] = load_board(src, base + 2 * kBlock * j);
+            b[2 * j + 1] = load_board(src, base + 2 * kBlock * j + 1);
         }
         LaneOut r[2 * NP];
 #pragma unroll
@@ -229,7 +235,7 @@ __global__ __launch_bounds__(kBlock) void k_step(int8_t *__restrict__ boards, in
             const int64_t i = base + 2 * kBlock * (j >> 1) + (j & 1);
             if (i < n) {
                 const Draw d = board_draw((uint64_t)(gid0 + i), step, k0, k1);
-                const LaneOut r = step_lane<RANDOM, AUTO_RESET, REWARD, false>(load_board(boards, i), i, d, actions,
+                const LaneOut r = step_lane<RANDOM, AUTO_RESET, REWARD, false>(load_board(src, i), i, d, actions,
                                                                                want_score, err);
                 emit<RANDOM, REWARD>(r, i, boards, actions, done, changed, reward, score);
             }
@@ -528,6 +534,11 @@ struct r48_env {
     hipStream_t chain[kMaxChains];  // private streams: one per shard chain of r48_env_step_n
     hipEvent_t fork, join[kMaxChains];
     std::map<GraphKey, hipGraphExec_t> graphs;
+    // r48_env_step_n on envs of >= pingpong_min boards alternates the boards between the bound
+    // array and this env-owned copy (read one, write the other): past the Infinity Cache an
+    // in-place read-modify-write sweep moves ~10 % fewer bytes per second than read-A/write-B
+    int8_t *scratch = nullptr;
+    int64_t pingpong_min = kPingPongMin;
 };
 
 namespace {
@@ -644,6 +655,8 @@ int r48_env_destroy(r48_env *env)
         (void)hipEventDestroy(env->fork);
     (void)hipFree(env->d_ctr);
     (void)hipFree(env->err);
+    if (env->scratch)
+        (void)hipFree(env->scratch);
     delete env;
     return R48_OK;
 }
@@ -664,6 +677,23 @@ int r48_env_bind_boards(r48_env *env, int8_t *boards)
 }
 
 int8_t *r48_env_boards(const r48_env *env) { return env ? env->boards : nullptr; }
+
+int r48_env_set_pingpong_min(r48_env *env, int64_t min_boards)
+{
+    if (int s = check_env(env, false))
+        return s;
+    if (min_boards < 0)
+        return fail(R48_EINVAL, "min_boards < 0");
+    env->pingpong_min = min_boards == 0 ? INT64_MAX : min_boards;
+    if (env->n < env->pingpong_min && env->scratch) {
+        for (auto &kv : env->graphs)
+            (void)hipGraphExecDestroy(kv.second);
+        env->graphs.clear();
+        (void)hipFree(env->scratch);
+        env->scratch = nullptr;
+    }
+    return R48_OK;
+}
 
 int64_t r48_env_size(const r48_env *env) { return env ? env->n : 0; }
 
@@ -744,15 +774,19 @@ int validate_step(const r48_env *env, const int8_t *actions, uint32_t flags)
 // (437 vs 428-432 us per step), so only NP = 1 is instantiated.
 void launch_step(r48_env *env, int64_t off, int64_t cnt, const uint32_t *d_ctr, uint32_t step_arg,
                  int8_t *actions, uint32_t flags, uint8_t *done, uint8_t *changed, int32_t *reward, int32_t *score,
-                 hipStream_t stream)
+                 hipStream_t stream, const int8_t *src = nullptr, int8_t *dst = nullptr)
 {
+    if (!src)
+        src = env->boards;
+    if (!dst)
+        dst = env->boards;
     const bool rnd = flags & R48_RANDOM_POLICY, ar = flags & R48_AUTO_RESET, rw = flags & R48_MERGE_REWARD;
     const uint32_t k0 = (uint32_t)env->seed, k1 = (uint32_t)(env->seed >> 32);
     auto at = [off](auto *p) { return p ? p + off : p; };
     auto go = [&](auto kern, int NP) {
         const int64_t tile = (int64_t)kBlock * 2 * NP;
         const dim3 grid((unsigned)((cnt + tile - 1) / tile));
-        hipLaunchKernelGGL(kern, grid, dim3(kBlock), 0, stream, env->boards + 16 * off, cnt, env->gid0 + off, k0,
+        hipLaunchKernelGGL(kern, grid, dim3(kBlock), 0, stream, src + 16 * off, dst + 16 * off, cnt, env->gid0 + off, k0,
                            k1, d_ctr, step_arg, at(actions), at(done), at(changed), at(reward), at(score), env->err);
     };
 #define R48_GO(RN, AR, RW) go(k_step<RN, AR, RW, 1>, 1)
@@ -791,6 +825,17 @@ namespace {
 int chain_graphs(r48_env *env, int32_t n_steps, int8_t *actions, uint32_t flags, uint8_t *done, uint8_t *changed,
                  int32_t *reward, int32_t *score, int chains, hipGraphExec_t *exec)
 {
+    if (env->n >= env->pingpong_min && !env->scratch) {
+        // one allocation per env; without it (out of memory) the chains simply step in place
+        if (hipMalloc(&env->scratch, (size_t)env->n * 16) != hipSuccess) {
+            (void)hipGetLastError();
+            env->scratch = nullptr;
+        } else {
+            for (auto &kv : env->graphs)   // graphs captured in place are stale now
+                (void)hipGraphExecDestroy(kv.second);
+            env->graphs.clear();
+        }
+    }
     if (!env->fork) {
         for (int c = 0; c < kMaxChains; c++)
             if (hipStreamCreateWithFlags(&env->chain[c], hipStreamNonBlocking) != hipSuccess ||
@@ -811,9 +856,16 @@ int chain_graphs(r48_env *env, int32_t n_steps, int8_t *actions, uint32_t flags,
             // step counter from d_ctr
             if (hipStreamBeginCapture(env->chain[c], hipStreamCaptureModeThreadLocal) != hipSuccess)
                 return fail(R48_EHIP, "hipStreamBeginCapture failed");
-            for (int32_t k = 0; k < n_steps; k++)
+            // ping-pong: step k writes the bound array when n_steps - 1 - k is even, else the
+            // scratch copy, and reads what step k - 1 wrote -- the last step always lands in the
+            // bound array (an odd count starts with one in-place step)
+            const int8_t *src = env->boards;
+            for (int32_t k = 0; k < n_steps; k++) {
+                int8_t *dst = (!env->scratch || ((n_steps - 1 - k) & 1) == 0) ? env->boards : env->scratch;
                 launch_step(env, off, cnt, env->d_ctr, (uint32_t)k, actions, flags, done, changed, reward, score,
-                            env->chain[c]);
+                            env->chain[c], src, dst);
+                src = dst;
+            }
             hipGraph_t graph = nullptr;
             const hipError_t ce = hipStreamEndCapture(env->chain[c], &graph);
             if (ce != hipSuccess || !graph)

@@ -158,6 +158,11 @@ class VecGame:
         check(self._lib.r48_env_step_n(self._env, int(n_steps), a[0], a[1], *a[2:], self._s()))
         return self.boards, (self.reward if merge_reward else self._zero_reward), self.done
 
+    def set_pingpong_min(self, min_boards):
+        """Board count from which step_n alternates between the boards and an env-owned scratch
+        copy (default 2^24 + 1, past the Infinity Cache; 0 = never). Results are unchanged."""
+        check(self._lib.r48_env_set_pingpong_min(self._env, int(min_boards)))
+
     def prepare_step_n(self, n_steps, actions=None, auto_reset=False, merge_reward=False, want_changed=False,
                        score=None):
         """Build (capture + instantiate) the graphs step_n would replay, without running them."""

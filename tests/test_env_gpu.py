@@ -435,6 +435,32 @@ def test_step_n_graph_equals_repeated_steps():
     assert a.counters == b.counters
 
 
+@pytest.mark.parametrize("off", [0, 3])
+def test_step_n_pingpong_equals_in_place(off):
+    """Above the ping-pong threshold (lowered here from 2^24 + 1 to every env) r48_env_step_n
+    alternates reads and writes between the bound boards and the env's scratch copy. Odd and
+    even chunk lengths, two shard chains, merge reward + done + actions outputs: identical to
+    eager in-place steps, and the bound array holds the result after every call."""
+    n, seed = 300_001, 91
+    rng = np.random.default_rng(12)
+    b0 = rand_boards(rng, n, emax=6)
+    a, b = vec(n, seed=seed, offset=off), vec(n, seed=seed, offset=off)
+    a.set_pingpong_min(1)
+    put(a, b0)
+    put(b, b0)
+    for chunk in (1, 2, 7, 8, 7):
+        _, ra, da = a.step_n(chunk, auto_reset=True, merge_reward=True)
+        for _ in range(chunk):
+            _, rb, db = b.step(None, auto_reset=True, merge_reward=True)
+        assert torch.equal(a.boards, b.boards), chunk
+        assert torch.equal(da, db) and torch.equal(ra, rb) and torch.equal(a.actions, b.actions)
+    a.set_pingpong_min(0)                                 # back to in place: same stream of results
+    a.step_n(5, auto_reset=True)
+    for _ in range(5):
+        b.step(None, auto_reset=True)
+    assert torch.equal(a.boards, b.boards) and a.counters == b.counters
+
+
 @pytest.mark.parametrize("off", [3, 0])               # odd: guarded per-board path; even: pair fast path
 @pytest.mark.parametrize("n", [300_001, 9_000_003])
 def test_step_n_chains_and_wide_tiles_match_oracle(n, off):

@@ -1,6 +1,6 @@
 """GPU experiment: VecGame.step_n per-step time for librein48 builds (one child process each).
 
-    python tools/exp_step_variants.py [lib.so ...]      (default: the product library)
+    python tools/exp_step_variants.py [--pingpong-min N] [lib.so ...]   (default: the product library)
 
 Variant libraries come from tools/build_variant.sh, e.g. the zero-compute floor with the same
 launch structure and I/O as the env step:
@@ -22,6 +22,8 @@ from rein48_amd import VecGame
 out = {}
 for n, chunk, reps in ((1 << 20, 1000, 8), (1 << 22, 1000, 2), (1 << 26, 200, 1)):
     env = VecGame(n, device="cuda:0", seed=1)
+    if %(pp)d >= 0:
+        env.set_pingpong_min(%(pp)d)
     env.fill_random(7)
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < 0.15:          # clock ramp + graph capture
@@ -43,17 +45,21 @@ print(json.dumps(out))
 
 
 def main():
-    libs = sys.argv[1:] or [os.path.join(ROOT, "rein48_amd", "lib", "librein48.so")]
+    args = sys.argv[1:]
+    pp = -1
+    if args[:1] == ["--pingpong-min"]:
+        pp, args = int(args[1]), args[2:]
+    libs = args or [os.path.join(ROOT, "rein48_amd", "lib", "librein48.so")]
     for lib in libs:
-        p = subprocess.run([sys.executable, "-c", CHILD % {"root": ROOT, "lib": os.path.abspath(lib)}],
+        p = subprocess.run([sys.executable, "-c", CHILD % {"root": ROOT, "lib": os.path.abspath(lib), "pp": pp}],
                            capture_output=True, text=True, timeout=300)
         if p.returncode != 0:
             print(lib, "FAILED", p.stderr[-800:], flush=True)
             sys.exit(1)
         r = json.loads(p.stdout.strip().splitlines()[-1])
         for n, v in r.items():
-            print("%-40s n=%9s  %8.3f us/step  %6.1f G steps/s  %6.0f GB/s" %
-                  (os.path.basename(lib), n, v["us_per_step"], v["G_env_steps_per_s"], v["GBs_34B"]), flush=True)
+            print("%-30s pp=%-9d n=%9s  %8.3f us/step  %6.1f G steps/s  %6.0f GB/s" %
+                  (os.path.basename(lib), pp, n, v["us_per_step"], v["G_env_steps_per_s"], v["GBs_34B"]), flush=True)
 
 
 if __name__ == "__main__":
