@@ -20,10 +20,10 @@
 // (element j of half h = channel 16s + 8(j>>2) + 4h + (j&3) of k-chunk s); the host packs the
 // weight (A) fragments in that order.
 // Per column group (2 boards) a 64->64 layer is 9 taps x 4 k-chunks x 2 row tiles = 72 MFMAs;
-// each wave carries G = 4 column groups (8 boards) so one LDS weight fragment feeds 4 MFMAs.
+// each wave carries G column groups (2G boards) so one LDS weight fragment feeds 2G MFMAs.
 // Weights: each layer's 72 fragments + its bias (1 KiB each) stream into one of two LDS
 // buffers by global_load_lds while the other buffer's layer computes; the workgroup is
-// persistent (one per CU) and cycles stem, conv1..conv8 per 32-board tile.
+// persistent (one per CU, 8 waves) and cycles stem, conv1..conv8 per 32-board tile.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -42,9 +42,21 @@ using bf16x8 = __attribute__((ext_vector_type(8))) short;
 using f32x16 = __attribute__((ext_vector_type(16))) float;
 typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 
-constexpr int kWaves = 4;
+// 8 waves x 2 column groups (two waves per SIMD, so one wave's exposed LDS-read latency runs
+// under the other's MFMAs) measured 14.7-14.9 ms per 2^21 boards against 15.5 for 4 waves x 4
+// groups and 16.7 for 8 x 1 (bit-identical outputs; tools/exp_resnet_fused.py)
+#ifndef R48_RESNET_WAVES
+#define R48_RESNET_WAVES 8
+#endif
+#ifndef R48_RESNET_G
+#define R48_RESNET_G 2
+#endif
+#ifndef R48_RN_ABL   // timing ablations only (wrong results): 1 no per-layer wait/barrier, 2 also no weight
+#define R48_RN_ABL 0 // DMA, 3 epilogue = bf16 pack only, 4 no DPP row shifts in the taps
+#endif
+constexpr int kWaves = R48_RESNET_WAVES;
 constexpr int kThreads = 64 * kWaves;
-constexpr int G = 4;                              // column groups (2 boards each) per wave
+constexpr int G = R48_RESNET_G;                   // column groups (2 boards each) per wave
 constexpr int kBoardsPerTile = kWaves * G * 2;    // 32
 constexpr int kConvLayers = 8;
 constexpr int kStemFrags = 9 * 2 * 2;             // taps x k-chunks (18 planes padded to 32) x row tiles
@@ -100,7 +112,7 @@ __device__ __forceinline__ void tap_mfma(const uint4 *wl, int s, const uint32_t 
         uint32_t r[4];
 #pragma unroll
         for (int q = 0; q < 4; q++)
-            r[q] = cell_shift<4 * DR>(xs[g][DC + 1][q]);
+            r[q] = R48_RN_ABL == 4 ? xs[g][DC + 1][q] : cell_shift<4 * DR>(xs[g][DC + 1][q]);
         bf16x8 B;
         __builtin_memcpy(&B, r, 16);
         acc[g][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A0, B, acc[g][0], 0, 0, 0);
@@ -119,7 +131,7 @@ __device__ __forceinline__ void tap_mfma1(const uint4 *wl, int s, const uint32_t
     uint32_t r[4];
 #pragma unroll
     for (int q = 0; q < 4; q++)
-        r[q] = cell_shift<4 * DR>(xs[DC + 1][q]);
+        r[q] = R48_RN_ABL == 4 ? xs[DC + 1][q] : cell_shift<4 * DR>(xs[DC + 1][q]);
     bf16x8 B;
     __builtin_memcpy(&B, r, 16);
     a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A0, B, a0, 0, 0, 0);
@@ -146,6 +158,10 @@ __device__ __forceinline__ void epilogue1(const f32x16 (&acc)[2], const float *b
         for (int q = 0; q < 4; q++) {
             const int i = 8 * (s & 1) + 2 * q;
             // bias of accumulator rows i, i+1: channels 32m + 8(i>>2) + 4h + (i&3), +1
+            if (R48_RN_ABL == 3) {
+                act[4 * s + q] = pack_bf16x2(acc[s >> 1][i], acc[s >> 1][i + 1]);
+                continue;
+            }
             const f32x2 bb = *reinterpret_cast<const f32x2 *>(bias + 32 * (s >> 1) + 8 * (i >> 2) + 4 * h + (i & 3));
             f32x2 v = f32x2{acc[s >> 1][i], acc[s >> 1][i + 1]} + bb;
             if (RESID)
@@ -293,10 +309,13 @@ __global__ __launch_bounds__(kThreads, 1) void k_resnet_q(const int8_t *__restri
         // ---- 8 convs = 4 basic blocks
         for (int L = 0; L < kConvLayers; ++L) {
             cur ^= 1;
-            __builtin_amdgcn_s_waitcnt(0);
-            __syncthreads();
+            if (R48_RN_ABL != 1 && R48_RN_ABL != 2) {
+                __builtin_amdgcn_s_waitcnt(0);
+                __syncthreads();
+            }
             // prefetch the next layer, or the next tile's stem
-            if (L + 1 < kConvLayers)
+            if (R48_RN_ABL == 2) {
+            } else if (L + 1 < kConvLayers)
                 stage_block(blob + (kStemBlock + (L + 1) * kConvBlock) * 64, buf(cur ^ 1), kConvBlock, wave, lane);
             else if (tile + gridDim.x < tiles)
                 stage_block(blob, buf(cur ^ 1), kStemBlock, wave, lane);

@@ -18,6 +18,9 @@ ISSUED = 2 * 16 * 9 * (32 * C + 8 * C * C)          # per board: 16 cells x 9 ta
 
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 21
+    if len(sys.argv) > 2:                                 # a variant library (tools/build_variant.sh)
+        from rein48_amd import _lib
+        _lib.LIB_PATH, _lib._lib = sys.argv[2], None
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     net = ResNet10Q().to(dev).eval()
@@ -37,6 +40,9 @@ def main():
         ms = ev[0].elapsed_time(ev[1]) / reps
         out[name] = {"ms": ms, "boards_per_s": n / ms * 1e3, "useful_TFLOPs": n * USEFUL / ms / 1e9,
                      "issued_mfma_TFLOPs": n * ISSUED / ms / 1e9, "frac_issued_of_2.5PF": n * ISSUED / ms / 1e9 / 2500}
+    q, _ = resnet_q_forward(boards, packed)
+    out["q_checksum"] = float(q.double().sum())              # tiling variants must agree bit for bit
+    out["q_bits_hash"] = int(q.view(torch.int32).long().mul(2654435761).sum()) & 0xFFFFFFFF
     print(json.dumps(out), flush=True)
 
 
