@@ -277,6 +277,15 @@ int r48_resnet_q_forward(const int8_t *boards, int64_t n, const void *wblob, con
                          int64_t gid0, uint32_t ctr, void *stream);
 int64_t r48_resnet_q_blob_bytes(void);
 
+/* Structured 3x3 (pad 1) conv weight on the 4x4 grid for the ResNet's GEMM form
+ * (rein48_amd/dqn/nets.py dense_conv_weight): w float[co][ci][3][3] -> dense[16 co][16 ci] (f32 or
+ * bf16, 16-byte aligned), block (P, Q) = w[:, :, dr + 1, dc + 1] where input cell Q = P + 4 dr + dc
+ * is an in-grid neighbour of output cell P, else zero. Needs 16 ci % 8 == 0. The gradient maps
+ * gdense[16 co][16 ci] (f32 or bf16) back to gw float[co][ci][3][3] (fixed summation order). */
+int r48_struct_conv_weight(const float *w, int32_t co, int32_t ci, int32_t out_dtype, void *dense, void *stream);
+int r48_struct_conv_weight_grad(const void *gdense, int32_t co, int32_t ci, int32_t in_dtype, float *gw,
+                                void *stream);
+
 /* Training-mode BatchNorm fused with ReLU and the basic block's identity add, for the ResNet-10
  * update (rein48_amd/dqn/nets.py, bn.py; replaces torch.nn.BatchNorm1d + F.relu + add on
  * channels-last bf16 activations). x, residual, y, dy, dx, dresidual: bf16 [rows][C], 16-byte

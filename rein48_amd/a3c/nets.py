@@ -53,7 +53,8 @@ class _SplitKLinear(torch.autograd.Function):
                 gw += (gy[main:].t() @ x[main:]).to(acc)
         else:
             gw = (gy.t() @ x).to(acc)
-        gb = gy.sum(0, dtype=acc) if ctx.has_bias else None     # fp32 accumulation, no cast copy
+        # fp32 accumulation, no cast copy; skipped when the bias is a constant (needs no grad)
+        gb = gy.sum(0, dtype=acc) if ctx.has_bias and ctx.needs_input_grad[2] else None
         return gx, gw.to(w.dtype), (gb.to(w.dtype) if gb is not None else None)
 
 

@@ -107,6 +107,60 @@ __global__ __launch_bounds__(kBlock) void k_td_target(const float *__restrict__ 
     y[i] = reward[i] + gamma * boot;
 }
 
+// ---- structured 3x3 conv weight on the 4x4 grid (rein48_amd/dqn/nets.py dense_conv_weight)
+// dense[P co + o][Q ci + i] = w[o][i][dr + 1][dc + 1] when input cell Q = P + 4 dr + dc is one of
+// output cell P's in-grid 3x3 neighbours, else 0 (100 of the 256 (P, Q) blocks are nonzero). One
+// thread writes 8 consecutive columns of one row; bf16 or f32 out (the zeros, the scatter and
+// the cast of the PyTorch path in one pass).
+__device__ __forceinline__ int tap_of(int P, int Q)
+{
+    const int dr = (Q >> 2) - (P >> 2), dc = (Q & 3) - (P & 3);
+    return (dr < -1 || dr > 1 || dc < -1 || dc > 1) ? -1 : (dr + 1) * 3 + (dc + 1);
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_struct_weight(const float *__restrict__ w, int co, int ci,
+                                                          T *__restrict__ dense)
+{
+    const int cols = 16 * ci, groups = cols / 8;
+    const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (t >= (int64_t)16 * co * groups)
+        return;
+    const int row = (int)(t / groups), c0 = (int)(t % groups) * 8;
+    const int P = row / co, o = row % co;
+    T out[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        const int col = c0 + k, Q = col / ci, i = col % ci;
+        const int tap = tap_of(P, Q);
+        out[k] = (T)(tap < 0 ? 0.0f : w[((int64_t)o * ci + i) * 9 + tap]);
+    }
+    __builtin_memcpy(dense + (int64_t)row * cols + c0, out, sizeof(out));
+}
+
+// gradient: gw[o][i][tap] = sum over the (P, Q) blocks of that tap of gd[P co + o][Q ci + i]
+// (fixed block order: deterministic); gd bf16 or f32, gw f32. One thread per (o, i, tap), i fastest.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_struct_weight_grad(const T *__restrict__ gd, int co, int ci,
+                                                               float *__restrict__ gw)
+{
+    const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (t >= (int64_t)9 * co * ci)
+        return;
+    const int i = (int)(t % ci), o = (int)((t / ci) % co), tap = (int)(t / ((int64_t)ci * co));
+    const int dr = tap / 3 - 1, dc = tap % 3 - 1;
+    const int64_t cols = 16 * (int64_t)ci;
+    float s = 0.0f;
+    for (int P = 0; P < 16; P++) {
+        const int r = (P >> 2) + dr, c = (P & 3) + dc;
+        if (r < 0 || r > 3 || c < 0 || c > 3)
+            continue;
+        const int Q = 4 * r + c;
+        s += (float)gd[((int64_t)P * co + o) * cols + (int64_t)Q * ci + i];
+    }
+    gw[((int64_t)o * ci + i) * 9 + tap] = s;
+}
+
 bool aligned16(const void *p) { return ((uintptr_t)p & 15u) == 0; }
 
 }  // namespace
@@ -156,6 +210,36 @@ int r48_td_target(const float *reward, const uint8_t *done, const float *q_next_
         hipLaunchKernelGGL(k_td_target<false>, grid_for(n), dim3(kBlock), 0, (hipStream_t)stream, reward, done,
                            q_next_target, nullptr, n, gamma, y);
     return launched("k_td_target");
+}
+
+int r48_struct_conv_weight(const float *w, int32_t co, int32_t ci, int32_t out_dtype, void *dense, void *stream)
+{
+    if (!w || !dense || co < 1 || ci < 1 || (16 * ci) % 8 || (out_dtype != R48_F32 && out_dtype != R48_BF16) ||
+        !aligned16(dense))
+        return fail(R48_EINVAL, "r48_struct_conv_weight: NULL/misaligned argument, bad dtype or 16 ci % 8 != 0");
+    const int64_t threads = (int64_t)16 * co * (16 * ci / 8);
+    if (out_dtype == R48_F32)
+        hipLaunchKernelGGL(k_struct_weight<float>, grid_for(threads), dim3(kBlock), 0, (hipStream_t)stream, w, co, ci,
+                           (float *)dense);
+    else
+        hipLaunchKernelGGL(k_struct_weight<__bf16>, grid_for(threads), dim3(kBlock), 0, (hipStream_t)stream, w, co,
+                           ci, (__bf16 *)dense);
+    return launched("k_struct_weight");
+}
+
+int r48_struct_conv_weight_grad(const void *gdense, int32_t co, int32_t ci, int32_t in_dtype, float *gw,
+                                void *stream)
+{
+    if (!gdense || !gw || co < 1 || ci < 1 || (in_dtype != R48_F32 && in_dtype != R48_BF16))
+        return fail(R48_EINVAL, "r48_struct_conv_weight_grad: NULL argument or bad dtype");
+    const int64_t threads = (int64_t)9 * co * ci;
+    if (in_dtype == R48_F32)
+        hipLaunchKernelGGL(k_struct_weight_grad<float>, grid_for(threads), dim3(kBlock), 0, (hipStream_t)stream,
+                           (const float *)gdense, co, ci, gw);
+    else
+        hipLaunchKernelGGL(k_struct_weight_grad<__bf16>, grid_for(threads), dim3(kBlock), 0, (hipStream_t)stream,
+                           (const __bf16 *)gdense, co, ci, gw);
+    return launched("k_struct_weight_grad");
 }
 
 }  // extern "C"

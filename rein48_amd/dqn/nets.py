@@ -48,31 +48,54 @@ def _tap_blocks(device):
 
 class _StructuredConvWeight(torch.autograd.Function):
     """w [co, ci, 3, 3] -> the [16 co, 16 ci] matrix of the conv on the 4x4 grid (block
-    (p, q) = w[:, :, dr + 1, dc + 1] for every in-grid pair). Backward sums each tap's 100
-    blocks with one index_add over 100 rows (no per-element scatter, no sort)."""
+    (p, q) = w[:, :, dr + 1, dc + 1] for every in-grid pair), in `dtype`. On the GPU one HIP pass
+    each way (r48_struct_conv_weight / _grad: zeros, scatter and cast fused; the gradient sums
+    each tap's blocks in a fixed order); on the CPU the same map as an index_put and a backward
+    index_add over the 100 in-grid blocks."""
 
     @staticmethod
-    def forward(ctx, w):
+    def forward(ctx, w, dtype):
         co, ci = w.shape[:2]
+        ctx.shape = (co, ci)
+        if w.is_cuda and dtype in (torch.float32, torch.bfloat16):
+            from .. import _lib
+            from .._lib import check, ptr
+            wf = w.detach().float().contiguous()
+            d = torch.empty(16 * co, 16 * ci, dtype=dtype, device=w.device)
+            check(_lib.load().r48_struct_conv_weight(ptr(wf), co, ci, _lib.BF16 if dtype == torch.bfloat16 else _lib.F32,
+                                                     ptr(d), torch.cuda.current_stream(w.device).cuda_stream))
+            ctx.w_dtype = w.dtype
+            return d
         P, Q, T = _tap_blocks(w.device)
         taps = w.permute(2, 3, 0, 1).reshape(9, co, ci)
         d = torch.zeros(16, co, 16, ci, dtype=w.dtype, device=w.device)
         d[P, :, Q, :] = taps[T]
-        ctx.shape = (co, ci)
-        return d.view(16 * co, 16 * ci)
+        ctx.w_dtype = w.dtype
+        return d.view(16 * co, 16 * ci).to(dtype)
 
     @staticmethod
     def backward(ctx, gd):
         co, ci = ctx.shape
+        if gd.is_cuda and gd.dtype in (torch.float32, torch.bfloat16):
+            from .. import _lib
+            from .._lib import check, ptr
+            gd = gd.contiguous()
+            gw = torch.empty(co, ci, 3, 3, dtype=torch.float32, device=gd.device)
+            check(_lib.load().r48_struct_conv_weight_grad(ptr(gd), co, ci,
+                                                          _lib.BF16 if gd.dtype == torch.bfloat16 else _lib.F32,
+                                                          ptr(gw), torch.cuda.current_stream(gd.device).cuda_stream))
+            return gw.to(ctx.w_dtype), None
         P, Q, T = _tap_blocks(gd.device)
+        gd = gd.to(ctx.w_dtype)
         blocks = gd.reshape(16, co, 16, ci)[P, :, Q, :]                       # [100, co, ci]
         g9 = torch.zeros(9, co, ci, dtype=gd.dtype, device=gd.device).index_add_(0, T, blocks)
-        return g9.view(3, 3, co, ci).permute(2, 3, 0, 1).contiguous()
+        return g9.view(3, 3, co, ci).permute(2, 3, 0, 1).contiguous(), None
 
 
-def dense_conv_weight(conv):
-    """[16 co, 16 ci] structured matrix of a Conv2d(ci, co, 3, padding=1) on the 4x4 grid."""
-    return _StructuredConvWeight.apply(conv.weight)
+def dense_conv_weight(conv, dtype=None):
+    """[16 co, 16 ci] structured matrix of a Conv2d(ci, co, 3, padding=1) on the 4x4 grid, in
+    `dtype` (default: the weight's)."""
+    return _StructuredConvWeight.apply(conv.weight, conv.weight.dtype if dtype is None else dtype)
 
 
 class ResNet10Q(nn.Module):
@@ -108,7 +131,14 @@ class ResNet10Q(nn.Module):
         return bn(x).view(B, 16 * self.channels)
 
     def _conv(self, conv, h):
-        return linear(h, dense_conv_weight(conv), conv.bias.repeat(16), self.dtype)
+        b = conv.bias.repeat(16)
+        if self.use_bn:
+            # every conv feeds a training-mode BN, which subtracts the batch mean: the conv bias has
+            # no effect on the output and an exactly zero gradient, so it is a constant here (no
+            # 65536 x 1024 bias-gradient reduction per layer); it still shifts the running mean
+            # like before, which the eval-mode fold (folded()) accounts for
+            b = b.detach()
+        return linear(h, dense_conv_weight(conv, self.dtype), b, self.dtype)
 
     def _fused_bn(self, h):
         return (self.use_bn and self.fused_bn and self.training and h.is_cuda and h.dtype == torch.bfloat16

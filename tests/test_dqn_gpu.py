@@ -274,3 +274,31 @@ def test_resnet_update_fused_bn_matches_torch_bn():
         assert float((ga - gb).norm()) <= 5e-2 * float(gb.norm()) + 1e-6
     for sa, sb in zip(*stats):
         torch.testing.assert_close(sa, sb, rtol=1e-2, atol=1e-3)
+
+
+@pytest.mark.parametrize("ci", [18, 64])
+def test_structured_conv_weight_kernels_match_cpu_map(ci):
+    """r48_struct_conv_weight / _grad (one HIP pass each way) == the CPU index_put / index_add
+    map of nets._StructuredConvWeight: forward exact in fp32 and equal to the rounded fp32 matrix
+    in bf16; gradient within fp32 summation-order error, for the stem (ci = 18) and a block conv."""
+    from rein48_amd.dqn.nets import _StructuredConvWeight
+    torch.manual_seed(ci)
+    co = 64
+    w = torch.randn(co, ci, 3, 3, dtype=torch.float32)
+    want = _StructuredConvWeight.apply(w, torch.float32)
+    got32 = _StructuredConvWeight.apply(w.to(DEV), torch.float32)
+    got16 = _StructuredConvWeight.apply(w.to(DEV), torch.bfloat16)
+    assert torch.equal(got32.cpu(), want)
+    assert torch.equal(got16.cpu(), want.to(torch.bfloat16))
+    gd = torch.randn(16 * co, 16 * ci, dtype=torch.float32)
+    wc = w.clone().requires_grad_(True)
+    _StructuredConvWeight.apply(wc, torch.float32).backward(gd)
+    for dt in (torch.float32, torch.bfloat16):
+        wg = w.to(DEV).requires_grad_(True)
+        _StructuredConvWeight.apply(wg, dt).backward(gd.to(DEV, dt))
+        ref = wc.grad if dt == torch.float32 else None
+        if ref is None:                                   # bf16 gradient input: the CPU map of the rounded gd
+            wr = w.clone().requires_grad_(True)
+            _StructuredConvWeight.apply(wr, torch.float32).backward(gd.to(torch.bfloat16).float())
+            ref = wr.grad
+        torch.testing.assert_close(wg.grad.cpu(), ref, rtol=1e-5, atol=1e-5)
