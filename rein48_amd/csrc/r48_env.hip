@@ -25,7 +25,10 @@ constexpr int kBlock = 256;
 // r48_env_step_n splits an env of >= kChainMin boards into kMaxChains contiguous shards, each
 // replaying its own graph on its own stream: the two dependent-launch chains overlap one
 // shard's load latency / store drain with the other's compute (1M boards: 10.3 -> 7.2 us).
-constexpr int kMaxChains = 2;
+#ifndef R48_MAX_CHAINS
+#define R48_MAX_CHAINS 2
+#endif
+constexpr int kMaxChains = R48_MAX_CHAINS;
 constexpr int64_t kChainMin = (int64_t)1 << 18;
 // 2^24 boards = 256 MiB, the Infinity Cache: above it both patterns stream from HBM and
 // ping-pong wins (2^26: 384 vs 425 us per step, tools/pingpong_bw.hip); at 2^24 the in-place
@@ -929,17 +932,20 @@ int r48_env_step_n(r48_env *env, int32_t n_steps, int8_t *actions, uint32_t flag
     // microseconds, so there is exactly one of each per call)
     if (hipMemsetD32Async((hipDeviceptr_t)env->d_ctr, (int)env->step_ctr, 1, user) != hipSuccess)
         return fail(R48_EHIP, "hipMemsetD32Async(step counter) failed");
-    if (chains > 1 && (hipEventRecord(env->fork, user) != hipSuccess ||
-                       hipStreamWaitEvent(env->chain[1], env->fork, 0) != hipSuccess))
-        return fail(R48_EHIP, "forking the second chain failed");
+    if (chains > 1 && hipEventRecord(env->fork, user) != hipSuccess)
+        return fail(R48_EHIP, "recording the fork event failed");
+    for (int c = 1; c < chains; c++)
+        if (hipStreamWaitEvent(env->chain[c], env->fork, 0) != hipSuccess)
+            return fail(R48_EHIP, "forking a shard chain failed");
     for (int c = 0; c < chains; c++) {
         const hipError_t le = hipGraphLaunch(exec[c], c == 0 ? user : env->chain[c]);
         if (le != hipSuccess)
             return fail(R48_EHIP, std::string("hipGraphLaunch failed: ") + hipGetErrorString(le));
     }
-    if (chains > 1 && (hipEventRecord(env->join[1], env->chain[1]) != hipSuccess ||
-                       hipStreamWaitEvent(user, env->join[1], 0) != hipSuccess))
-        return fail(R48_EHIP, "joining the second chain failed");
+    for (int c = 1; c < chains; c++)
+        if (hipEventRecord(env->join[c], env->chain[c]) != hipSuccess ||
+            hipStreamWaitEvent(user, env->join[c], 0) != hipSuccess)
+            return fail(R48_EHIP, "joining a shard chain failed");
     env->step_ctr += (uint32_t)n_steps;
     return R48_OK;
 }

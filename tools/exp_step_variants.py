@@ -20,6 +20,15 @@ from rein48_amd import _lib
 _lib.LIB_PATH, _lib._lib = %(lib)r, None
 from rein48_amd import VecGame
 out = {}
+# deterministic result check first: every build / chain count / ping-pong setting must agree
+env = VecGame(300_001, device="cuda:0", seed=5)
+if %(pp)d >= 0:
+    env.set_pingpong_min(%(pp)d)
+env.fill_random(7)
+env.step_n(777, auto_reset=True)
+env.step_n(64, auto_reset=True)
+out["check_hash"] = int(env.boards.view(torch.int32).long().mul(2654435761).sum()) & 0xFFFFFFFF
+del env
 for n, chunk, reps in ((1 << 20, 1000, 8), (1 << 22, 1000, 2), (1 << 26, 200, 1)):
     env = VecGame(n, device="cuda:0", seed=1)
     if %(pp)d >= 0:
@@ -57,6 +66,7 @@ def main():
             print(lib, "FAILED", p.stderr[-800:], flush=True)
             sys.exit(1)
         r = json.loads(p.stdout.strip().splitlines()[-1])
+        print("%-30s pp=%-9d check hash %d" % (os.path.basename(lib), pp, r.pop("check_hash")), flush=True)
         for n, v in r.items():
             print("%-30s pp=%-9d n=%9s  %8.3f us/step  %6.1f G steps/s  %6.0f GB/s" %
                   (os.path.basename(lib), pp, n, v["us_per_step"], v["G_env_steps_per_s"], v["GBs_34B"]), flush=True)
