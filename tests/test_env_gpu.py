@@ -498,3 +498,38 @@ def test_play_loop_matches_reference_score(golden):
         m = (z["step_seed"] == seed) & (z["step_episode"] == 0)
         last = z["step_after"][m][-1].astype(np.int64)
         assert score == int(np.where(last > 0, 1 << last, 0).sum())
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 511, 512, 513, 1025])
+def test_tiny_and_ragged_envs_match_oracle(n):
+    """Edge sizes (one board, a partial pair, a partial tile, one tile +- 1): eager steps under the
+    random policy, given actions read through views at odd offsets (the pair path's 2-byte stores
+    fall back to the per-board path for misaligned planes), and a step_n chunk, all == the oracle.
+    Boards hold exponents up to 29, so merges reach 2^30 (the largest exponent the int8 cell and
+    the int32 merge reward both hold)."""
+    rng = np.random.default_rng(n)
+    seed = 31337
+    b0 = rand_boards(rng, n, emax=29, p_empty=0.3)
+    v = vec(n, seed=seed)
+    put(v, b0)
+    ob = b0
+    flags = O.RANDOM_POLICY | O.MERGE_REWARD
+    v.step(None, merge_reward=True)
+    r = O.step_philox(ob, seed, 0, flags)
+    ob = r["boards"]
+    assert np.array_equal(host(v.boards), ob) and np.array_equal(host(v.reward), r["reward"])
+    # given actions and done/reward outputs through odd-offset views of larger buffers
+    acts = rng.integers(0, 4, n).astype(np.int8)
+    abuf = torch.zeros(n + 1, dtype=torch.int8, device=DEV)
+    abuf[1:] = torch.from_numpy(acts).to(DEV)
+    dbuf = torch.zeros(n + 1, dtype=torch.uint8, device=DEV)
+    _, rew, done = v.step(abuf[1:], merge_reward=True, done_out=dbuf[1:])
+    r = O.step_philox(ob, seed, 1, O.MERGE_REWARD, actions=acts)
+    ob = r["boards"]
+    assert np.array_equal(host(v.boards), ob)
+    assert np.array_equal(host(done), r["done"]) and np.array_equal(host(rew), r["reward"])
+    v.step_n(3, auto_reset=True)
+    for k in range(3):
+        ob = O.step_philox(ob, seed, 2 + k, O.RANDOM_POLICY | O.AUTO_RESET)["boards"]
+    assert np.array_equal(host(v.boards), ob)
+    assert v.counters == (5, 0)
