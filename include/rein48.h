@@ -195,6 +195,23 @@ int r48_cnn_policy_forward(const int8_t *boards, int64_t n, const void *wfrag, c
                            int32_t mode, float *logits, float *value, int8_t *actions, int8_t *boards_out,
                            uint64_t seed, int64_t gid0, uint32_t ctr, void *stream);
 
+/* The whole fused A3C rollout (configs 3-4; rein48_amd/a3c/trainer.py A3CTrainer.rollout, the
+ * batched a3c.py:194-212 loop) in ONE launch: for each of n_steps steps, every board goes through
+ * the policy of r48_cnn_policy_forward (same weights/bias packing and mode, action draw with
+ * policy_seed, counter sample_ctr + t, board id gid0 + i) and then the env step of r48_env_step
+ * with those actions (Philox key env_seed, step counter env_step + t, board id gid0 + i; no
+ * auto-reset; R48_MERGE_REWARD in flags for the merge reward). boards int8[n][16] (16-byte
+ * aligned) are read at the start and hold the final boards at the end; traj_boards
+ * int8[n_steps + 1][n][16] receives the pre-step board of every step and the final board;
+ * actions int8[n_steps][n], done uint8[n_steps][n], reward int32[n_steps][n] (nullable), lengths
+ * int32[n] (nullable): 1 + the first step that ended done, else n_steps (a3c.py:201). Results
+ * equal n_steps x (r48_cnn_policy_forward + r48_env_step) bit for bit; the caller advances the
+ * env's step counter by n_steps (r48_env_set_counters). */
+int r48_cnn_rollout(int8_t *boards, int64_t n, int32_t n_steps, const void *wfrag, const float *bias, int32_t mode,
+                    int8_t *traj_boards, int8_t *actions, uint8_t *done, int32_t *reward, int32_t *lengths,
+                    uint64_t policy_seed, int64_t gid0, uint32_t sample_ctr, uint64_t env_seed, uint32_t env_step,
+                    uint32_t flags, void *stream);
+
 /* Fused A3C update for the CNN (configs 3-4; rein48_amd/a3c/losses.py restating a3c.py:99-123):
  * the gradient of (actor + critic) over `rows` training states w.r.t. every ActorCriticCNN
  * parameter, in one pass with no activation written to memory. boards int8[rows][16], actions

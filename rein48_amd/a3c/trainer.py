@@ -51,6 +51,7 @@ class A3CConfig:
     bf16: bool = False            # run the net's GEMMs in bf16 (MFMA, fp32 accumulate)
     fused_policy: bool = True     # cnn + bf16: rollout inference in one fused MFMA kernel (r48_policy.hip)
     fused_update: bool = True     # cnn + bf16: the whole update's gradient in one fused pass (r48_a3c_train.hip)
+    fused_rollout: bool = True    # cnn + bf16: all max_steps policy + env steps in one launch (r48_cnn_rollout)
 
 
 class A3CTrainer:
@@ -95,7 +96,9 @@ class A3CTrainer:
             wfrag, bias = pack_cnn(self.net)   # weights are fixed for the whole rollout
         if merge and getattr(self, "_rewards_i32", None) is None:
             self._rewards_i32 = torch.zeros((cfg.max_steps, cfg.n_boards), dtype=torch.int32, device=self.device)
-        if fused:   # board -> CNN -> softmax -> Philox draw in one kernel, then the env kernel
+        if fused and cfg.fused_rollout:   # every step of every board in one persistent kernel
+            self._rollout_megakernel(wfrag, bias, merge)
+        elif fused:   # per step: board -> CNN -> softmax -> Philox draw in one kernel, then the env kernel
             self._rollout_fused(wfrag, bias, merge)
         else:
             for t in range(cfg.max_steps):
@@ -109,11 +112,16 @@ class A3CTrainer:
                          reward_out=self._rewards_i32[t] if merge else None)
         if merge:
             self.rewards.copy_(self._rewards_i32)     # one int32 -> fp32 pass for the whole rollout
-        self.boards[cfg.max_steps].copy_(env.boards)
         # segment length: through the first done step, else max_steps (a3c.py:201)
-        notdone = (self.done.cumsum(0) == 0)
-        self.lengths = (notdone.sum(0) + 1).clamp(max=cfg.max_steps).to(torch.int32)
-        self.finished = self.done.bool().any(0)
+        if fused and cfg.fused_rollout:                # the megakernel wrote boards[T] and the lengths
+            self.lengths = self._lengths
+            last = (self.lengths.long() - 1).view(1, -1)
+            self.finished = self.done.gather(0, last)[0].bool()
+        else:
+            self.boards[cfg.max_steps].copy_(env.boards)
+            notdone = (self.done.cumsum(0) == 0)
+            self.lengths = (notdone.sum(0) + 1).clamp(max=cfg.max_steps).to(torch.int32)
+            self.finished = self.done.bool().any(0)
         t = torch.arange(cfg.max_steps, device=self.device).unsqueeze(1)
         self.mask = t < self.lengths.unsqueeze(0)
         return self.lengths
@@ -142,6 +150,25 @@ class A3CTrainer:
             self.sample_ctr += 1
             _lib.check(lib.r48_env_step(env._env, at, flags, d0 + t * n, None,
                                         None if r0 is None else r0 + 4 * t * n, None, stream))
+
+    def _rollout_megakernel(self, wfrag, bias, merge):
+        """r48_cnn_rollout: the T policy + env steps of every board in one launch (boards stay in
+        registers; only the trajectory rows are written), bit-identical to _rollout_fused. The
+        env's step counter then advances by T like T r48_env_step calls."""
+        cfg, env = self.cfg, self.env
+        T, n = cfg.max_steps, cfg.n_boards
+        step0, resets = env.counters
+        self._lengths = torch.empty(n, dtype=torch.int32, device=self.device)
+        _lib.check(_lib.load().r48_cnn_rollout(
+            env.boards.data_ptr(), n, T, wfrag.data_ptr(), bias.data_ptr(),
+            _lib.FEAT_EXPONENTS if cfg.features == "exponents" else _lib.FEAT_VALUES,
+            self.boards.data_ptr(), self.actions.data_ptr(), self.done.data_ptr(),
+            self._rewards_i32.data_ptr() if merge else None, self._lengths.data_ptr(),
+            int(cfg.seed) & (2 ** 64 - 1), self.gid0,
+            self.sample_ctr & 0xFFFFFFFF, int(env.seed) & (2 ** 64 - 1), step0,
+            _lib.MERGE_REWARD if merge else 0, torch.cuda.current_stream(self.device).cuda_stream))
+        self.sample_ctr += T
+        env.counters = (step0 + T, resets)
 
     # ------------------------------------------------------------------ update (a3c.py:218-234)
     def _states(self):

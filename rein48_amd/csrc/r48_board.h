@@ -318,6 +318,18 @@ static constexpr uint32_t kFourThresh = 0x1999999Au;     // P(4) = 0.1   (GameCl
 static constexpr uint32_t kFourThresh30 = 0x06666666u;   // same on 30 bits (P = 0.1 - 4e-10)
 static constexpr uint32_t kFourThresh28 = 0x0199999Au;   // same on 28 bits
 
+// The env step's draw words of board `gid` at step `step` (the k_step contract of r48_env.hip,
+// DESIGN.md section 7): boards 2q, 2q + 1 share Philox4x32-10(key, {q lo, q hi, step, kStepTag});
+// the even board takes (x, y) = (w0, w1), the odd one (w2, w3).
+R48_HD void step_draw(uint64_t gid, uint32_t step, uint32_t k0, uint32_t k1, uint32_t &x, uint32_t &y)
+{
+    const uint64_t q = gid >> 1;
+    uint32_t w[4] = {(uint32_t)q, (uint32_t)(q >> 32), step, kStepTag};
+    philox4x32_10(w, k0, k1);
+    x = (gid & 1u) ? w[2] : w[0];
+    y = (gid & 1u) ? w[3] : w[1];
+}
+
 struct StepOut {
     uint32_t changed, done, n_blank, reward, score;
 };

@@ -116,6 +116,138 @@ __global__ __launch_bounds__(kThreads, 2) void k_cnn_forward(const int8_t *__res
     }
 }
 
+// ---------------------------------------------------------------- rollout megakernel
+// The whole A3C rollout (a3c.py:194-212 batched, trainer.A3CTrainer.rollout) in one launch: every
+// board is independent, so a wave keeps its boards in registers for all T steps and writes only
+// the trajectory rows (pre-step board, action, done, merge reward) -- no per-step launches and no
+// board round trip through HBM. A wave owns a PAIR of 32-board tiles (A, B). Lane (col, h) holds
+// bytes 8h..8h+7 (rows 2h, 2h+1) of board col of both tiles. Per step: the policy of
+// k_cnn_forward on A, then on B (boards on the MFMA columns, action draw in lane half 0), then ONE
+// env step pass (Game.step, GameClient.py:40-51, r48_board.h, the k_step draw contract) in which
+// lane half 0 steps tile A's board and lane half 1 tile B's: one cross-half shuffle assembles the
+// whole board, one more returns the halves -- every lane does useful env work. Per board the first
+// step that ends done gives the segment length (a3c.py:201). Results are bit-identical to
+// T x (r48_cnn_policy_forward + r48_env_step) (tests/test_a3c_gpu.py).
+template <int MODE>
+__device__ __forceinline__ uint32_t policy_action(const uint4 *w_lds, const float *b_lds, int lane, int h, uint2 raw,
+                                                  uint64_t gid, uint32_t ctr, uint32_t pk0, uint32_t pk1)
+{
+    uint32_t xp[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const uint32_t w = q < 2 ? raw.x : raw.y;
+        const int sh = 16 * (q & 1);
+        xp[q] = cell_bf16((w >> sh) & 0xffu, MODE) | (cell_bf16((w >> (sh + 8)) & 0xffu, MODE) << 16);
+    }
+    bf16x8 x;
+    __builtin_memcpy(&x, xp, 16);
+    bf16x8 h1[9][2], h2[4][2][2];
+    f32x16 out;
+    WStream ws;
+    ws.start(w_lds, fwd_frag(0), fwd_frag(1), lane);
+    cnn_conv1(w_lds, b_lds, lane, h, x, ws, h1);
+    cnn_conv2_heads(w_lds, b_lds, lane, h, h1, ws, h2, out);
+    uint32_t act = 0;
+    if (h == 0) {   // the logits rows; softmax + Philox inverse CDF exactly as k_cnn_forward
+        const float z0 = out[0] + b_lds[96], z1 = out[1] + b_lds[97], z2 = out[2] + b_lds[98], z3 = out[3] + b_lds[99];
+        const float m = fmaxf(fmaxf(z0, z1), fmaxf(z2, z3));
+        const float e0 = __expf(z0 - m), e1 = __expf(z1 - m), e2 = __expf(z2 - m), e3 = __expf(z3 - m);
+        const float inv = 1.0f / (e0 + e1 + e2 + e3);
+        const float p0 = e0 * inv, c1 = p0 + e1 * inv, c2 = c1 + e2 * inv;
+        uint32_t w[4] = {(uint32_t)gid, (uint32_t)(gid >> 32), ctr, kSampleTag};
+        r48::philox4x32_10(w, pk0, pk1);
+        const float u = (float)(w[0] >> 8) * (1.0f / 16777216.0f);
+        act = (p0 > u) ? 0u : (c1 > u) ? 1u : (c2 > u) ? 2u : 3u;
+    }
+    return act;
+}
+
+template <int MODE, bool REWARD>
+__global__ __launch_bounds__(kThreads, 2) void k_cnn_rollout(int8_t *__restrict__ boards, int64_t n, int32_t T,
+                                                             const uint4 *__restrict__ wfrag,
+                                                             const float *__restrict__ bias,
+                                                             int8_t *__restrict__ traj, int8_t *__restrict__ actions,
+                                                             uint8_t *__restrict__ done, int32_t *__restrict__ reward,
+                                                             int32_t *__restrict__ lengths, int64_t gid0, uint32_t pk0,
+                                                             uint32_t pk1, uint32_t ctr0, uint32_t ek0, uint32_t ek1,
+                                                             uint32_t step0)
+{
+    __shared__ uint4 w_lds[kFrags * 64];
+    __shared__ __attribute__((aligned(16))) float b_lds[32 + 64 + 8];
+    for (int i = threadIdx.x; i < kFrags * 64; i += kThreads)
+        w_lds[i] = wfrag[i];
+    for (int i = threadIdx.x; i < 32 + 64 + 8; i += kThreads)
+        b_lds[i] = bias[i];
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63, h = lane >> 5, col = lane & 31;
+    const int64_t n_pairs = (n + 63) / 64;
+    const int64_t stride = (int64_t)gridDim.x * kWaves;
+    for (int64_t pair = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6); pair < n_pairs; pair += stride) {
+        const int64_t bA = pair * 64 + col, bB = bA + 32;
+        const bool liveA = bA < n, liveB = bB < n;
+        const int64_t cA = liveA ? bA : n - 1, cB = liveB ? bB : n - 1;   // padding lanes: a valid duplicate
+        uint2 rawA = *reinterpret_cast<const uint2 *>(boards + 16 * cA + 8 * h);
+        uint2 rawB = *reinterpret_cast<const uint2 *>(boards + 16 * cB + 8 * h);
+        const uint64_t gA = (uint64_t)(gid0 + cA), gB = (uint64_t)(gid0 + cB);
+        // the board this lane steps in the env pass: tile A in half 0, tile B in half 1
+        const int64_t bE = h == 0 ? bA : bB;
+        const bool liveE = h == 0 ? liveA : liveB;
+        const uint64_t gE = h == 0 ? gA : gB;
+        int32_t len = T;
+        for (int32_t t = 0; t < T; t++) {
+            const int64_t row0 = (int64_t)t * n;
+            if (liveA)
+                *reinterpret_cast<uint2 *>(traj + 16 * (row0 + bA) + 8 * h) = rawA;
+            if (liveB)
+                *reinterpret_cast<uint2 *>(traj + 16 * (row0 + bB) + 8 * h) = rawB;
+            const uint32_t aA = policy_action<MODE>(w_lds, b_lds, lane, h, rawA, gA, ctr0 + (uint32_t)t, pk0, pk1);
+            const uint32_t aB = policy_action<MODE>(w_lds, b_lds, lane, h, rawB, gB, ctr0 + (uint32_t)t, pk0, pk1);
+            // half 0 keeps its A action; half 1 takes B's action from lane col (half 0)
+            const uint32_t aBall = (uint32_t)__shfl((int)aB, col);
+            const uint32_t act = h == 0 ? aA : aBall;
+            // assemble the env board: half 0 gets A's rows 2-3 from its partner, half 1 B's rows 0-1
+            const uint2 send = h == 0 ? rawB : rawA;
+            const uint2 recv = make_uint2((uint32_t)__shfl_xor((int)send.x, 32), (uint32_t)__shfl_xor((int)send.y, 32));
+            r48::Board bd = h == 0 ? r48::Board{rawA.x, rawA.y, recv.x, recv.y} : r48::Board{recv.x, recv.y, rawB.x, rawB.y};
+            uint32_t dx, dy;
+            r48::step_draw(gE, step0 + (uint32_t)t, ek0, ek1, dx, dy);
+            const r48::StepOut o =
+                r48::step_board<REWARD, false, false>(bd, act, dy, (dx & 0x3FFFFFFFu) < r48::kFourThresh30);
+            // return the halves: half 0 keeps A's rows 0-1, half 1 keeps B's rows 2-3, and each sends
+            // the other half of its board to its partner
+            const uint2 back = h == 0 ? make_uint2(bd.w2, bd.w3) : make_uint2(bd.w0, bd.w1);
+            const uint2 got = make_uint2((uint32_t)__shfl_xor((int)back.x, 32), (uint32_t)__shfl_xor((int)back.y, 32));
+            if (h == 0) {
+                rawA = make_uint2(bd.w0, bd.w1);
+                rawB = got;
+            } else {
+                rawA = got;
+                rawB = make_uint2(bd.w2, bd.w3);
+            }
+            if (o.done && len == T)
+                len = t + 1;                                   // through the first done step
+            if (liveE) {
+                actions[row0 + bE] = (int8_t)act;
+                done[row0 + bE] = (uint8_t)o.done;
+                if (reward)
+                    reward[row0 + bE] = REWARD ? (int32_t)o.reward : 0;
+            }
+        }
+        const int64_t rowT = (int64_t)T * n;
+        if (liveA) {
+            *reinterpret_cast<uint2 *>(traj + 16 * (rowT + bA) + 8 * h) = rawA;
+            *reinterpret_cast<uint2 *>(boards + 16 * bA + 8 * h) = rawA;
+        }
+        if (liveB) {
+            *reinterpret_cast<uint2 *>(traj + 16 * (rowT + bB) + 8 * h) = rawB;
+            *reinterpret_cast<uint2 *>(boards + 16 * bB + 8 * h) = rawB;
+        }
+        if (lengths && liveE)
+            lengths[bE] = len;
+    }
+}
+
 int fail(int code, const std::string &msg)
 {
     r48::set_last_error(msg);
@@ -151,6 +283,38 @@ int r48_cnn_policy_forward(const int8_t *boards, int64_t n, const void *wfrag, c
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess)
         return fail(R48_EHIP, std::string("k_cnn_forward: ") + hipGetErrorString(e));
+    return R48_OK;
+}
+
+int r48_cnn_rollout(int8_t *boards, int64_t n, int32_t n_steps, const void *wfrag, const float *bias, int32_t mode,
+                    int8_t *traj_boards, int8_t *actions, uint8_t *done, int32_t *reward, int32_t *lengths,
+                    uint64_t policy_seed, int64_t gid0, uint32_t sample_ctr, uint64_t env_seed, uint32_t env_step,
+                    uint32_t flags, void *stream)
+{
+    if (!boards || !wfrag || !bias || !traj_boards || !actions || !done || n < 0 || gid0 < 0 || n_steps < 1 ||
+        (mode != R48_FEAT_VALUES && mode != R48_FEAT_EXPONENTS) || (flags & ~R48_MERGE_REWARD))
+        return fail(R48_EINVAL, "r48_cnn_rollout: NULL argument, n/gid0 < 0, n_steps < 1, bad mode or flags");
+    if ((reinterpret_cast<uintptr_t>(boards) | reinterpret_cast<uintptr_t>(wfrag) |
+         reinterpret_cast<uintptr_t>(traj_boards)) & 15u)
+        return fail(R48_EINVAL, "boards, traj_boards and wfrag must be 16-byte aligned");
+    if (n == 0)
+        return R48_OK;
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess)
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const int64_t pairs = (n + 63) / 64;
+    const int64_t blocks = std::min<int64_t>((pairs + kWaves - 1) / kWaves, (int64_t)cus * 2);
+    const bool rw = flags & R48_MERGE_REWARD;
+    auto kern = mode == R48_FEAT_VALUES ? (rw ? k_cnn_rollout<R48_FEAT_VALUES, true> : k_cnn_rollout<R48_FEAT_VALUES, false>)
+                                        : (rw ? k_cnn_rollout<R48_FEAT_EXPONENTS, true>
+                                              : k_cnn_rollout<R48_FEAT_EXPONENTS, false>);
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kThreads), 0, (hipStream_t)stream, boards, n, n_steps,
+                       (const uint4 *)wfrag, bias, traj_boards, actions, done, reward, lengths, gid0, (uint32_t)policy_seed,
+                       (uint32_t)(policy_seed >> 32), sample_ctr, (uint32_t)env_seed, (uint32_t)(env_seed >> 32),
+                       env_step);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess)
+        return fail(R48_EHIP, std::string("k_cnn_rollout: ") + hipGetErrorString(e));
     return R48_OK;
 }
 

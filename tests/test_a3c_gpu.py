@@ -280,3 +280,27 @@ def test_fused_rollout_trajectory_replays_through_the_env():
         assert torch.equal(env.boards, tr.boards[t + 1]), t
         assert torch.equal(done, tr.done[t]), t
         assert torch.equal(rew.float(), tr.rewards[t]), t
+
+
+@pytest.mark.parametrize("mode", ["textbook", "reference"])
+def test_rollout_megakernel_equals_per_step_rollout(mode):
+    """r48_cnn_rollout (all steps of every board in one launch, boards in registers) == the
+    per-step rollout (r48_cnn_policy_forward + r48_env_step per step), bit for bit: trajectory
+    boards, actions, done, rewards, final boards and the env / sampling counters; a ragged board
+    count exercises the padding lanes of the last tile."""
+    from rein48_amd.a3c import A3CConfig, A3CTrainer
+    out = []
+    for mega in (True, False):
+        cfg = A3CConfig(n_boards=5003, max_steps=37, mode=mode, net="cnn", bf16=True, features="exponents",
+                        seed=77, fused_rollout=mega)                # 5003 = 78 tile pairs + a partial one
+        tr = A3CTrainer(cfg, device=DEV)
+        tr.rollout()
+        tr.rollout()                                   # second rollout: counters carried over
+        out.append((tr.boards.clone(), tr.actions.clone(), tr.done.clone(), tr.rewards.clone(),
+                    tr.env.boards.clone(), tr.env.counters, tr.sample_ctr, tr.lengths.clone(), tr.finished.clone(),
+                    tr.mask.clone()))
+    for a, b in zip(*out):
+        if isinstance(a, torch.Tensor):
+            assert torch.equal(a, b)
+        else:
+            assert a == b
