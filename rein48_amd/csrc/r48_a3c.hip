@@ -121,11 +121,26 @@ __global__ __launch_bounds__(kBlock) void k_returns(const float *__restrict__ re
     for (int32_t t = T - 1; t >= L; t--)
         out[(int64_t)t * n + i] = 0.0f;
     float g = bootstrap[i];
-    for (int32_t t = L - 1; t >= 0; t--) {
-        if (DROP_LAST && t == L - 1) {
-            out[(int64_t)t * n + i] = g;
-            continue;
+    int32_t t = L - 1;
+    if (DROP_LAST && t >= 0) {
+        out[(int64_t)t * n + i] = g;
+        t--;
+    }
+    // the scan is serial in g, the loads are not: 8 rewards are in flight per chunk, so each
+    // step no longer waits a full memory latency (same arithmetic, same order)
+    constexpr int kAhead = 8;
+    for (; t >= kAhead - 1; t -= kAhead) {
+        float r[kAhead];
+#pragma unroll
+        for (int k = 0; k < kAhead; k++)
+            r[k] = rewards[(int64_t)(t - k) * n + i];
+#pragma unroll
+        for (int k = 0; k < kAhead; k++) {
+            g = r[k] + gamma * g;
+            out[(int64_t)(t - k) * n + i] = g;
         }
+    }
+    for (; t >= 0; t--) {
         g = rewards[(int64_t)t * n + i] + gamma * g;
         out[(int64_t)t * n + i] = g;
     }

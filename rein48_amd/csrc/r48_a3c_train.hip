@@ -604,15 +604,31 @@ __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
 }
 
 // deterministic sum of the per-wave records: out[k] = sum_w partials[w][k]
-__global__ __launch_bounds__(256) void k_reduce(const float *__restrict__ partials, int64_t n_rec,
-                                                float *__restrict__ out)
+// fixed-order sum of the per-wave records in two passes: pass 1 sums the records of group g
+// (records g, g + kGroups, ...) per output (kGroups x 38 blocks instead of 38 reading all 1024
+// records each), pass 2 sums the kGroups group sums in order -- deterministic
+constexpr int kGroups = 32;
+
+__global__ __launch_bounds__(256) void k_reduce_groups(const float *__restrict__ partials, int64_t n_rec,
+                                                       float *__restrict__ group_sums)
+{
+    const int k = blockIdx.x * 256 + threadIdx.x, g = blockIdx.y;
+    if (k >= kPartial)
+        return;
+    float s = 0.f;
+    for (int64_t w = g; w < n_rec; w += kGroups)
+        s += partials[w * kPartial + k];
+    group_sums[(int64_t)g * kPartial + k] = s;
+}
+
+__global__ __launch_bounds__(256) void k_reduce(const float *__restrict__ group_sums, float *__restrict__ out)
 {
     const int k = blockIdx.x * 256 + threadIdx.x;
     if (k >= kPartial)
         return;
     float s = 0.f;
-    for (int64_t w = 0; w < n_rec; w++)
-        s += partials[w * kPartial + k];
+    for (int g = 0; g < kGroups; g++)
+        s += group_sums[(int64_t)g * kPartial + k];
     out[k] = s;
 }
 
@@ -634,7 +650,8 @@ int grid_size()
 
 extern "C" {
 
-int64_t r48_cnn_train_workspace_floats(void) { return (int64_t)grid_size() * kWaves * kPartial; }
+// per-wave records + the reduction's kGroups group sums
+int64_t r48_cnn_train_workspace_floats(void) { return ((int64_t)grid_size() * kWaves + kGroups) * kPartial; }
 
 int64_t r48_cnn_train_grad_floats(void) { return kPartial; }
 
@@ -661,8 +678,11 @@ int r48_cnn_train_grad(const int8_t *boards, int64_t rows, int64_t n_boards, con
     }
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), lds, (hipStream_t)stream, boards, rows, n_boards, actions,
                        targets, wn, cm, counts, beta, (const uint4 *)wfrag, bias, workspace);
-    hipLaunchKernelGGL(k_reduce, dim3((kPartial + 255) / 256), dim3(256), 0, (hipStream_t)stream, workspace,
-                       (int64_t)grid * kWaves, grad);
+    // the group sums go after the records in the workspace (r48_cnn_train_workspace_floats)
+    float *group_sums = workspace + (int64_t)grid * kWaves * kPartial;
+    hipLaunchKernelGGL(k_reduce_groups, dim3((kPartial + 255) / 256, kGroups), dim3(256), 0, (hipStream_t)stream,
+                       workspace, (int64_t)grid * kWaves, group_sums);
+    hipLaunchKernelGGL(k_reduce, dim3((kPartial + 255) / 256), dim3(256), 0, (hipStream_t)stream, group_sums, grad);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess)
         return fail(R48_EHIP, std::string("k_cnn_train: ") + hipGetErrorString(e));
