@@ -293,6 +293,13 @@ int r48_resnet_q_forward(const int8_t *boards, int64_t n, const void *wblob, con
                          const float *head_b, float *q, int8_t *actions, float eps, uint64_t seed,
                          int64_t gid0, uint32_t ctr, void *stream);
 int64_t r48_resnet_q_blob_bytes(void);
+/* The packing of rein48_amd/dqn/fused.py:pack_resnet in one launch (eval-mode BN folded, bf16
+ * fragments, head layout): ptrs is a DEVICE array of 56 float pointers -- for conv L = 0..8 (stem,
+ * conv1..8): weight [co][ci][3][3], bias [co], BN gamma, beta, running mean, running var (gamma
+ * NULL: no BN) -- then head weight [4][1024] and head bias [4]. Same layout as pack_resnet; the
+ * BN scale is computed with correctly rounded f32 division and sqrt (may differ from PyTorch's
+ * in the last ulp). */
+int r48_resnet_pack(const float *const *ptrs, float bn_eps, void *wblob, void *head_w, float *head_b, void *stream);
 
 /* Structured 3x3 (pad 1) conv weight on the 4x4 grid for the ResNet's GEMM form
  * (rein48_amd/dqn/nets.py dense_conv_weight): w float[co][ci][3][3] -> dense[16 co][16 ci] (f32 or

@@ -370,6 +370,72 @@ __global__ __launch_bounds__(kThreads, 1) void k_resnet_q(const int8_t *__restri
     __builtin_amdgcn_s_waitcnt(0);                     // no DMA left in flight at exit
 }
 
+// ---- weight packing for k_resnet_q (rein48_amd/dqn/fused.py pack_resnet, one launch instead of ~50
+// PyTorch ops per repack). ptr[6 L + {0..5}] = conv L's weight [co][ci][3][3], bias [co], BN gamma,
+// beta, running mean, running var (gamma NULL: no BN); ptr[54], ptr[55] = head weight [4][1024],
+// bias [4]. Folding as ResNet10Q.folded(): s = gamma / sqrt(var + eps), w s, (b - mean) s + beta,
+// in f32 with correctly rounded sqrt and division, then bf16 (RNE): the layout is exactly the
+// PyTorch packing's; the BN scale may differ from PyTorch's in the last f32 ulp (tests/test_dqn_gpu.py).
+__device__ __forceinline__ float bn_scale(const float *const *p, int L, int co, float eps)
+{
+    const float *g = p[6 * L + 2];
+    return g ? __fdiv_rn(g[co], __fsqrt_rn(__fadd_rn(p[6 * L + 5][co], eps))) : 1.0f;
+}
+
+__global__ __launch_bounds__(256) void k_resnet_pack(const float *const *__restrict__ p, float eps,
+                                                      uint16_t *__restrict__ blob, uint16_t *__restrict__ head_w,
+                                                      float *__restrict__ head_b)
+{
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;     // bf16 element of the blob
+    constexpr int64_t kBlobElems = (int64_t)kBlobFrags * 512;
+    if (e < kBlobElems) {
+        const int frag = (int)(e / 512), lane = (int)(e % 512) / 8, j = (int)(e % 8);
+        const int r = lane & 31, h = lane >> 5;
+        int L, f, nch, ci_n;
+        if (frag < kStemBlock) {
+            L = 0, f = frag, nch = 2, ci_n = 18;
+        } else {
+            L = 1 + (frag - kStemBlock) / kConvBlock, f = (frag - kStemBlock) % kConvBlock, nch = 4, ci_n = 64;
+        }
+        const int nfrag = 9 * nch * 2;
+        uint16_t out;
+        if (f == nfrag) {   // bias fragment: 64 f32 (folded bias) then zeros, as bf16 pairs
+            const int word = (int)(e % 512) / 2, half = (int)(e % 2);
+            float v = 0.0f;
+            if (word < 64) {
+                const float sc = bn_scale(p, L, word, eps);
+                const float b = p[6 * L + 1][word];
+                // separate correctly rounded ops, as PyTorch's two elementwise kernels (no FMA)
+                v = p[6 * L + 2] ? __fadd_rn(__fmul_rn(__fsub_rn(b, p[6 * L + 4][word]), sc), p[6 * L + 3][word]) : b;
+            }
+            out = (uint16_t)(__float_as_uint(v) >> (16 * half));
+        } else {
+            const int m = f & 1, sk = (f >> 1) % nch, t = (f >> 1) / nch;
+            const int co = 32 * m + r;
+            const int ci = nch == 2 ? 16 * sk + 8 * h + j : 16 * sk + 8 * (j >> 2) + 4 * h + (j & 3);
+            float v = 0.0f;
+            if (ci < ci_n)
+                v = __fmul_rn(p[6 * L][((int64_t)co * ci_n + ci) * 9 + t], bn_scale(p, L, co, eps));
+            const __bf16 bv = (__bf16)v;
+            out = __builtin_bit_cast(uint16_t, bv);
+        }
+        blob[e] = out;
+        return;
+    }
+    const int64_t k = e - kBlobElems;                                 // head weight element
+    if (k < kHeadBf16) {
+        const int cell = (int)(k / 256), hh = (int)(k / 128) % 2, a = (int)(k / 32) % 4, idx = (int)(k % 32);
+        const int kk = idx >> 1, ee = idx & 1, sq = kk >> 2, q = kk & 3, m = sq >> 1;
+        const int i = 8 * (sq & 1) + 2 * q + ee;
+        const int ci = 32 * m + 8 * (i >> 2) + 4 * hh + (i & 3);
+        const __bf16 bv = (__bf16)p[54][a * 1024 + cell * 64 + ci];
+        head_w[k] = __builtin_bit_cast(uint16_t, bv);
+        return;
+    }
+    if (k - kHeadBf16 < 4)
+        head_b[k - kHeadBf16] = p[55][k - kHeadBf16];
+}
+
 int fail(int code, const char *msg)
 {
     r48::set_last_error(msg);
@@ -414,5 +480,20 @@ int r48_resnet_q_forward(const int8_t *boards, int64_t n, const void *wblob, con
 }
 
 int64_t r48_resnet_q_blob_bytes(void) { return (int64_t)kBlobFrags * 1024; }
+
+int r48_resnet_pack(const float *const *ptrs, float bn_eps, void *wblob, void *head_w, float *head_b, void *stream)
+{
+    if (!ptrs || !wblob || !head_w || !head_b || ((uintptr_t)wblob & 15u) || ((uintptr_t)head_w & 15u))
+        return fail(R48_EINVAL, "r48_resnet_pack: NULL or misaligned argument");
+    const int64_t total = (int64_t)kBlobFrags * 512 + kHeadBf16 + 4;
+    hipLaunchKernelGGL(k_resnet_pack, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream, ptrs,
+                       bn_eps, (uint16_t *)wblob, (uint16_t *)head_w, head_b);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        r48::set_last_error(std::string("k_resnet_pack: ") + hipGetErrorString(e));
+        return R48_EHIP;
+    }
+    return R48_OK;
+}
 
 }  // extern "C"

@@ -112,6 +112,44 @@ def pack_resnet(net):
     return blob, head_w, hb.float().contiguous()
 
 
+_PTRS = {}
+
+
+@torch.no_grad()
+def pack_resnet_gpu(net, out=None):
+    """pack_resnet in one HIP launch (r48_resnet_pack): same layout, BN scale correctly rounded
+    in f32 (PyTorch's may differ in the last ulp); `out` (a previous result for the same net) is
+    overwritten in place."""
+    if net.channels != 64 or net.n_blocks != 4:
+        raise ValueError("the fused kernel is built for ResNet10Q(channels=64, blocks=4)")
+    dev = net.head.weight.device
+    tensors = []
+    for k, conv in enumerate(net.conv_layers()):
+        bn = net.bns[k] if net.use_bn else None
+        tensors += [conv.weight, conv.bias] + ([bn.weight, bn.bias, bn.running_mean, bn.running_var] if bn is not None
+                                               else [None] * 4)
+    tensors += [net.head.weight, net.head.bias]
+    for t in tensors:
+        if t is not None and (t.dtype != torch.float32 or not t.is_contiguous() or t.device != dev):
+            raise ValueError("pack_resnet_gpu needs contiguous fp32 parameters on the net's device")
+    addrs = tuple(0 if t is None else t.data_ptr() for t in tensors)
+    key = (str(dev), addrs)
+    if key not in _PTRS:                     # parameter storage is stable between updates: upload once
+        _PTRS.clear() if len(_PTRS) > 16 else None
+        _PTRS[key] = torch.tensor(addrs, dtype=torch.int64, device=dev)
+    ptrs = _PTRS[key]
+    if out is None:
+        blob = torch.empty(_lib.load().r48_resnet_q_blob_bytes() // 2, dtype=torch.bfloat16, device=dev)
+        head_w = torch.empty(16 * 2 * 4 * 32, dtype=torch.bfloat16, device=dev)
+        head_b = torch.empty(4, dtype=torch.float32, device=dev)
+    else:
+        blob, head_w, head_b = out
+    eps = float(net.bns[0].eps) if net.use_bn else 1e-5
+    check(_lib.load().r48_resnet_pack(ptr(ptrs), C.c_float(eps), ptr(blob), ptr(head_w), ptr(head_b),
+                                      C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)))
+    return blob, head_w, head_b
+
+
 def resnet_q_forward(boards, packed, q=True, actions=False, eps=0.0, seed=0, ctr=0, gid0=0):
     """Fused ResNet-10 inference over int8 boards [n, 16] -> (Q [n, 4] or None, actions [n] or None)."""
     if not boards.is_cuda or boards.dtype != torch.int8 or not boards.is_contiguous():

@@ -125,10 +125,10 @@ class DQNTrainer:
 
     def packed(self, net):
         """Fused-kernel weights of `net` (eval-mode BN folded), repacked when the weights changed."""
-        from .fused import pack_resnet
+        from .fused import pack_resnet_gpu
         ver, p = self._packed.get(id(net), (-1, None))
         if ver != self._version:
-            p = pack_resnet(net)
+            p = pack_resnet_gpu(net, out=p)    # one HIP launch, into the previous buffers
             self._packed[id(net)] = (self._version, p)
         return p
 

@@ -1,7 +1,7 @@
 import sys, time, torch
 sys.path.insert(0, ".")
 from rein48_amd.dqn import DQNConfig, DQNTrainer
-from rein48_amd.dqn.fused import pack_resnet
+from rein48_amd.dqn.fused import pack_resnet, pack_resnet_gpu
 cfg = DQNConfig(n_boards=1 << 21, replay_capacity=1 << 25, batch=1 << 16, learn_start=1, seed=1, act_chunk=1 << 18)
 tr = DQNTrainer(cfg, device="cuda:0")
 tr.train_step()
@@ -16,5 +16,6 @@ def act_after_update():
     tr.act()
 print("act cached pack   gpu/wall ms", t(tr.act))
 print("act + repack      gpu/wall ms", t(act_after_update))
-print("pack only         gpu/wall ms", t(lambda: pack_resnet(tr.net)))
+print("pack (PyTorch)    gpu/wall ms", t(lambda: pack_resnet(tr.net)))
+print("pack (HIP)        gpu/wall ms", t(lambda: pack_resnet_gpu(tr.net)))
 print("update            gpu/wall ms", t(tr.update))
