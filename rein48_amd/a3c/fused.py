@@ -50,6 +50,17 @@ _MAPS = None
 _MAPS_BWD = None
 
 
+_DEV_MAPS = {}
+
+
+def _on_device(name, maps, dev):
+    """The index maps on `dev`, uploaded once (a host-to-device copy per pack stalls the stream)."""
+    key = (name, str(dev))
+    if key not in _DEV_MAPS:
+        _DEV_MAPS[key] = tuple(torch.as_tensor(m, device=dev) for m in maps)
+    return _DEV_MAPS[key]
+
+
 @torch.no_grad()
 def pack_cnn(net):
     """-> (wfrag bf16 [41, 64, 8], bias f32 [104]) on the net's device."""
@@ -57,7 +68,7 @@ def pack_cnn(net):
     if _MAPS is None:
         _MAPS = _index_maps()
     dev = net.conv1.weight.device
-    w1_idx, w2_idx, wh_idx = (torch.as_tensor(m, device=dev) for m in _MAPS)
+    w1_idx, w2_idx, wh_idx = _on_device("fwd", _MAPS, dev)
     w1_dense, _, _, _ = net.dense_weights()
     f1 = w1_dense.reshape(-1)[w1_idx]
     f2 = net.conv2.weight.reshape(-1)[w2_idx]
@@ -80,7 +91,7 @@ def pack_cnn_train(net):
         _MAPS_BWD = _index_maps_backward()
     wfrag, bias = pack_cnn(net)
     dev = net.conv1.weight.device
-    wht_idx, w2t_idx = (torch.as_tensor(m, device=dev) for m in _MAPS_BWD)
+    wht_idx, w2t_idx = _on_device("bwd", _MAPS_BWD, dev)
     hw = torch.cat([net.heads.weight.reshape(-1), torch.zeros(1, device=dev)])
     fwht = hw[torch.where(wht_idx < 0, hw.numel() - 1, wht_idx)]
     fw2t = net.conv2.weight.reshape(-1)[w2t_idx]
