@@ -202,7 +202,8 @@ def _ddp_worker(rank, world, port, q):
         local = flat.grad.clone()
         flat.allreduce_grad()
         opt.step()
-        q.put((rank, local, flat.grad.clone(), flat.data.clone()))
+        # numpy copies: torch tensors travel as shared-memory fds that vanish when the worker exits
+        q.put((rank, local.numpy().copy(), flat.grad.numpy().copy(), flat.data.numpy().copy()))
     finally:
         dist.destroy_process_group()
 
@@ -220,7 +221,7 @@ def test_two_rank_gradient_allreduce_gloo():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    (_, l0, g0, d0), (_, l1, g1, d1) = res
+    (_, l0, g0, d0), (_, l1, g1, d1) = [(r, *map(torch.from_numpy, t)) for r, *t in res]
     torch.testing.assert_close(g0, (l0 + l1) / 2)
     torch.testing.assert_close(g0, g1)
     torch.testing.assert_close(d0, d1)
