@@ -1,9 +1,12 @@
 """float64 numpy restatement of the reference A3C maths -- TEST INFRASTRUCTURE ONLY.
 
 nevertiree/Rein48 algorithm/a3c/a3c.py cannot run (a3c.py:8 imports the missing
-game.game_cli; TensorFlow 1.x is not installed), so this restatement is "parity unpinned":
-it follows the reference's formulas line by line, and tests/test_a3c.py checks the product
-(PyTorch-ROCm + HIP kernels) against it within fp32 tolerance.
+game.game_cli; TensorFlow 1.x is not installed), so the TF parts of this restatement (net,
+losses, optimiser) are "parity unpinned": they follow the reference's formulas line by line,
+and tests/test_a3c.py checks the product (PyTorch-ROCm + HIP kernels) against them within fp32
+tolerance. Two parts ARE pinned (tests/golden/a3c_golden.json, tests/golden/make_a3c_golden.py):
+target_values by the reference's own _get_target_value_list executed on 48 seeded reward lists,
+and choose_action by numpy's np.random.choice in the a3c.py:89-93 call form.
 
   net_forward        a3c.py:136-169  actor 16->64 relu6 ->(dropout = identity)-> 64->4 relu -> softmax;
                                       critic 16->64 relu6 -> 64->1; input = raw tile values

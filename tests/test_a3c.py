@@ -225,3 +225,27 @@ def test_two_rank_gradient_allreduce_gloo():
     torch.testing.assert_close(g0, (l0 + l1) / 2)
     torch.testing.assert_close(g0, g1)
     torch.testing.assert_close(d0, d1)
+
+
+def _a3c_golden():
+    import json
+    import os
+    return json.load(open(os.path.join(os.path.dirname(__file__), "golden", "a3c_golden.json")))
+
+
+def test_oracle_target_values_pinned_by_reference():
+    """oracle.target_values == the reference's own _get_target_value_list (a3c.py:246-256),
+    executed in tests/golden/make_a3c_golden.py, on 48 seeded reward lists (T = 1..100)."""
+    g = _a3c_golden()
+    for c in g["returns"]:
+        got = R.target_values(np.asarray(c["rewards"], np.float64), c["last_target_value"])
+        np.testing.assert_allclose(got, c["targets"], rtol=1e-12, atol=1e-12)
+
+
+def test_oracle_choose_action_pinned_by_numpy_choice():
+    """oracle.choose_action(p, u) == np.random.choice(range(4), p=p) (the a3c.py:89-93 call) for
+    the uniform u that numpy's legacy sampler drew under the same seed."""
+    g = _a3c_golden()
+    p = np.array([c["p"] for c in g["choice"]])
+    u = np.array([c["u"] for c in g["choice"]])
+    np.testing.assert_array_equal(R.choose_action(p, u), [c["action"] for c in g["choice"]])

@@ -71,6 +71,28 @@ def test_discounted_returns_match_oracle(drop_last):
         assert (out[L:, i] == 0).all()
 
 
+def test_discounted_returns_match_reference_golden():
+    """r48_discounted_returns (drop-last mode) vs the reference's own _get_target_value_list
+    outputs (tests/golden/a3c_golden.json, made by executing a3c.py:246-256), all 48 cases in
+    one launch, fp32 tolerance rtol=1e-5."""
+    import json
+    import os
+    from rein48_amd.a3c import kernels as K
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "a3c_golden.json")))["returns"]
+    T, n = max(len(c["rewards"]) for c in g), len(g)
+    rewards = np.zeros((T, n), np.float32)
+    for i, c in enumerate(g):
+        rewards[:len(c["rewards"]), i] = c["rewards"]
+    lengths = np.array([len(c["rewards"]) for c in g], np.int32)
+    boot = np.array([c["last_target_value"] for c in g], np.float32)
+    out = K.discounted_returns(torch.from_numpy(rewards).to(DEV), torch.from_numpy(lengths).to(DEV),
+                               torch.from_numpy(boot).to(DEV), 0.9, drop_last=True).cpu().numpy()
+    for i, c in enumerate(g):
+        L = lengths[i]
+        np.testing.assert_allclose(out[:L, i], c["targets"], rtol=1e-5, atol=1e-4)
+        assert (out[L:, i] == 0).all()
+
+
 def test_rmsprop_kernel_matches_oracle():
     from rein48_amd.a3c import kernels as K
     rng = np.random.default_rng(3)
