@@ -301,6 +301,15 @@ int64_t r48_resnet_q_blob_bytes(void);
  * in the last ulp). */
 int r48_resnet_pack(const float *const *ptrs, float bn_eps, void *wblob, void *head_w, float *head_b, void *stream);
 
+/* Cell-grouped variant of r48_resnet_q_forward (csrc/r48_resnet2.hip: v_mfma_f32_16x16x32_bf16,
+ * columns = 16 boards at one cell, only the 100 in-grid (cell, tap) pairs issued). Same network,
+ * outputs and Philox contract; boards 16-byte aligned; wblob (r48_resnet2_q_blob_bytes() bytes)
+ * holds every layer including the head, packed by r48_resnet2_pack (ptrs as r48_resnet_pack). */
+int r48_resnet2_q_forward(const int8_t *boards, int64_t n, const void *wblob, float *q, int8_t *actions,
+                          float eps, uint64_t seed, int64_t gid0, uint32_t ctr, void *stream);
+int64_t r48_resnet2_q_blob_bytes(void);
+int r48_resnet2_pack(const float *const *ptrs, float bn_eps, void *wblob, void *stream);
+
 /* Structured 3x3 (pad 1) conv weight on the 4x4 grid for the ResNet's GEMM form
  * (rein48_amd/dqn/nets.py dense_conv_weight): w float[co][ci][3][3] -> dense[16 co][16 ci] (f32 or
  * bf16, 16-byte aligned), block (P, Q) = w[:, :, dr + 1, dc + 1] where input cell Q = P + 4 dr + dc

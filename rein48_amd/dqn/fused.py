@@ -163,3 +163,96 @@ def resnet_q_forward(boards, packed, q=True, actions=False, eps=0.0, seed=0, ctr
                                            float(eps), int(seed) & (2 ** 64 - 1), int(gid0), int(ctr) & 0xFFFFFFFF,
                                            C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)))
     return qt, at
+
+
+# ---- cell-grouped kernel (r48_resnet2_*, csrc/r48_resnet2.hip) -------------------------------
+# v_mfma_f32_16x16x32_bf16 A fragments, lane l: row r = l & 15, channel group g = l >> 4, element j;
+# the k order of chunk c is channel 16(2c + (j >> 2)) + 4g + (j & 3) (the accumulator layout):
+#   stem (tap t, row tile o):              W0[16o + r][8g + j][t]          (planes >= 18: 0)
+#   conv (tap t, row tile o, k-chunk c):   W[16o + r][16(2c + (j>>2)) + 4g + (j&3)][t]
+#   head (cell p, k-chunk c):              Wh[r][64 p + same channel]      (rows r >= 4: 0)
+# blob = stem (36 + bias) | conv1..8 (72 + bias each) | head (32 + bias of 4 floats), 1 KiB fragments.
+_MAPS2 = {}
+
+
+def _maps2():
+    if _MAPS2:
+        return _MAPS2["m"]
+    lane = np.arange(64)
+    r, g = (lane & 15)[:, None], (lane >> 4)[:, None]
+    j = np.arange(8)[None, :]
+    ch = lambda c: 16 * (2 * c + (j >> 2)) + 4 * g + (j & 3)
+    st = [np.where(8 * g + j < 18, ((16 * o + r) * 18 + 8 * g + j) * 9 + t, -1)
+          for t in range(9) for o in range(4)]
+    cv = [((16 * o + r) * 64 + ch(c)) * 9 + t for t in range(9) for o in range(4) for c in range(2)]
+    hd = [np.where(r < 4, r * 1024 + 64 * p + ch(c), -1) for p in range(16) for c in range(2)]
+    _MAPS2["m"] = tuple(np.stack(m).astype(np.int64) for m in (st, cv, hd))
+    return _MAPS2["m"]
+
+
+@torch.no_grad()
+def pack_resnet2(net):
+    """Host (PyTorch gather) packing for r48_resnet2_q_forward -> blob bf16 [frags * 512]; the
+    reference that r48_resnet2_pack is tested against."""
+    if net.channels != 64 or net.n_blocks != 4:
+        raise ValueError("the fused kernel is built for ResNet10Q(channels=64, blocks=4)")
+    dev = net.head.weight.device
+    convs, (hw, hb) = net.folded()
+    st, cv, hd = _maps2()
+    parts = []
+    w, b = convs[0]
+    parts += [_gather(w.reshape(-1), st, dev).reshape(-1), _bias_frag(b, dev)]
+    for w, b in convs[1:]:
+        parts += [_gather(w.reshape(-1), cv, dev).reshape(-1), _bias_frag(b, dev)]
+    parts += [_gather(hw.reshape(-1), hd, dev).reshape(-1), _bias_frag(hb, dev)]
+    blob = torch.cat(parts).contiguous()
+    assert blob.numel() * 2 == _lib.load().r48_resnet2_q_blob_bytes()
+    return blob
+
+
+def _param_ptrs(net, dev):
+    tensors = []
+    for k, conv in enumerate(net.conv_layers()):
+        bn = net.bns[k] if net.use_bn else None
+        tensors += [conv.weight, conv.bias] + ([bn.weight, bn.bias, bn.running_mean, bn.running_var] if bn is not None
+                                               else [None] * 4)
+    tensors += [net.head.weight, net.head.bias]
+    for t in tensors:
+        if t is not None and (t.dtype != torch.float32 or not t.is_contiguous() or t.device != dev):
+            raise ValueError("packing on the GPU needs contiguous fp32 parameters on the net's device")
+    addrs = tuple(0 if t is None else t.data_ptr() for t in tensors)
+    key = (str(dev), addrs)
+    if key not in _PTRS:                     # parameter storage is stable between updates: upload once
+        _PTRS.clear() if len(_PTRS) > 16 else None
+        _PTRS[key] = torch.tensor(addrs, dtype=torch.int64, device=dev)
+    return _PTRS[key]
+
+
+@torch.no_grad()
+def pack_resnet2_gpu(net, out=None):
+    """pack_resnet2 in one HIP launch (r48_resnet2_pack); `out` is overwritten in place."""
+    if net.channels != 64 or net.n_blocks != 4:
+        raise ValueError("the fused kernel is built for ResNet10Q(channels=64, blocks=4)")
+    dev = net.head.weight.device
+    ptrs = _param_ptrs(net, dev)
+    blob = torch.empty(_lib.load().r48_resnet2_q_blob_bytes() // 2, dtype=torch.bfloat16, device=dev) \
+        if out is None else out
+    eps = float(net.bns[0].eps) if net.use_bn else 1e-5
+    check(_lib.load().r48_resnet2_pack(ptr(ptrs), C.c_float(eps), ptr(blob),
+                                       C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)))
+    return blob
+
+
+def resnet2_q_forward(boards, blob, q=True, actions=False, eps=0.0, seed=0, ctr=0, gid0=0):
+    """Cell-grouped fused ResNet-10 inference over int8 boards [n, 16] -> (Q [n, 4] or None,
+    actions [n] or None)."""
+    if not boards.is_cuda or boards.dtype != torch.int8 or not boards.is_contiguous():
+        raise ValueError("boards must be a contiguous int8 GPU tensor")
+    n = boards.numel() // 16
+    dev = boards.device
+    qt = torch.empty((n, 4), dtype=torch.float32, device=dev) if q else None
+    at = torch.empty(n, dtype=torch.int8, device=dev) if actions else None
+    check(_lib.load().r48_resnet2_q_forward(ptr(boards), n, ptr(blob), ptr(qt), ptr(at), float(eps),
+                                            int(seed) & (2 ** 64 - 1), int(gid0), int(ctr) & 0xFFFFFFFF,
+                                            C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)))
+    return qt, at
