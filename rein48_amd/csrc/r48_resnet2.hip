@@ -51,9 +51,11 @@ constexpr int kHeadOff = kStemBlock + kConvLayers * kConvBlock;
 constexpr int kBlobFrags = kHeadOff + kHeadBlock;
 constexpr uint32_t kEgreedyTag = 0xD0Eu;
 
-__device__ __forceinline__ bf16x8 lds_frag(const uint4 *lds, int frag, int lane)
+// wl = the lane's 16 B in a weight image (buffer base + lane, see k_resnet2_q's begin): fragment f
+// is one ds_read_b128 at immediate offset 1024 f
+__device__ __forceinline__ bf16x8 lds_frag(const uint4 *wl, int frag, int)
 {
-    const uint4 v = lds[frag * 64 + lane];
+    const uint4 v = wl[frag * 64];
     return __builtin_bit_cast(bf16x8, v);
 }
 
@@ -124,9 +126,12 @@ __device__ __forceinline__ void tap(const uint4 *wl, int o, const uint32_t (&x)[
 
 // row tile O of a layer: accumulators start at bias (+ the residual held in out), the centre tap
 // (all 16 cells) first, then the 8 border taps; epilogue relu -> bf16 into out's tile-O slots
-template <int NC, bool RESID, bool OUT_A, int O>
+// `mid` runs between the MFMAs and the epilogue (the last tile of a layer passes the next layer's
+// barrier + weight prefetch there, so this epilogue's VALU shares a scheduling region with the
+// next layer's first MFMAs, which read only k-chunk 0 = row tiles 0 and 1)
+template <int NC, bool RESID, bool OUT_A, int O, typename Mid>
 __device__ __forceinline__ void row_tile(const uint4 *wl, const float *bias, const uint32_t (&x)[16][NC][4],
-                                         uint32_t (&out)[16][2][4], const bf16x8 (&ident)[2], int lane)
+                                         uint32_t (&out)[16][2][4], const bf16x8 (&ident)[2], int lane, Mid &&mid)
 {
     const int g = lane >> 4;
     const f32x4 b4 = *reinterpret_cast<const f32x4 *>(bias + 16 * O + 4 * g);
@@ -157,6 +162,7 @@ __device__ __forceinline__ void row_tile(const uint4 *wl, const float *bias, con
     tap<1, -1, NC>(wl, O, x, acc, lane);
     tap<1, 0, NC>(wl, O, x, acc, lane);
     tap<1, 1, NC>(wl, O, x, acc, lane);
+    mid();
 #pragma unroll
     for (int p = 0; p < 16; p++) {
         const uint32_t lo = relu_pack(acc[p][0], acc[p][1]), hi = relu_pack(acc[p][2], acc[p][3]);
@@ -165,15 +171,19 @@ __device__ __forceinline__ void row_tile(const uint4 *wl, const float *bias, con
     }
 }
 
-template <int NC, bool RESID, bool OUT_A>
-__device__ __forceinline__ void layer(const uint4 *wl, const uint32_t (&x)[16][NC][4], uint32_t (&out)[16][2][4],
-                                      const bf16x8 (&ident)[2], int lane)
+// one layer from the weight image w; `next` (the next layer's begin) runs before the last
+// tile's epilogue
+template <int NC, bool RESID, bool OUT_A, typename Next>
+__device__ __forceinline__ void layer(const uint4 *const (&w)[2], const uint32_t (&x)[16][NC][4],
+                                      uint32_t (&out)[16][2][4], const bf16x8 (&ident)[2], int lane, Next &&next)
 {
-    const float *bias = reinterpret_cast<const float *>(wl + 9 * 4 * NC * 64);
-    row_tile<NC, RESID, OUT_A, 0>(wl, bias, x, out, ident, lane);
-    row_tile<NC, RESID, OUT_A, 1>(wl, bias, x, out, ident, lane);
-    row_tile<NC, RESID, OUT_A, 2>(wl, bias, x, out, ident, lane);
-    row_tile<NC, RESID, OUT_A, 3>(wl, bias, x, out, ident, lane);
+    const uint4 *wl = w[0];
+    const float *bias = reinterpret_cast<const float *>(w[1] + 9 * 4 * NC * 64);
+    auto none = [] {};
+    row_tile<NC, RESID, OUT_A, 0>(wl, bias, x, out, ident, lane, none);
+    row_tile<NC, RESID, OUT_A, 1>(wl, bias, x, out, ident, lane, none);
+    row_tile<NC, RESID, OUT_A, 2>(wl, bias, x, out, ident, lane, none);
+    row_tile<NC, RESID, OUT_A, 3>(wl, bias, x, out, ident, lane, next);
 }
 
 // LDS-DMA of one weight block (frags x 1 KiB): wave w moves fragments w, w + 4, ...
@@ -229,32 +239,40 @@ __global__ __launch_bounds__(kThreads, 1) void k_resnet2_q(const int8_t *__restr
         }
         // weight block blk landed in buf(cur) (own DMA + barrier); the next block (or the next
         // tile's stem) goes into the other buffer, which every wave has finished reading
-        auto begin = [&](int blk) -> const uint4 * {
+        // -> {the lane's 16 B in the image, the image base}. The lane offset is hidden from the
+        // optimiser per layer, so each fragment read is one ds_read_b128 at an immediate offset
+        // from it, instead of per-fragment addresses hoisted out of the tile loop (and spilled)
+        auto begin = [&](int blk, const uint4 *(&w)[2]) {
             __builtin_amdgcn_s_waitcnt(0);
             __syncthreads();
             if (blk + 1 < kConvLayers + 2)
                 stage(blob, blk + 1, buf(cur ^ 1), wave, lane);
             else if (tile + gridDim.x < tiles)
                 stage(blob, 0, buf(cur ^ 1), wave, lane);
-            const uint4 *wl = buf(cur);
+            int idx = cur * (kBufFrags * 64) + lane;
+            asm volatile("" : "+v"(idx));
+            w[0] = lds + idx;
+            w[1] = buf(cur);
             cur ^= 1;
-            return wl;
         };
-        layer<1, false, true>(begin(0), oh, h, ident, lane);
+        const uint4 *w[2];
+        begin(0, w);
+        layer<1, false, true>(w, oh, h, ident, lane, [&] { begin(1, w); });
         for (int blk = 0; blk < kConvLayers / 2; blk++) {
-            layer<2, false, false>(begin(1 + 2 * blk), h, y, ident, lane);   // first conv of a block: h stays as the skip
-            layer<2, true, true>(begin(2 + 2 * blk), y, h, ident, lane);    // second conv: bias + skip, output over h
+            // first conv of a block: h stays as the skip; second conv: bias + skip, output over h
+            layer<2, false, false>(w, h, y, ident, lane, [&] { begin(2 + 2 * blk, w); });
+            layer<2, true, true>(w, y, h, ident, lane, [&] { begin(3 + 2 * blk, w); });
         }
         {
-            // head: Q rows = actions (fragment rows >= 4 are zero), columns = the 16 boards
-            const uint4 *wl = begin(kConvLayers + 1);
+            // head (its weights were begun inside the last conv): Q rows = actions (fragment
+            // rows >= 4 are zero), columns = the 16 boards
             f32x4 qa = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int p = 0; p < 16; p++)
 #pragma unroll
                 for (int c = 0; c < 2; c++)
-                    qa = mfma(lds_frag(wl, 2 * p + c, lane), as_b(h[p][c]), qa);
-            const float *hb = reinterpret_cast<const float *>(wl + 32 * 64);
+                    qa = mfma(lds_frag(w[0], 2 * p + c, lane), as_b(h[p][c]), qa);
+            const float *hb = reinterpret_cast<const float *>(w[1] + 32 * 64);
             if (g == 0 && b < n) {
                 const float4 qv = make_float4(qa[0] + hb[0], qa[1] + hb[1], qa[2] + hb[2], qa[3] + hb[3]);
                 if (q_out)
