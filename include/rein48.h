@@ -285,30 +285,22 @@ int r48_td_target(const float *reward, const uint8_t *done, const float *q_next_
                   const float *q_next_online, int64_t n, float gamma, float *y, void *stream);
 
 /* Fused ResNet-10 Q-network inference on bf16 MFMA (rein48_amd/dqn/nets.py:ResNet10Q with
- * C = 64, 4 basic blocks, eval-mode BN folded): boards int8[n][16] -> q float[n][4] (nullable,
- * 16-byte aligned) and, when actions != NULL, the epsilon-greedy draw of r48_egreedy_actions
- * (same Philox contract) into actions int8[n]. wblob (r48_resnet_q_blob_bytes() bytes), head_w
- * (8 KiB bf16) and head_b (4 floats) are packed by rein48_amd/dqn/fused.py:pack_resnet. */
-int r48_resnet_q_forward(const int8_t *boards, int64_t n, const void *wblob, const void *head_w,
-                         const float *head_b, float *q, int8_t *actions, float eps, uint64_t seed,
-                         int64_t gid0, uint32_t ctr, void *stream);
+ * C = 64, 4 basic blocks, eval-mode BN folded): boards int8[n][16] (16-byte aligned) -> q
+ * float[n][4] (nullable, 16-byte aligned) and, when actions != NULL, the epsilon-greedy draw of
+ * r48_egreedy_actions (same Philox contract) into actions int8[n]. wblob
+ * (r48_resnet_q_blob_bytes() bytes, 16-byte aligned: every layer incl. the head as
+ * v_mfma_f32_16x16x32_bf16 fragments) is packed by r48_resnet_pack or
+ * rein48_amd/dqn/fused.py:pack_resnet. */
+int r48_resnet_q_forward(const int8_t *boards, int64_t n, const void *wblob, float *q, int8_t *actions,
+                         float eps, uint64_t seed, int64_t gid0, uint32_t ctr, void *stream);
 int64_t r48_resnet_q_blob_bytes(void);
 /* The packing of rein48_amd/dqn/fused.py:pack_resnet in one launch (eval-mode BN folded, bf16
- * fragments, head layout): ptrs is a DEVICE array of 56 float pointers -- for conv L = 0..8 (stem,
- * conv1..8): weight [co][ci][3][3], bias [co], BN gamma, beta, running mean, running var (gamma
- * NULL: no BN) -- then head weight [4][1024] and head bias [4]. Same layout as pack_resnet; the
- * BN scale is computed with correctly rounded f32 division and sqrt (may differ from PyTorch's
- * in the last ulp). */
-int r48_resnet_pack(const float *const *ptrs, float bn_eps, void *wblob, void *head_w, float *head_b, void *stream);
-
-/* Cell-grouped variant of r48_resnet_q_forward (csrc/r48_resnet2.hip: v_mfma_f32_16x16x32_bf16,
- * columns = 16 boards at one cell, only the 100 in-grid (cell, tap) pairs issued). Same network,
- * outputs and Philox contract; boards 16-byte aligned; wblob (r48_resnet2_q_blob_bytes() bytes)
- * holds every layer including the head, packed by r48_resnet2_pack (ptrs as r48_resnet_pack). */
-int r48_resnet2_q_forward(const int8_t *boards, int64_t n, const void *wblob, float *q, int8_t *actions,
-                          float eps, uint64_t seed, int64_t gid0, uint32_t ctr, void *stream);
-int64_t r48_resnet2_q_blob_bytes(void);
-int r48_resnet2_pack(const float *const *ptrs, float bn_eps, void *wblob, void *stream);
+ * fragments): ptrs is a DEVICE array of 56 float pointers -- for conv L = 0..8 (stem, conv1..8):
+ * weight [co][ci][3][3], bias [co], BN gamma, beta, running mean, running var (gamma NULL: no BN)
+ * -- then head weight [4][1024] and head bias [4]. Same layout as pack_resnet; the BN scale is
+ * computed with correctly rounded f32 division and sqrt (may differ from PyTorch's in the last
+ * ulp). */
+int r48_resnet_pack(const float *const *ptrs, float bn_eps, void *wblob, void *stream);
 
 /* Structured 3x3 (pad 1) conv weight on the 4x4 grid for the ResNet's GEMM form
  * (rein48_amd/dqn/nets.py dense_conv_weight): w float[co][ci][3][3] -> dense[16 co][16 ci] (f32 or

@@ -28,12 +28,9 @@ SIGNATURES = {
     "r48_cnn_train_grad": (C.c_int, [_P, _I64, _I64, _P, _P, _P, _P, _P, C.c_float, _I32, _P, _P, _P, _P, _P]),
     "r48_cnn_train_workspace_floats": (_I64, []),
     "r48_cnn_train_grad_floats": (_I64, []),
-    "r48_resnet_q_forward": (C.c_int, [_P, _I64, _P, _P, _P, _P, _P, C.c_float, _U64, _I64, _U32, _P]),
+    "r48_resnet_q_forward": (C.c_int, [_P, _I64, _P, _P, _P, C.c_float, _U64, _I64, _U32, _P]),
     "r48_resnet_q_blob_bytes": (_I64, []),
-    "r48_resnet_pack": (C.c_int, [_P, C.c_float, _P, _P, _P, _P]),
-    "r48_resnet2_q_forward": (C.c_int, [_P, _I64, _P, _P, _P, C.c_float, _U64, _I64, _U32, _P]),
-    "r48_resnet2_q_blob_bytes": (_I64, []),
-    "r48_resnet2_pack": (C.c_int, [_P, C.c_float, _P, _P]),
+    "r48_resnet_pack": (C.c_int, [_P, C.c_float, _P, _P]),
     "r48_struct_conv_weight": (C.c_int, [_P, _I32, _I32, _I32, _P, _P]),
     "r48_struct_conv_weight_grad": (C.c_int, [_P, _I32, _I32, _I32, _P, _P]),
     "r48_bn_workspace_floats": (_I64, [_I64, _I32]),

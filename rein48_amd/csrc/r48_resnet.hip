@@ -1,29 +1,33 @@
 // r48_resnet.hip -- fused ResNet-10 Q-network inference on gfx950 MFMA (BASELINE config 5).
 //
-// rein48_amd/dqn/nets.py:ResNet10Q in eval mode (BatchNorm folded into the convs on the host,
-// rein48_amd/dqn/fused.py:pack_resnet), forward only, for acting on millions of boards:
+// rein48_amd/dqn/nets.py:ResNet10Q in eval mode (BatchNorm folded by k_resnet_pack or the host
+// pack_resnet), forward only, for acting on millions of boards:
 //   x   = one-hot of the 16 cell exponents (18 planes)
 //   h   = relu(conv3x3(x))                                     stem, 18 -> 64
 //   4 x h = relu(conv3x3(relu(conv3x3(h))) + h)                basic blocks, 64 -> 64
 //   Q   = Wh . flatten(h) + bh                                 head, 1024 -> 4
 // and optionally the epsilon-greedy draw of r48_egreedy_actions (same Philox contract).
 //
-// Orientation (v_mfma_f32_32x32x16_bf16): rows = 32 output channels (two tiles per layer),
-// columns = 32 board-positions = 2 boards x 16 cells. Lane l owns column l & 31 (board
-// (l & 31) >> 4, cell l & 15) and the half h = l >> 5 of its K range. A layer's 32x32 f32
-// accumulators therefore hold each cell's channel vector in that cell's own lanes, and the next
-// layer's B operand is built in registers: the 3x3 tap (dr, dc) reads cell p + 4dr + dc, which
-// is the lane 4dr + dc further along the same 16-lane DPP row (one board = one DPP row), so a
-// tap is a v_mov_b32_dpp row shift with zero fill (cells past the top/bottom edge fall off the
-// row) plus a v_cndmask for the left/right edge. No LDS traffic for activations, no lane
-// crossing between boards. The k order inside a fragment follows the accumulator layout
-// (element j of half h = channel 16s + 8(j>>2) + 4h + (j&3) of k-chunk s); the host packs the
-// weight (A) fragments in that order.
-// Per column group (2 boards) a 64->64 layer is 9 taps x 4 k-chunks x 2 row tiles = 72 MFMAs;
-// each wave carries G column groups (2G boards) so one LDS weight fragment feeds 2G MFMAs.
-// Weights: each layer's 72 fragments + its bias (1 KiB each) stream into one of two LDS
-// buffers by global_load_lds while the other buffer's layer computes; the workgroup is
-// persistent (one per CU, 8 waves) and cycles stem, conv1..conv8 per 32-board tile.
+// Cell-grouped tiling (replaced a 32x32x16 kernel with columns = 2 boards x 16 cells and the
+// taps as DPP row shifts: that one issued all 144 (cell, tap) pairs with zero fill and re-read an
+// LDS weight fragment every 4 MFMAs -- 14.8 ms per 2^21 boards against 9.75 ms here):
+// v_mfma_f32_16x16x32_bf16 with rows = 16 output channels (four row tiles per 64-channel layer)
+// and columns = 16 BOARDS at the SAME cell. A wave owns 16 boards and keeps all 16 cells of
+// them in registers: x[cell][k-chunk][4] packed bf16, lane l = board l & 15, channel group
+// g = l >> 4. The 3x3 tap (dr, dc) of output cell p reads input cell q = p + 4dr + dc, i.e.
+// simply another register array -- no lane movement, and only the 100 in-grid (cell, tap)
+// pairs are issued (the 32x32 kernel issues all 144 with zero fill). One LDS weight fragment
+// (tap, row tile, k-chunk) feeds every cell that has that tap (9, 12 or 16 MFMAs).
+// Accumulator layout (16x16): lane l holds rows 4g..4g+3 of column l & 15, so a finished row
+// tile o leaves channels 16o + 4g + i of board l & 15 in the lane; k-chunk c of the next layer
+// packs tiles 2c and 2c+1: element j <-> channel 16(2c + (j >> 2)) + 4g + (j & 3), and the
+// host packs the A fragments with the same k order. Row tiles run one after another, each
+// finishing with its epilogue (bias [+ residual], ReLU, bf16), so only 16 x 4 accumulators are
+// live. A basic block's second conv starts its accumulators from bias + the block input (the
+// skip connection) and writes its output over that input.
+// Weights stream per layer (stem 37, conv 73, head 33 fragments of 1 KiB) into a
+// double-buffered LDS image by global_load_lds while the other buffer's layer computes; one
+// persistent workgroup per CU, 4 waves (one per SIMD: ~330 registers per lane), 64 boards per tile.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -38,206 +42,160 @@ void set_last_error(const std::string &msg);
 
 namespace {
 
-using bf16x8 = __attribute__((ext_vector_type(8))) short;
-using f32x16 = __attribute__((ext_vector_type(16))) float;
+using bf16x8 = __attribute__((ext_vector_type(8))) __bf16;
+using f32x4 = __attribute__((ext_vector_type(4))) float;
+using u32x4 = __attribute__((ext_vector_type(4))) uint32_t;
 typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef short i16x2 __attribute__((ext_vector_type(2)));
 
-// 8 waves x 2 column groups (two waves per SIMD, so one wave's exposed LDS-read latency runs
-// under the other's MFMAs) measured 14.7-14.9 ms per 2^21 boards against 15.5 for 4 waves x 4
-// groups and 16.7 for 8 x 1 (bit-identical outputs; tools/exp_resnet_fused.py)
-#ifndef R48_RESNET_WAVES
-#define R48_RESNET_WAVES 8
-#endif
-#ifndef R48_RESNET_G
-#define R48_RESNET_G 2
-#endif
-#ifndef R48_RN_ABL   // timing ablations only (wrong results): 1 no per-layer wait/barrier, 2 also no weight
-#define R48_RN_ABL 0 // DMA, 3 epilogue = bf16 pack only, 4 no DPP row shifts in the taps
-#endif
-constexpr int kWaves = R48_RESNET_WAVES;
+constexpr int kWaves = 4;
 constexpr int kThreads = 64 * kWaves;
-constexpr int G = R48_RESNET_G;                   // column groups (2 boards each) per wave
-constexpr int kBoardsPerTile = kWaves * G * 2;    // 32
+constexpr int kBoardsPerTile = 16 * kWaves;
 constexpr int kConvLayers = 8;
-constexpr int kStemFrags = 9 * 2 * 2;             // taps x k-chunks (18 planes padded to 32) x row tiles
-constexpr int kConvFrags = 9 * 4 * 2;
-constexpr int kStemBlock = kStemFrags + 1;        // + bias fragment
-constexpr int kConvBlock = kConvFrags + 1;
-constexpr int kBufFrags = kConvBlock;             // 73 KiB per LDS buffer
-constexpr int kHeadBf16 = 16 * 2 * 4 * 32;        // [cell][half][action][32 channels]
+constexpr int kStemBlock = 9 * 4 + 1;        // (tap, row tile) fragments + bias fragment
+constexpr int kConvBlock = 9 * 4 * 2 + 1;    // (tap, row tile, k-chunk) + bias
+constexpr int kHeadBlock = 16 * 2 + 1;       // (cell, k-chunk) + bias (4 floats)
+constexpr int kBufFrags = kConvBlock;        // 73 KiB per LDS buffer
+constexpr int kHeadOff = kStemBlock + kConvLayers * kConvBlock;
+constexpr int kBlobFrags = kHeadOff + kHeadBlock;
 constexpr uint32_t kEgreedyTag = 0xD0Eu;
-constexpr int kBlobFrags = kStemBlock + kConvLayers * kConvBlock;
 
-__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi)
+// wl = the lane's 16 B in a weight image (buffer base + lane, see k_resnet_q's begin): fragment f
+// is one ds_read_b128 at immediate offset 1024 f
+__device__ __forceinline__ bf16x8 lds_frag(const uint4 *wl, int frag, int)
 {
-    const bf16x2_t v = {(__bf16)lo, (__bf16)hi};
-    return __builtin_bit_cast(uint32_t, v);
+    const uint4 v = wl[frag * 64];
+    return __builtin_bit_cast(bf16x8, v);
+}
+
+__device__ __forceinline__ bf16x8 as_b(const uint32_t (&r)[4])
+{
+    const u32x4 v = {r[0], r[1], r[2], r[3]};
+    return __builtin_bit_cast(bf16x8, v);
+}
+
+__device__ __forceinline__ f32x4 mfma(bf16x8 a, bf16x8 b, f32x4 c)
+{
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
 __device__ __forceinline__ float bf_lo(uint32_t v) { return __uint_as_float(v << 16); }
 __device__ __forceinline__ float bf_hi(uint32_t v) { return __uint_as_float(v & 0xFFFF0000u); }
 
-// value of cell p + D in the same board (DPP row = 16 lanes), 0 past the row's ends
-template <int D>
-__device__ __forceinline__ uint32_t cell_shift(uint32_t v)
-{
-    if constexpr (D == 0)
-        return v;
-    else if constexpr (D > 0)
-        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x100 + D, 0xF, 0xF, true);   // row_shl: lane i <- i + D
-    else
-        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x110 - D, 0xF, 0xF, true);   // row_shr: lane i <- i - |D|
-}
-
-__device__ __forceinline__ bf16x8 lds_frag(const uint4 *lds, int frag, int lane)
-{
-    const uint4 v = lds[frag * 64 + lane];
-    bf16x8 f;
-    __builtin_memcpy(&f, &v, 16);
-    return f;
-}
-
-// tap (DR, DC) of k-chunk s for all column groups: B = the chunk's registers shifted by DR
-// grid rows (xs[g][DC + 1] already holds the column-shifted, edge-masked copy), times both
-// row tiles -- one pair of LDS weight fragments feeds 2G MFMAs
-template <int DR, int DC, int NCH>
-__device__ __forceinline__ void tap_mfma(const uint4 *wl, int s, const uint32_t (&xs)[G][3][4], f32x16 (&acc)[G][2],
-                                         int lane)
-{
-    constexpr int t = (DR + 1) * 3 + (DC + 1);
-    const bf16x8 A0 = lds_frag(wl, (t * NCH + s) * 2 + 0, lane);
-    const bf16x8 A1 = lds_frag(wl, (t * NCH + s) * 2 + 1, lane);
-#pragma unroll
-    for (int g = 0; g < G; g++) {
-        uint32_t r[4];
-#pragma unroll
-        for (int q = 0; q < 4; q++)
-            r[q] = R48_RN_ABL == 4 ? xs[g][DC + 1][q] : cell_shift<4 * DR>(xs[g][DC + 1][q]);
-        bf16x8 B;
-        __builtin_memcpy(&B, r, 16);
-        acc[g][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A0, B, acc[g][0], 0, 0, 0);
-        acc[g][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A1, B, acc[g][1], 0, 0, 0);
-    }
-}
-
-// the same tap for ONE column group (the last k-chunk runs group by group)
-template <int DR, int DC, int NCH>
-__device__ __forceinline__ void tap_mfma1(const uint4 *wl, int s, const uint32_t (&xs)[3][4], f32x16 &a0, f32x16 &a1,
-                                          int lane)
-{
-    constexpr int t = (DR + 1) * 3 + (DC + 1);
-    const bf16x8 A0 = lds_frag(wl, (t * NCH + s) * 2 + 0, lane);
-    const bf16x8 A1 = lds_frag(wl, (t * NCH + s) * 2 + 1, lane);
-    uint32_t r[4];
-#pragma unroll
-    for (int q = 0; q < 4; q++)
-        r[q] = R48_RN_ABL == 4 ? xs[DC + 1][q] : cell_shift<4 * DR>(xs[DC + 1][q]);
-    bf16x8 B;
-    __builtin_memcpy(&B, r, 16);
-    a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A0, B, a0, 0, 0, 0);
-    a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A1, B, a1, 0, 0, 0);
-}
-
+// relu(lo, hi) as one packed bf16 pair (one v_cvt_pk_bf16_f32, RNE; then ReLU as signed-int16 max)
 typedef float f32x2 __attribute__((ext_vector_type(2)));
-typedef short i16x2 __attribute__((ext_vector_type(2)));
-
-// bias (+ residual) + ReLU of one column group -> packed bf16 activations; SAVE first keeps
-// the layer input in res for the block's skip connection
-template <bool RESID, bool SAVE>
-__device__ __forceinline__ void epilogue1(const f32x16 (&acc)[2], const float *bias, int h, uint32_t (&act)[16],
-                                          uint32_t (&res)[16])
+__device__ __forceinline__ uint32_t relu_pack(float lo, float hi)
 {
-    if (SAVE) {
-#pragma unroll
-        for (int k = 0; k < 16; k++)
-            res[k] = act[k];
+    const i16x2 p = __builtin_bit_cast(i16x2, __builtin_convertvector(f32x2{lo, hi}, bf16x2_t));
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(p, i16x2{0, 0}));
+}
+
+// identity A fragment of row tile O's position in its k-chunk (O & 1): row r = lane & 15 picks
+// channel 16 O + r, which sits in lane group g = r >> 2 at element 4 (O & 1) + (r & 3); MFMA-ing it
+// with the block input adds the skip connection exactly (1.0 x bf16 in f32)
+__device__ __forceinline__ bf16x8 identity_frag(int odd, int lane)
+{
+    const int r = lane & 15, g = lane >> 4;
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+    if (g == (r >> 2)) {
+        const int j = 4 * odd + (r & 3);
+        w[j >> 1] = 0x3F80u << (16 * (j & 1));
     }
+    return as_b(w);
+}
+
+// a packed activation defined in an AGPR: the block input h lives in the accumulator file (MFMA
+// B operands may be AGPRs; VALU reads get a v_accvgpr_read), y and the temporaries in VGPRs, so
+// h + y (256 registers) do not both compete for the 256 VGPRs
+__device__ __forceinline__ uint32_t in_agpr(uint32_t v)
+{
+    uint32_t r;
+    asm("v_accvgpr_write_b32 %0, %1" : "=a"(r) : "v"(v));
+    return r;
+}
+
+// one tap (DR, DC) of row tile o: per k-chunk one LDS fragment, one MFMA per in-grid cell
+template <int DR, int DC, int NC>
+__device__ __forceinline__ void tap(const uint4 *wl, int o, const uint32_t (&x)[16][NC][4], f32x4 (&acc)[16],
+                                    int lane)
+{
+    constexpr int t = (DR + 1) * 3 + (DC + 1);
 #pragma unroll
-    for (int s = 0; s < 4; s++)
+    for (int c = 0; c < NC; c++) {
+        const bf16x8 A = lds_frag(wl, (t * 4 + o) * NC + c, lane);
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const int i = 8 * (s & 1) + 2 * q;
-            // bias of accumulator rows i, i+1: channels 32m + 8(i>>2) + 4h + (i&3), +1
-            if (R48_RN_ABL == 3) {
-                act[4 * s + q] = pack_bf16x2(acc[s >> 1][i], acc[s >> 1][i + 1]);
+        for (int p = 0; p < 16; p++) {
+            const int r = p >> 2, cc = p & 3;
+            if (r + DR < 0 || r + DR > 3 || cc + DC < 0 || cc + DC > 3)
                 continue;
-            }
-            const f32x2 bb = *reinterpret_cast<const f32x2 *>(bias + 32 * (s >> 1) + 8 * (i >> 2) + 4 * h + (i & 3));
-            f32x2 v = f32x2{acc[s >> 1][i], acc[s >> 1][i + 1]} + bb;
-            if (RESID)
-                v += f32x2{bf_lo(res[4 * s + q]), bf_hi(res[4 * s + q])};
-            // ReLU on the packed bf16 pair as signed int16 (negative bf16 <=> negative int16)
-            const i16x2 p = __builtin_bit_cast(i16x2, __builtin_convertvector(v, bf16x2_t));   // one v_cvt_pk_bf16_f32
-            act[4 * s + q] = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(p, i16x2{0, 0}));
+            acc[p] = mfma(A, as_b(x[p + 4 * DR + DC][c]), acc[p]);
         }
+    }
 }
 
-// One conv layer: k-chunk by k-chunk, the column-shifted copies x[p-1] (zero on the left edge),
-// x[p], x[p+1] (zero on the right edge) of every group are built once and each of the 9 taps
-// is then a single DPP row shift by 4dr; then the epilogue (bias, optional residual, ReLU,
-// bf16) per group. act[g] is the layer's input and output; SAVE keeps the input in res[g] for
-// the block's skip connection. act[g][4s + q] = channels of row tile s >> 1, accumulator
-// registers 8(s & 1) + 2q, +1.
-// The edge masks are applied as AND with a 0 / all-ones lane mask, never as a select around the
-// DPP: the compiler lowers `edge ? 0 : dpp(x)` to an EXEC-masked DPP move, and a DPP read from a
-// lane disabled in EXEC returns 0 -- interior cells would lose their edge neighbours.
-template <int NCH, bool RESID, bool SAVE>
-__device__ __forceinline__ void layer(const uint4 *wl, const float *bias, uint32_t (&act)[G][16],
-                                      uint32_t (&res)[G][16], f32x16 (&acc)[G][2], int lane, int h, uint32_t keep_l,
-                                      uint32_t keep_r)
+// row tile O of a layer: accumulators start at bias (+ the residual held in out), the centre tap
+// (all 16 cells) first, then the 8 border taps; epilogue relu -> bf16 into out's tile-O slots
+// `mid` runs between the MFMAs and the epilogue (the last tile of a layer passes the next layer's
+// barrier + weight prefetch there, so this epilogue's VALU shares a scheduling region with the
+// next layer's first MFMAs, which read only k-chunk 0 = row tiles 0 and 1)
+template <int NC, bool RESID, bool OUT_A, int O, typename Mid>
+__device__ __forceinline__ void row_tile(const uint4 *wl, const float *bias, const uint32_t (&x)[16][NC][4],
+                                         uint32_t (&out)[16][2][4], const bf16x8 (&ident)[2], int lane, Mid &&mid)
 {
+    const int g = lane >> 4;
+    const f32x4 b4 = *reinterpret_cast<const f32x4 *>(bias + 16 * O + 4 * g);
+    constexpr int s = O >> 1, w = 2 * (O & 1);
+    f32x4 acc[16];
+    {
+        // accumulators start at the bias (MFMA C operand); a block's second conv first adds its
+        // input (held in out) through the identity fragment
+        const bf16x8 A = lds_frag(wl, (4 * 4 + O) * NC, lane);
 #pragma unroll
-    for (int g = 0; g < G; g++)
-        acc[g][0] = acc[g][1] = f32x16{};
-#pragma unroll
-    for (int s = 0; s < NCH - 1; s++) {
-        uint32_t xs[G][3][4];
-#pragma unroll
-        for (int g = 0; g < G; g++)
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const uint32_t x = act[g][4 * s + q];
-                xs[g][0][q] = cell_shift<-1>(x) & keep_l;   // cell p - 1, zero on the left edge
-                xs[g][1][q] = x;
-                xs[g][2][q] = cell_shift<1>(x) & keep_r;    // cell p + 1, zero on the right edge
-            }
-        tap_mfma<-1, -1, NCH>(wl, s, xs, acc, lane);
-        tap_mfma<-1, 0, NCH>(wl, s, xs, acc, lane);
-        tap_mfma<-1, 1, NCH>(wl, s, xs, acc, lane);
-        tap_mfma<0, -1, NCH>(wl, s, xs, acc, lane);
-        tap_mfma<0, 0, NCH>(wl, s, xs, acc, lane);
-        tap_mfma<0, 1, NCH>(wl, s, xs, acc, lane);
-        tap_mfma<1, -1, NCH>(wl, s, xs, acc, lane);
-        tap_mfma<1, 0, NCH>(wl, s, xs, acc, lane);
-        tap_mfma<1, 1, NCH>(wl, s, xs, acc, lane);
-    }
-    // last k-chunk group by group, each group's epilogue right behind its last MFMAs so the
-    // scheduler can run it under the next group's MFMAs
-    constexpr int s = NCH - 1;
-#pragma unroll
-    for (int g = 0; g < G; g++) {
-        uint32_t xs[3][4];
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const uint32_t x = act[g][4 * s + q];
-            xs[0][q] = cell_shift<-1>(x) & keep_l;
-            xs[1][q] = x;
-            xs[2][q] = cell_shift<1>(x) & keep_r;
+        for (int p = 0; p < 16; p++) {
+            const f32x4 init = RESID ? mfma(ident[O & 1], as_b(out[p][s]), b4) : b4;
+            acc[p] = mfma(A, as_b(x[p][0]), init);
         }
-        tap_mfma1<-1, -1, NCH>(wl, s, xs, acc[g][0], acc[g][1], lane);
-        tap_mfma1<-1, 0, NCH>(wl, s, xs, acc[g][0], acc[g][1], lane);
-        tap_mfma1<-1, 1, NCH>(wl, s, xs, acc[g][0], acc[g][1], lane);
-        tap_mfma1<0, -1, NCH>(wl, s, xs, acc[g][0], acc[g][1], lane);
-        tap_mfma1<0, 0, NCH>(wl, s, xs, acc[g][0], acc[g][1], lane);
-        tap_mfma1<0, 1, NCH>(wl, s, xs, acc[g][0], acc[g][1], lane);
-        tap_mfma1<1, -1, NCH>(wl, s, xs, acc[g][0], acc[g][1], lane);
-        tap_mfma1<1, 0, NCH>(wl, s, xs, acc[g][0], acc[g][1], lane);
-        tap_mfma1<1, 1, NCH>(wl, s, xs, acc[g][0], acc[g][1], lane);
-        epilogue1<RESID, SAVE>(acc[g], bias, h, act[g], res[g]);
+#pragma unroll
+        for (int c = 1; c < NC; c++) {
+            const bf16x8 A1 = lds_frag(wl, (4 * 4 + O) * NC + c, lane);
+#pragma unroll
+            for (int p = 0; p < 16; p++)
+                acc[p] = mfma(A1, as_b(x[p][c]), acc[p]);
+        }
+    }
+    tap<-1, -1, NC>(wl, O, x, acc, lane);
+    tap<-1, 0, NC>(wl, O, x, acc, lane);
+    tap<-1, 1, NC>(wl, O, x, acc, lane);
+    tap<0, -1, NC>(wl, O, x, acc, lane);
+    tap<0, 1, NC>(wl, O, x, acc, lane);
+    tap<1, -1, NC>(wl, O, x, acc, lane);
+    tap<1, 0, NC>(wl, O, x, acc, lane);
+    tap<1, 1, NC>(wl, O, x, acc, lane);
+    mid();
+#pragma unroll
+    for (int p = 0; p < 16; p++) {
+        const uint32_t lo = relu_pack(acc[p][0], acc[p][1]), hi = relu_pack(acc[p][2], acc[p][3]);
+        out[p][s][w] = OUT_A ? in_agpr(lo) : lo;
+        out[p][s][w + 1] = OUT_A ? in_agpr(hi) : hi;
     }
 }
 
-// LDS-DMA of one layer block (frags x 1 KiB) into an LDS buffer: wave w moves fragments w, w+4, ...
+// one layer from the weight image w; `next` (the next layer's begin) runs before the last
+// tile's epilogue
+template <int NC, bool RESID, bool OUT_A, typename Next>
+__device__ __forceinline__ void layer(const uint4 *const (&w)[2], const uint32_t (&x)[16][NC][4],
+                                      uint32_t (&out)[16][2][4], const bf16x8 (&ident)[2], int lane, Next &&next)
+{
+    const uint4 *wl = w[0];
+    const float *bias = reinterpret_cast<const float *>(w[1] + 9 * 4 * NC * 64);
+    auto none = [] {};
+    row_tile<NC, RESID, OUT_A, 0>(wl, bias, x, out, ident, lane, none);
+    row_tile<NC, RESID, OUT_A, 1>(wl, bias, x, out, ident, lane, none);
+    row_tile<NC, RESID, OUT_A, 2>(wl, bias, x, out, ident, lane, none);
+    row_tile<NC, RESID, OUT_A, 3>(wl, bias, x, out, ident, lane, next);
+}
+
+// LDS-DMA of one weight block (frags x 1 KiB): wave w moves fragments w, w + 4, ...
 __device__ __forceinline__ void stage_block(const uint4 *src, uint4 *dst, int frags, int wave, int lane)
 {
     for (int f = wave; f < frags; f += kWaves)
@@ -245,195 +203,167 @@ __device__ __forceinline__ void stage_block(const uint4 *src, uint4 *dst, int fr
                                          (__attribute__((address_space(3))) void *)(dst + f * 64), 16, 0, 0);
 }
 
-__device__ __forceinline__ float row16_sum(float x)
+__device__ __forceinline__ void stage(const uint4 *blob, int blk, uint4 *dst, int wave, int lane)
 {
-    // sum over the 16 lanes of a DPP row: quad pairs, quads, half-rows, rows
-    x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0xB1, 0xF, 0xF, false));   // quad_perm 1,0,3,2
-    x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x4E, 0xF, 0xF, false));   // quad_perm 2,3,0,1
-    x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x141, 0xF, 0xF, false));  // row_half_mirror
-    x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x140, 0xF, 0xF, false));  // row_mirror
-    return x;
+    // blk 0 = stem, 1..8 = conv1..8, 9 = head
+    if (blk == 0)
+        stage_block(blob, dst, kStemBlock, wave, lane);
+    else if (blk <= kConvLayers)
+        stage_block(blob + (kStemBlock + (blk - 1) * kConvBlock) * 64, dst, kConvBlock, wave, lane);
+    else
+        stage_block(blob + kHeadOff * 64, dst, kHeadBlock, wave, lane);
 }
 
 __global__ __launch_bounds__(kThreads, 1) void k_resnet_q(const int8_t *__restrict__ boards, int64_t n,
-                                                         const uint4 *__restrict__ blob,
-                                                         const uint4 *__restrict__ head_w,
-                                                         const float *__restrict__ head_b, float *__restrict__ q_out,
-                                                         int8_t *__restrict__ actions, float eps, uint32_t k0,
-                                                         uint32_t k1, int64_t gid0, uint32_t ctr)
+                                                          const uint4 *__restrict__ blob, float *__restrict__ q_out,
+                                                          int8_t *__restrict__ actions, float eps, uint32_t k0,
+                                                          uint32_t k1, int64_t gid0, uint32_t ctr)
 {
-    extern __shared__ uint4 lds[];                  // [2][kBufFrags * 64] weights | head [kHeadBf16 / 8]
+    extern __shared__ uint4 lds[];                  // [2][kBufFrags * 64]
     auto buf = [](int i) { return lds + i * (kBufFrags * 64); };
-    const uint16_t *head_lds = reinterpret_cast<const uint16_t *>(lds + 2 * kBufFrags * 64);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int h = lane >> 5, cell = lane & 15;
-    const uint32_t keep_l = (lane & 3) == 0 ? 0u : ~0u, keep_r = (lane & 3) == 3 ? 0u : ~0u;
+    const int g = lane >> 4;
     const int64_t tiles = (n + kBoardsPerTile - 1) / kBoardsPerTile;
-
-    // head weights once per workgroup; first stem block into buffer 0
-    for (int i = threadIdx.x; i < kHeadBf16 / 8; i += kThreads)
-        lds[2 * kBufFrags * 64 + i] = head_w[i];
     int cur = 0;
     if ((int64_t)blockIdx.x < tiles)
-        stage_block(blob, buf(0), kStemBlock, wave, lane);
-    const float hb0 = head_b[0], hb1 = head_b[1], hb2 = head_b[2], hb3 = head_b[3];
+        stage(blob, 0, buf(0), wave, lane);
 
-    uint32_t act[G][16], res[G][16];
-    f32x16 acc[G][2];
+    uint32_t h[16][2][4], y[16][2][4];
+    const bf16x8 ident[2] = {identity_frag(0, lane), identity_frag(1, lane)};
     for (int64_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
-        const int64_t b0 = tile * kBoardsPerTile + wave * (2 * G);
-        // cell exponents of this wave's 8 boards (one byte per lane and group)
-        uint32_t e[G];
+        const int64_t b = tile * kBoardsPerTile + wave * 16 + (lane & 15);
+        uint4 bd = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);   // past n: no plane set
+        if (b < n)
+            bd = reinterpret_cast<const uint4 *>(boards)[b];
+        const uint32_t bw[4] = {bd.x, bd.y, bd.z, bd.w};
+        // one-hot stem input: cell q, element j of the lane's k slots = plane 8g + j
+        uint32_t oh[16][1][4];
 #pragma unroll
-        for (int g = 0; g < G; g++) {
-            const int64_t b = b0 + 2 * g + ((lane & 31) >> 4);
-            e[g] = b < n ? (uint32_t)(uint8_t)boards[16 * b + cell] : 0xFFu;
+        for (int q = 0; q < 16; q++) {
+            const uint32_t d = ((bw[q >> 2] >> (8 * (q & 3))) & 0xFFu) - (uint32_t)(8 * g);
+            const uint32_t one = 0x3F80u << (16 * (d & 1u));
+#pragma unroll
+            for (int r = 0; r < 4; r++)
+                oh[q][0][r] = (d < 8u && (d >> 1) == (uint32_t)r) ? one : 0u;
         }
-        // one-hot B registers of the stem: k-chunk s, element j of half h = plane 16s + 8h + j
-#pragma unroll
-        for (int g = 0; g < G; g++)
-#pragma unroll
-            for (int s = 0; s < 2; s++) {
-                const uint32_t d = e[g] - (uint32_t)(16 * s + 8 * h);
-                const uint32_t one = 0x3F80u << (16 * (d & 1u));
-#pragma unroll
-                for (int q = 0; q < 4; q++)
-                    act[g][4 * s + q] = (d < 8u && (d >> 1) == (uint32_t)q) ? one : 0u;
-            }
-        // ---- stem: its block landed (own DMA + barrier); prefetch conv1 into the other buffer
-        __builtin_amdgcn_s_waitcnt(0);                 // vmcnt(0) lgkmcnt(0): this wave's DMA done
-        __syncthreads();
-        stage_block(blob + kStemBlock * 64, buf(cur ^ 1), kConvBlock, wave, lane);
-        layer<2, false, false>(buf(cur), reinterpret_cast<const float *>(buf(cur) + kStemFrags * 64), act, res, acc,
-                               lane, h, keep_l, keep_r);
-        // ---- 8 convs = 4 basic blocks
-        for (int L = 0; L < kConvLayers; ++L) {
-            cur ^= 1;
-            if (R48_RN_ABL != 1 && R48_RN_ABL != 2) {
-                __builtin_amdgcn_s_waitcnt(0);
-                __syncthreads();
-            }
-            // prefetch the next layer, or the next tile's stem
-            if (R48_RN_ABL == 2) {
-            } else if (L + 1 < kConvLayers)
-                stage_block(blob + (kStemBlock + (L + 1) * kConvBlock) * 64, buf(cur ^ 1), kConvBlock, wave, lane);
+        // weight block blk landed in buf(cur) (own DMA + barrier); the next block (or the next
+        // tile's stem) goes into the other buffer, which every wave has finished reading
+        // -> {the lane's 16 B in the image, the image base}. The lane offset is hidden from the
+        // optimiser per layer, so each fragment read is one ds_read_b128 at an immediate offset
+        // from it, instead of per-fragment addresses hoisted out of the tile loop (and spilled)
+        auto begin = [&](int blk, const uint4 *(&w)[2]) {
+            __builtin_amdgcn_s_waitcnt(0);
+            __syncthreads();
+            if (blk + 1 < kConvLayers + 2)
+                stage(blob, blk + 1, buf(cur ^ 1), wave, lane);
             else if (tile + gridDim.x < tiles)
-                stage_block(blob, buf(cur ^ 1), kStemBlock, wave, lane);
-            const float *bias = reinterpret_cast<const float *>(buf(cur) + kConvFrags * 64);
-            if ((L & 1) == 0)                        // first conv of a block: keep its input for the skip
-                layer<4, false, true>(buf(cur), bias, act, res, acc, lane, h, keep_l, keep_r);
-            else
-                layer<4, true, false>(buf(cur), bias, act, res, acc, lane, h, keep_l, keep_r);
+                stage(blob, 0, buf(cur ^ 1), wave, lane);
+            int idx = cur * (kBufFrags * 64) + lane;
+            asm volatile("" : "+v"(idx));
+            w[0] = lds + idx;
+            w[1] = buf(cur);
+            cur ^= 1;
+        };
+        const uint4 *w[2];
+        begin(0, w);
+        layer<1, false, true>(w, oh, h, ident, lane, [&] { begin(1, w); });
+        for (int blk = 0; blk < kConvLayers / 2; blk++) {
+            // first conv of a block: h stays as the skip; second conv: bias + skip, output over h
+            layer<2, false, false>(w, h, y, ident, lane, [&] { begin(2 + 2 * blk, w); });
+            layer<2, true, true>(w, y, h, ident, lane, [&] { begin(3 + 2 * blk, w); });
         }
-        // ---- head: per-lane partial dot products over the lane's 32 channels, then sum over the
-        // 16 cells (DPP row) and the two halves
-        const uint16_t *hw = head_lds + (cell * 2 + h) * 4 * 32;
+        {
+            // head (its weights were begun inside the last conv): Q rows = actions (fragment
+            // rows >= 4 are zero), columns = the 16 boards
+            f32x4 qa = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int g = 0; g < G; g++) {
-            float part[4] = {0.f, 0.f, 0.f, 0.f};
+            for (int p = 0; p < 16; p++)
 #pragma unroll
-            for (int k = 0; k < 16; k++) {
-                const float lo = bf_lo(act[g][k]), hi = bf_hi(act[g][k]);
-#pragma unroll
-                for (int a = 0; a < 4; a++) {
-                    part[a] += lo * __uint_as_float((uint32_t)hw[a * 32 + 2 * k] << 16);
-                    part[a] += hi * __uint_as_float((uint32_t)hw[a * 32 + 2 * k + 1] << 16);
-                }
-            }
-            float qv[4];
-#pragma unroll
-            for (int a = 0; a < 4; a++) {
-                const float r = row16_sum(part[a]);
-                qv[a] = r + __shfl_xor(r, 32);
-            }
-            const int64_t b = b0 + 2 * g + ((lane & 31) >> 4);
-            if (lane < 32 && cell == 0 && b < n) {
-                const float4 q = make_float4(qv[0] + hb0, qv[1] + hb1, qv[2] + hb2, qv[3] + hb3);
+                for (int c = 0; c < 2; c++)
+                    qa = mfma(lds_frag(w[0], 2 * p + c, lane), as_b(h[p][c]), qa);
+            const float *hb = reinterpret_cast<const float *>(w[1] + 32 * 64);
+            if (g == 0 && b < n) {
+                const float4 qv = make_float4(qa[0] + hb[0], qa[1] + hb[1], qa[2] + hb[2], qa[3] + hb[3]);
                 if (q_out)
-                    reinterpret_cast<float4 *>(q_out)[b] = q;
+                    reinterpret_cast<float4 *>(q_out)[b] = qv;
                 if (actions) {
                     const uint64_t gid = (uint64_t)(gid0 + b);
-                    uint32_t w[4] = {(uint32_t)gid, (uint32_t)(gid >> 32), ctr, kEgreedyTag};
-                    r48::philox4x32_10(w, k0, k1);
-                    const float u = (float)(w[0] >> 8) * (1.0f / 16777216.0f);
+                    uint32_t wv[4] = {(uint32_t)gid, (uint32_t)(gid >> 32), ctr, kEgreedyTag};
+                    r48::philox4x32_10(wv, k0, k1);
+                    const float u = (float)(wv[0] >> 8) * (1.0f / 16777216.0f);
                     uint32_t am = 0;
-                    float mx = q.x;
-                    if (q.y > mx) { mx = q.y; am = 1; }
-                    if (q.z > mx) { mx = q.z; am = 2; }
-                    if (q.w > mx) { am = 3; }
-                    actions[b] = (int8_t)(u < eps ? (w[1] >> 30) : am);
+                    float mx = qv.x;
+                    if (qv.y > mx) { mx = qv.y; am = 1; }
+                    if (qv.z > mx) { mx = qv.z; am = 2; }
+                    if (qv.w > mx) { am = 3; }
+                    actions[b] = (int8_t)(u < eps ? (wv[1] >> 30) : am);
                 }
             }
         }
-        cur ^= 1;                                      // the next tile's stem was staged into the other buffer
     }
     __builtin_amdgcn_s_waitcnt(0);                     // no DMA left in flight at exit
 }
 
-// ---- weight packing for k_resnet_q (rein48_amd/dqn/fused.py pack_resnet, one launch instead of ~50
-// PyTorch ops per repack). ptr[6 L + {0..5}] = conv L's weight [co][ci][3][3], bias [co], BN gamma,
-// beta, running mean, running var (gamma NULL: no BN); ptr[54], ptr[55] = head weight [4][1024],
-// bias [4]. Folding as ResNet10Q.folded(): s = gamma / sqrt(var + eps), w s, (b - mean) s + beta,
-// in f32 with correctly rounded sqrt and division, then bf16 (RNE): the layout is exactly the
-// PyTorch packing's; the BN scale may differ from PyTorch's in the last f32 ulp (tests/test_dqn_gpu.py).
+// ---- packing (BN fold + fragment layout), one thread per bf16 of the blob. ptr[6 L + {0..5}] =
+// conv L's weight [co][ci][3][3], bias [co], BN gamma, beta, running mean, running var (gamma
+// NULL: no BN); ptr[54], ptr[55] = head weight [4][1024], bias [4]. Folding as
+// ResNet10Q.folded(): s = gamma / sqrt(var + eps), w s, (b - mean) s + beta (f32, correctly rounded).
 __device__ __forceinline__ float bn_scale(const float *const *p, int L, int co, float eps)
 {
-    const float *g = p[6 * L + 2];
-    return g ? __fdiv_rn(g[co], __fsqrt_rn(__fadd_rn(p[6 * L + 5][co], eps))) : 1.0f;
+    const float *gm = p[6 * L + 2];
+    return gm ? __fdiv_rn(gm[co], __fsqrt_rn(__fadd_rn(p[6 * L + 5][co], eps))) : 1.0f;
+}
+
+__device__ __forceinline__ float folded_bias(const float *const *p, int L, int co, float eps)
+{
+    const float b = p[6 * L + 1][co];
+    return p[6 * L + 2] ? __fadd_rn(__fmul_rn(__fsub_rn(b, p[6 * L + 4][co]), bn_scale(p, L, co, eps)), p[6 * L + 3][co])
+                        : b;
 }
 
 __global__ __launch_bounds__(256) void k_resnet_pack(const float *const *__restrict__ p, float eps,
-                                                      uint16_t *__restrict__ blob, uint16_t *__restrict__ head_w,
-                                                      float *__restrict__ head_b)
+                                                       uint16_t *__restrict__ blob)
 {
-    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;     // bf16 element of the blob
-    constexpr int64_t kBlobElems = (int64_t)kBlobFrags * 512;
-    if (e < kBlobElems) {
-        const int frag = (int)(e / 512), lane = (int)(e % 512) / 8, j = (int)(e % 8);
-        const int r = lane & 31, h = lane >> 5;
-        int L, f, nch, ci_n;
-        if (frag < kStemBlock) {
-            L = 0, f = frag, nch = 2, ci_n = 18;
-        } else {
-            L = 1 + (frag - kStemBlock) / kConvBlock, f = (frag - kStemBlock) % kConvBlock, nch = 4, ci_n = 64;
-        }
-        const int nfrag = 9 * nch * 2;
-        uint16_t out;
-        if (f == nfrag) {   // bias fragment: 64 f32 (folded bias) then zeros, as bf16 pairs
-            const int word = (int)(e % 512) / 2, half = (int)(e % 2);
-            float v = 0.0f;
-            if (word < 64) {
-                const float sc = bn_scale(p, L, word, eps);
-                const float b = p[6 * L + 1][word];
-                // separate correctly rounded ops, as PyTorch's two elementwise kernels (no FMA)
-                v = p[6 * L + 2] ? __fadd_rn(__fmul_rn(__fsub_rn(b, p[6 * L + 4][word]), sc), p[6 * L + 3][word]) : b;
-            }
-            out = (uint16_t)(__float_as_uint(v) >> (16 * half));
-        } else {
-            const int m = f & 1, sk = (f >> 1) % nch, t = (f >> 1) / nch;
-            const int co = 32 * m + r;
-            const int ci = nch == 2 ? 16 * sk + 8 * h + j : 16 * sk + 8 * (j >> 2) + 4 * h + (j & 3);
-            float v = 0.0f;
-            if (ci < ci_n)
-                v = __fmul_rn(p[6 * L][((int64_t)co * ci_n + ci) * 9 + t], bn_scale(p, L, co, eps));
-            const __bf16 bv = (__bf16)v;
-            out = __builtin_bit_cast(uint16_t, bv);
-        }
-        blob[e] = out;
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= (int64_t)kBlobFrags * 512)
         return;
+    const int frag = (int)(e >> 9), within = (int)(e & 511), lane = within >> 3, j = within & 7;
+    const int r = lane & 15, g = lane >> 4;
+    int kind, L, f;        // kind 0 stem, 1 conv, 2 head
+    if (frag < kStemBlock)
+        kind = 0, L = 0, f = frag;
+    else if (frag < kHeadOff)
+        kind = 1, L = 1 + (frag - kStemBlock) / kConvBlock, f = (frag - kStemBlock) % kConvBlock;
+    else
+        kind = 2, L = 9, f = frag - kHeadOff;
+    const int nfrag = kind == 0 ? 36 : kind == 1 ? 72 : 32;
+    uint16_t out;
+    if (f == nfrag) {      // bias fragment: f32 words (64 channels, or 4 head biases), zero padded
+        const int word = within >> 1, half = within & 1;
+        float v = 0.0f;
+        if (kind == 2 && word < 4)
+            v = p[55][word];
+        else if (kind != 2 && word < 64)
+            v = folded_bias(p, L, word, eps);
+        out = (uint16_t)(__float_as_uint(v) >> (16 * half));
+    } else {
+        const int ci = 16 * (2 * (f & 1) + (j >> 2)) + 4 * g + (j & 3);   // conv / head k order
+        float v = 0.0f;
+        if (kind == 0) {
+            const int t = f >> 2, o = f & 3, co = 16 * o + r, plane = 8 * g + j;
+            if (plane < 18)
+                v = __fmul_rn(p[0][((int64_t)co * 18 + plane) * 9 + t], bn_scale(p, 0, co, eps));
+        } else if (kind == 1) {
+            const int t = f >> 3, o = (f >> 1) & 3, co = 16 * o + r;
+            v = __fmul_rn(p[6 * L][((int64_t)co * 64 + ci) * 9 + t], bn_scale(p, L, co, eps));
+        } else {
+            const int cell = f >> 1;
+            if (r < 4)
+                v = p[54][r * 1024 + cell * 64 + ci];
+        }
+        out = __builtin_bit_cast(uint16_t, (__bf16)v);
     }
-    const int64_t k = e - kBlobElems;                                 // head weight element
-    if (k < kHeadBf16) {
-        const int cell = (int)(k / 256), hh = (int)(k / 128) % 2, a = (int)(k / 32) % 4, idx = (int)(k % 32);
-        const int kk = idx >> 1, ee = idx & 1, sq = kk >> 2, q = kk & 3, m = sq >> 1;
-        const int i = 8 * (sq & 1) + 2 * q + ee;
-        const int ci = 32 * m + 8 * (i >> 2) + 4 * hh + (i & 3);
-        const __bf16 bv = (__bf16)p[54][a * 1024 + cell * 64 + ci];
-        head_w[k] = __builtin_bit_cast(uint16_t, bv);
-        return;
-    }
-    if (k - kHeadBf16 < 4)
-        head_b[k - kHeadBf16] = p[55][k - kHeadBf16];
+    blob[e] = out;
 }
 
 int fail(int code, const char *msg)
@@ -446,13 +376,13 @@ int fail(int code, const char *msg)
 
 extern "C" {
 
-int r48_resnet_q_forward(const int8_t *boards, int64_t n, const void *wblob, const void *head_w, const float *head_b,
-                         float *q, int8_t *actions, float eps, uint64_t seed, int64_t gid0, uint32_t ctr, void *stream)
+int r48_resnet_q_forward(const int8_t *boards, int64_t n, const void *wblob, float *q, int8_t *actions, float eps,
+                          uint64_t seed, int64_t gid0, uint32_t ctr, void *stream)
 {
-    if (!boards || !wblob || !head_w || !head_b || n < 0 || gid0 < 0 || (!q && !actions))
+    if (!boards || !wblob || n < 0 || gid0 < 0 || (!q && !actions))
         return fail(R48_EINVAL, "NULL argument, n/gid0 < 0, or neither q nor actions requested");
-    if (((uintptr_t)wblob & 15u) || ((uintptr_t)head_w & 15u) || (q && ((uintptr_t)q & 15u)))
-        return fail(R48_EINVAL, "wblob, head_w and q must be 16-byte aligned");
+    if (((uintptr_t)wblob & 15u) || ((uintptr_t)boards & 15u) || (q && ((uintptr_t)q & 15u)))
+        return fail(R48_EINVAL, "boards, wblob and q must be 16-byte aligned");
     if (n == 0)
         return R48_OK;
     int dev = 0, cus = 0;
@@ -461,7 +391,7 @@ int r48_resnet_q_forward(const int8_t *boards, int64_t n, const void *wblob, con
         cus = 256;
     const int64_t tiles = (n + kBoardsPerTile - 1) / kBoardsPerTile;
     const int grid = (int)(tiles < cus ? tiles : cus);
-    const size_t lds = (size_t)(2 * kBufFrags * 64) * 16 + kHeadBf16 * 2;
+    const size_t lds = (size_t)(2 * kBufFrags * 64) * 16;
     static bool attr_set = false;
     if (!attr_set) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_resnet_q),
@@ -469,8 +399,8 @@ int r48_resnet_q_forward(const int8_t *boards, int64_t n, const void *wblob, con
         attr_set = true;
     }
     hipLaunchKernelGGL(k_resnet_q, dim3(grid), dim3(kThreads), lds, (hipStream_t)stream, boards, n,
-                       reinterpret_cast<const uint4 *>(wblob), reinterpret_cast<const uint4 *>(head_w), head_b, q,
-                       actions, eps, (uint32_t)seed, (uint32_t)(seed >> 32), gid0, ctr);
+                       reinterpret_cast<const uint4 *>(wblob), q, actions, eps, (uint32_t)seed,
+                       (uint32_t)(seed >> 32), gid0, ctr);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         r48::set_last_error(std::string("k_resnet_q: ") + hipGetErrorString(e));
@@ -481,13 +411,13 @@ int r48_resnet_q_forward(const int8_t *boards, int64_t n, const void *wblob, con
 
 int64_t r48_resnet_q_blob_bytes(void) { return (int64_t)kBlobFrags * 1024; }
 
-int r48_resnet_pack(const float *const *ptrs, float bn_eps, void *wblob, void *head_w, float *head_b, void *stream)
+int r48_resnet_pack(const float *const *ptrs, float bn_eps, void *wblob, void *stream)
 {
-    if (!ptrs || !wblob || !head_w || !head_b || ((uintptr_t)wblob & 15u) || ((uintptr_t)head_w & 15u))
+    if (!ptrs || !wblob || ((uintptr_t)wblob & 15u))
         return fail(R48_EINVAL, "r48_resnet_pack: NULL or misaligned argument");
-    const int64_t total = (int64_t)kBlobFrags * 512 + kHeadBf16 + 4;
+    const int64_t total = (int64_t)kBlobFrags * 512;
     hipLaunchKernelGGL(k_resnet_pack, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream, ptrs,
-                       bn_eps, (uint16_t *)wblob, (uint16_t *)head_w, head_b);
+                       bn_eps, (uint16_t *)wblob);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         r48::set_last_error(std::string("k_resnet_pack: ") + hipGetErrorString(e));

@@ -125,16 +125,16 @@ def test_dqn_bf16_resnet10_trains():
         assert torch.equal(a, b)                                     # synced after update 4
 
 
-@pytest.mark.parametrize("kernel", ["dpp", "cell"])
+@pytest.mark.parametrize("pack", ["host", "gpu"])
 @pytest.mark.parametrize("empty_frac", [0.4, 0.9])
-def test_fused_resnet_matches_torch(empty_frac, kernel):
-    """The fused kernels (bf16 MFMA, activations in registers, eval-mode BN folded) vs the
-    PyTorch ResNet10Q: "dpp" = r48_resnet_q_forward (32x32x16, taps as DPP row shifts), "cell" =
-    r48_resnet2_q_forward (16x16x32, columns = boards of one cell, in-grid taps only). Error
-    metric: max |got - ref| / (|ref| + mean|ref|). Against fp32 the kernel's error is within 1.5x
-    (+1e-3) of PyTorch's own bf16 forward's error and below 5e-2; the fused epsilon-greedy draw
-    equals r48_egreedy_actions on the kernel's own Q."""
-    from rein48_amd.dqn.fused import pack_resnet, pack_resnet2_gpu, resnet2_q_forward, resnet_q_forward
+def test_fused_resnet_matches_torch(empty_frac, pack):
+    """r48_resnet_q_forward (bf16 16x16x32 MFMA, columns = 16 boards of one cell, in-grid taps
+    only, activations in registers, eval-mode BN folded; weights packed by pack_resnet or
+    r48_resnet_pack) vs the PyTorch ResNet10Q. Error metric: max |got - ref| / (|ref| +
+    mean|ref|). Against fp32 the kernel's error is within 1.5x (+1e-3) of PyTorch's own bf16
+    forward's error and below 5e-2; the fused epsilon-greedy draw equals r48_egreedy_actions on
+    the kernel's own Q."""
+    from rein48_amd.dqn.fused import pack_resnet, pack_resnet_gpu, resnet_q_forward
     from rein48_amd.dqn.kernels import board_onehot, egreedy_actions
     from rein48_amd.dqn.nets import ResNet10Q
     torch.manual_seed(5)
@@ -156,12 +156,8 @@ def test_fused_resnet_matches_torch(empty_frac, kernel):
     b[:5] = np.arange(16, dtype=np.int8)[None] % 18  # every plane incl. 15, and one 17-tile board
     b[5, 3] = 17
     bt = torch.from_numpy(b).to(DEV)
-    if kernel == "dpp":
-        packed = pack_resnet(net)
-        fwd = resnet_q_forward
-    else:
-        packed = pack_resnet2_gpu(net)
-        fwd = resnet2_q_forward
+    packed = pack_resnet(net) if pack == "host" else pack_resnet_gpu(net)
+    fwd = resnet_q_forward
     q, _ = fwd(bt, packed)
     with torch.no_grad():
         ref32 = net(board_onehot(bt, dtype=torch.float32))
@@ -313,59 +309,13 @@ def test_structured_conv_weight_kernels_match_cpu_map(ci):
 
 @pytest.mark.parametrize("bn", [True, False])
 def test_gpu_weight_packing_equals_pack_resnet(bn):
-    """r48_resnet_pack (one launch: BN fold, bf16 fragments, head layout) == the PyTorch
+    """r48_resnet_pack (one launch: BN fold, 16x16x32 fragments incl. the head) == the PyTorch
     pack_resnet. The layout is exact (without BN: bit for bit); with BN the scale gamma /
     sqrt(var + eps) may differ from PyTorch's in the last f32 ulp (its division / sqrt kernels
     are not guaranteed correctly rounded), so the folded f32 biases agree to 1e-6 relative and the
-    bf16 weights to one bf16 ulp on < 0.1 % of elements. Repacking into the same buffers after a
+    bf16 weights to one bf16 ulp on < 0.1 % of elements. Repacking into the same buffer after a
     weight change tracks it."""
     from rein48_amd.dqn.fused import pack_resnet, pack_resnet_gpu
-    from rein48_amd.dqn.nets import ResNet10Q
-    torch.manual_seed(11)
-    net = ResNet10Q(bn=bn).to(DEV).eval()
-    with torch.no_grad():
-        if bn:
-            for m in net.bns:
-                m.running_mean.uniform_(-0.3, 0.3)
-                m.running_var.uniform_(0.5, 2.0)
-                m.weight.uniform_(0.5, 1.5)
-                m.bias.uniform_(-0.2, 0.2)
-        for c in net.conv_layers():
-            c.bias.uniform_(-0.2, 0.2)
-        net.head.bias.uniform_(-1, 1)
-
-    def check(got, want):
-        g16, w16 = got[0].view(torch.int16).long(), want[0].view(torch.int16).long()
-        frags = g16.view(-1, 512)
-        wf = w16.view(-1, 512)
-        stem, conv = 37, 73
-        bias_rows = [stem - 1] + [stem + conv * L + conv - 1 for L in range(8)]
-        is_bias = torch.zeros(frags.shape[0], dtype=torch.bool, device=DEV)
-        is_bias[bias_rows] = True
-        gw, ww = frags[~is_bias], wf[~is_bias]               # bf16 weight fragments
-        if not bn:
-            assert torch.equal(gw, ww)
-        else:
-            diff = (gw - ww).abs()
-            assert int(diff.max()) <= 1 and float((diff > 0).float().mean()) < 1e-3
-        gb = got[0].view(-1, 512)[is_bias].contiguous().view(torch.float32)   # f32 folded biases
-        wb = want[0].view(-1, 512)[is_bias].contiguous().view(torch.float32)
-        torch.testing.assert_close(gb, wb, rtol=1e-6, atol=1e-7)
-        assert torch.equal(got[1].view(torch.int16), want[1].view(torch.int16)) and torch.equal(got[2], want[2])
-
-    got = pack_resnet_gpu(net)
-    check(got, pack_resnet(net))
-    with torch.no_grad():
-        net.convs[3].weight.mul_(1.5)
-    got = pack_resnet_gpu(net, out=got)
-    check(got, pack_resnet(net))
-
-
-@pytest.mark.parametrize("bn", [True, False])
-def test_gpu_weight_packing_equals_pack_resnet2(bn):
-    """r48_resnet2_pack (one launch: BN fold, 16x16x32 fragments incl. the head) == the PyTorch
-    pack_resnet2, with the same BN-scale ulp allowance as r48_resnet_pack."""
-    from rein48_amd.dqn.fused import pack_resnet2, pack_resnet2_gpu
     from rein48_amd.dqn.nets import ResNet10Q
     torch.manual_seed(12)
     net = ResNet10Q(bn=bn).to(DEV).eval()
@@ -396,9 +346,9 @@ def test_gpu_weight_packing_equals_pack_resnet2(bn):
         wb = want.view(-1, 512)[is_bias].contiguous().view(torch.float32)
         torch.testing.assert_close(gb, wb, rtol=1e-6, atol=1e-7)
 
-    got = pack_resnet2_gpu(net)
-    check(got, pack_resnet2(net))
+    got = pack_resnet_gpu(net)
+    check(got, pack_resnet(net))
     with torch.no_grad():
         net.convs[3].weight.mul_(1.5)
-    got = pack_resnet2_gpu(net, out=got)
-    check(got, pack_resnet2(net))
+    got = pack_resnet_gpu(net, out=got)
+    check(got, pack_resnet(net))

@@ -1,7 +1,8 @@
 """Probe: fused ResNet-10 inference (r48_resnet_q_forward) throughput at 2^21 boards.
 
 Useful FLOPs count only in-grid taps (100 of 144 (cell, tap) pairs); issued MFMA FLOPs count
-every MFMA the kernel runs (all 9 taps, 18 planes padded to 32)."""
+every MFMA the kernel runs (in-grid taps, 18 planes padded to 32, the skip connections as identity
+MFMAs, the head's 4 rows padded to 16)."""
 import json
 import sys
 
@@ -13,7 +14,7 @@ from rein48_amd.dqn.nets import ResNet10Q  # noqa: E402
 
 C = 64
 USEFUL = 2 * 100 * (18 * C + 8 * C * C) + 2 * 16 * C * 4
-ISSUED = 2 * 16 * 9 * (32 * C + 8 * C * C)          # per board: 16 cells x 9 taps x K x N
+ISSUED = 2 * 100 * (32 * C + 8 * C * C) + 2 * 16 * 4 * C * 32 + 2 * 16 * C * 16   # per board
 
 
 def main():
