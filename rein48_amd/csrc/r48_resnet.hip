@@ -10,7 +10,7 @@
 //
 // Cell-grouped tiling (replaced a 32x32x16 kernel with columns = 2 boards x 16 cells and the
 // taps as DPP row shifts: that one issued all 144 (cell, tap) pairs with zero fill and re-read an
-// LDS weight fragment every 4 MFMAs -- 14.8 ms per 2^21 boards against 9.75 ms here):
+// LDS weight fragment every 4 MFMAs -- 14.8 ms per 2^21 boards against 8.9 ms here):
 // v_mfma_f32_16x16x32_bf16 with rows = 16 output channels (four row tiles per 64-channel layer)
 // and columns = 16 BOARDS at the SAME cell. A wave owns 16 boards and keeps all 16 cells of
 // them in registers: x[cell][k-chunk][4] packed bf16, lane l = board l & 15, channel group
@@ -23,11 +23,11 @@
 // packs tiles 2c and 2c+1: element j <-> channel 16(2c + (j >> 2)) + 4g + (j & 3), and the
 // host packs the A fragments with the same k order. Row tiles run one after another, each
 // finishing with its epilogue (bias [+ residual], ReLU, bf16), so only 16 x 4 accumulators are
-// live. A basic block's second conv starts its accumulators from bias + the block input (the
+// live (VGPRs); the activations sit in AGPRs. A basic block's second conv starts its accumulators from bias + the block input (the
 // skip connection) and writes its output over that input.
 // Weights stream per layer (stem 37, conv 73, head 33 fragments of 1 KiB) into a
 // double-buffered LDS image by global_load_lds while the other buffer's layer computes; one
-// persistent workgroup per CU, 4 waves (one per SIMD: ~330 registers per lane), 64 boards per tile.
+// persistent workgroup per CU, 4 waves (one per SIMD: 256 VGPR + 208 AGPR, no scratch), 64 boards per tile.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -104,9 +104,10 @@ __device__ __forceinline__ bf16x8 identity_frag(int odd, int lane)
     return as_b(w);
 }
 
-// a packed activation defined in an AGPR: the block input h lives in the accumulator file (MFMA
-// B operands may be AGPRs; VALU reads get a v_accvgpr_read), y and the temporaries in VGPRs, so
-// h + y (256 registers) do not both compete for the 256 VGPRs
+// a packed activation defined in an AGPR: the layer activations h and y (128 registers each) live
+// in the accumulator file -- they are only ever MFMA B operands, which may be AGPRs -- leaving the
+// VGPRs to the live accumulators, the prefetched weight fragments and addresses (with y in VGPRs
+// the scheduler had no room to read fragments ahead: 9.77 -> 8.89 ms per 2^21 boards)
 __device__ __forceinline__ uint32_t in_agpr(uint32_t v)
 {
     uint32_t r;
@@ -114,30 +115,13 @@ __device__ __forceinline__ uint32_t in_agpr(uint32_t v)
     return r;
 }
 
-// one tap (DR, DC) of row tile o: per k-chunk one LDS fragment, one MFMA per in-grid cell
-template <int DR, int DC, int NC>
-__device__ __forceinline__ void tap(const uint4 *wl, int o, const uint32_t (&x)[16][NC][4], f32x4 (&acc)[16],
-                                    int lane)
-{
-    constexpr int t = (DR + 1) * 3 + (DC + 1);
-#pragma unroll
-    for (int c = 0; c < NC; c++) {
-        const bf16x8 A = lds_frag(wl, (t * 4 + o) * NC + c, lane);
-#pragma unroll
-        for (int p = 0; p < 16; p++) {
-            const int r = p >> 2, cc = p & 3;
-            if (r + DR < 0 || r + DR > 3 || cc + DC < 0 || cc + DC > 3)
-                continue;
-            acc[p] = mfma(A, as_b(x[p + 4 * DR + DC][c]), acc[p]);
-        }
-    }
-}
+// tap order of a row tile: the centre (all 16 cells, starts the accumulators) first
+__device__ constexpr int kTapOrder[9] = {4, 0, 1, 2, 3, 5, 6, 7, 8};
 
-// row tile O of a layer: accumulators start at bias (+ the residual held in out), the centre tap
-// (all 16 cells) first, then the 8 border taps; epilogue relu -> bf16 into out's tile-O slots
-// `mid` runs between the MFMAs and the epilogue (the last tile of a layer passes the next layer's
-// barrier + weight prefetch there, so this epilogue's VALU shares a scheduling region with the
-// next layer's first MFMAs, which read only k-chunk 0 = row tiles 0 and 1)
+// row tile O of a layer: 9 NC fragment groups (tap, k-chunk), each one LDS fragment applied to every
+// in-grid cell of its tap; the next group's fragment is read before this group's MFMAs issue
+// (one group of MFMA time to land). Accumulators start at the bias (+ the skip connection through
+// the identity fragment); `mid` runs between the MFMAs and the epilogue (see layer)
 template <int NC, bool RESID, bool OUT_A, int O, typename Mid>
 __device__ __forceinline__ void row_tile(const uint4 *wl, const float *bias, const uint32_t (&x)[16][NC][4],
                                          uint32_t (&out)[16][2][4], const bf16x8 (&ident)[2], int lane, Mid &&mid)
@@ -145,32 +129,30 @@ __device__ __forceinline__ void row_tile(const uint4 *wl, const float *bias, con
     const int g = lane >> 4;
     const f32x4 b4 = *reinterpret_cast<const f32x4 *>(bias + 16 * O + 4 * g);
     constexpr int s = O >> 1, w = 2 * (O & 1);
+    constexpr int kGroups = 9 * NC;
     f32x4 acc[16];
-    {
-        // accumulators start at the bias (MFMA C operand); a block's second conv first adds its
-        // input (held in out) through the identity fragment
-        const bf16x8 A = lds_frag(wl, (4 * 4 + O) * NC, lane);
+    bf16x8 A = lds_frag(wl, (4 * 4 + O) * NC, lane);
+#pragma unroll
+    for (int k = 0; k < kGroups; k++) {
+        const int t = kTapOrder[k / NC], c = k % NC;
+        bf16x8 An = A;
+        if (k + 1 < kGroups)
+            An = lds_frag(wl, (kTapOrder[(k + 1) / NC] * 4 + O) * NC + (k + 1) % NC, lane);
+        const int DR = t / 3 - 1, DC = t % 3 - 1;
 #pragma unroll
         for (int p = 0; p < 16; p++) {
-            const f32x4 init = RESID ? mfma(ident[O & 1], as_b(out[p][s]), b4) : b4;
-            acc[p] = mfma(A, as_b(x[p][0]), init);
+            const int r = p >> 2, cc = p & 3;
+            if (r + DR < 0 || r + DR > 3 || cc + DC < 0 || cc + DC > 3)
+                continue;
+            if (k == 0) {
+                const f32x4 init = RESID ? mfma(ident[O & 1], as_b(out[p][s]), b4) : b4;
+                acc[p] = mfma(A, as_b(x[p][0]), init);
+            } else {
+                acc[p] = mfma(A, as_b(x[p + 4 * DR + DC][c]), acc[p]);
+            }
         }
-#pragma unroll
-        for (int c = 1; c < NC; c++) {
-            const bf16x8 A1 = lds_frag(wl, (4 * 4 + O) * NC + c, lane);
-#pragma unroll
-            for (int p = 0; p < 16; p++)
-                acc[p] = mfma(A1, as_b(x[p][c]), acc[p]);
-        }
+        A = An;
     }
-    tap<-1, -1, NC>(wl, O, x, acc, lane);
-    tap<-1, 0, NC>(wl, O, x, acc, lane);
-    tap<-1, 1, NC>(wl, O, x, acc, lane);
-    tap<0, -1, NC>(wl, O, x, acc, lane);
-    tap<0, 1, NC>(wl, O, x, acc, lane);
-    tap<1, -1, NC>(wl, O, x, acc, lane);
-    tap<1, 0, NC>(wl, O, x, acc, lane);
-    tap<1, 1, NC>(wl, O, x, acc, lane);
     mid();
 #pragma unroll
     for (int p = 0; p < 16; p++) {
@@ -180,8 +162,6 @@ __device__ __forceinline__ void row_tile(const uint4 *wl, const float *bias, con
     }
 }
 
-// one layer from the weight image w; `next` (the next layer's begin) runs before the last
-// tile's epilogue
 template <int NC, bool RESID, bool OUT_A, typename Next>
 __device__ __forceinline__ void layer(const uint4 *const (&w)[2], const uint32_t (&x)[16][NC][4],
                                       uint32_t (&out)[16][2][4], const bf16x8 (&ident)[2], int lane, Next &&next)
@@ -269,7 +249,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_resnet_q(const int8_t *__restri
         layer<1, false, true>(w, oh, h, ident, lane, [&] { begin(1, w); });
         for (int blk = 0; blk < kConvLayers / 2; blk++) {
             // first conv of a block: h stays as the skip; second conv: bias + skip, output over h
-            layer<2, false, false>(w, h, y, ident, lane, [&] { begin(2 + 2 * blk, w); });
+            layer<2, false, true>(w, h, y, ident, lane, [&] { begin(2 + 2 * blk, w); });
             layer<2, true, true>(w, y, h, ident, lane, [&] { begin(3 + 2 * blk, w); });
         }
         {
