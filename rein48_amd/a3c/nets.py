@@ -28,6 +28,26 @@ import torch.nn.functional as F
 SPLITK_MIN_ROWS = 1 << 16
 
 
+def splitk_weight_grad(gy, x):
+    """gy^T x (the weight gradient of y = x w^T) in fp32 (fp64 for fp64 inputs): for >= 2^16 rows
+    a batched GEMM over row chunks then a sum. bf16 on the GPU: the per-chunk partial products come
+    out of hipBLASLt in fp32 (bmm out_dtype), so no bf16 rounding of partials and no cast pass."""
+    acc = torch.float64 if x.dtype == torch.float64 else torch.float32
+    rows = x.shape[0]
+    f32_out = gy.is_cuda and gy.dtype == torch.bfloat16
+    if rows >= SPLITK_MIN_ROWS:
+        s = min(1024, rows // 8192)
+        main = (rows // s) * s
+        a, b = gy[:main].view(s, -1, gy.shape[1]).transpose(1, 2), x[:main].view(s, -1, x.shape[1])
+        gw = (torch.bmm(a, b, out_dtype=acc) if f32_out else torch.bmm(a, b).to(acc)).sum(0)
+        if main < rows:
+            gw += (gy[main:].t() @ x[main:]).to(acc)
+        return gw
+    if f32_out:
+        return torch.bmm(gy.t()[None], x[None], out_dtype=acc)[0]
+    return (gy.t() @ x).to(acc)
+
+
 class _SplitKLinear(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b):
@@ -40,19 +60,7 @@ class _SplitKLinear(torch.autograd.Function):
         x, w = ctx.saved_tensors
         acc = torch.float64 if x.dtype == torch.float64 else torch.float32  # bf16 partials sum in fp32
         gx = gy @ w
-        rows = x.shape[0]
-        # bf16 on the GPU: the per-chunk partial products come out of hipBLASLt in fp32
-        # (bmm out_dtype), so no bf16 rounding of partials and no cast pass
-        f32_out = gy.is_cuda and gy.dtype == torch.bfloat16
-        if rows >= SPLITK_MIN_ROWS:
-            s = min(1024, rows // 8192)
-            main = (rows // s) * s
-            a, b = gy[:main].view(s, -1, gy.shape[1]).transpose(1, 2), x[:main].view(s, -1, x.shape[1])
-            gw = (torch.bmm(a, b, out_dtype=acc) if f32_out else torch.bmm(a, b).to(acc)).sum(0)
-            if main < rows:
-                gw += (gy[main:].t() @ x[main:]).to(acc)
-        else:
-            gw = (gy.t() @ x).to(acc)
+        gw = splitk_weight_grad(gy, x)
         # fp32 accumulation, no cast copy; skipped when the bias is a constant (needs no grad)
         gb = gy.sum(0, dtype=acc) if ctx.has_bias and ctx.needs_input_grad[2] else None
         return gx, gw.to(w.dtype), (gb.to(w.dtype) if gb is not None else None)
