@@ -394,7 +394,10 @@ def main():
         ex = {}
         for key, fn in (("a3c_config4", lambda: a3c_config3(dev, args.seed, n, world=world)),
                         ("dqn_config5", lambda: dqn_config5(dev, args.seed, 1 << 21, world=world))):
-            ex[key] = fn()
+            try:              # the env bench line must print even if a trainer fails (on every rank alike)
+                ex[key] = fn()
+            except Exception as e:
+                ex[key] = {"error": repr(e)}
         line["extras"] = ex
     if rank == 0:
         print(json.dumps(line), flush=True)
