@@ -23,11 +23,13 @@
 // packs tiles 2c and 2c+1: element j <-> channel 16(2c + (j >> 2)) + 4g + (j & 3), and the
 // host packs the A fragments with the same k order. Row tiles run one after another, each
 // finishing with its epilogue (bias [+ residual], ReLU, bf16), so only 16 x 4 accumulators are
-// live (VGPRs); the activations sit in AGPRs. A basic block's second conv starts its accumulators from bias + the block input (the
-// skip connection) and writes its output over that input.
+// live (VGPRs); the activations sit in AGPRs. A basic block's second conv starts its
+// accumulators from bias + the block input (the skip connection, as an identity MFMA) and writes
+// its output over that input.
 // Weights stream per layer (stem 37, conv 73, head 33 fragments of 1 KiB) into a
 // double-buffered LDS image by global_load_lds while the other buffer's layer computes; one
-// persistent workgroup per CU, 4 waves (one per SIMD: 256 VGPR + 208 AGPR, no scratch), 64 boards per tile.
+// persistent workgroup per CU, 4 waves (one per SIMD: 256 VGPR + 208 AGPR, no scratch), 64
+// boards per tile.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
