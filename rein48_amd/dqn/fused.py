@@ -137,6 +137,8 @@ def resnet_q_forward(boards, blob, q=True, actions=False, eps=0.0, seed=0, ctr=0
     dev = boards.device
     qt = torch.empty((n, 4), dtype=torch.float32, device=dev) if q else None
     at = torch.empty(n, dtype=torch.int8, device=dev) if actions else None
+    if n == 0:                               # empty tensors may have NULL data pointers
+        return qt, at
     check(_lib.load().r48_resnet_q_forward(ptr(boards), n, ptr(blob), ptr(qt), ptr(at), float(eps),
                                            int(seed) & (2 ** 64 - 1), int(gid0), int(ctr) & 0xFFFFFFFF,
                                            C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)))

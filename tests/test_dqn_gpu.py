@@ -352,3 +352,24 @@ def test_gpu_weight_packing_equals_pack_resnet(bn):
         net.convs[3].weight.mul_(1.5)
     got = pack_resnet_gpu(net, out=got)
     check(got, pack_resnet(net))
+
+
+def test_fused_resnet_tile_edges_bit_identical():
+    """Every board's Q is computed in its own MFMA column with a fixed summation order, so the
+    result must not depend on n or on where the board sits in its 64-board tile / persistent
+    loop: Q(boards[:n]) equals Q(boards)[:n] bit for bit at the tile edges (1, 15, 16, 17, 63, 64,
+    65, 257 boards and 256 CUs' worth + 1), and n = 0 launches nothing."""
+    from rein48_amd.dqn.fused import pack_resnet_gpu, resnet_q_forward
+    from rein48_amd.dqn.nets import ResNet10Q
+    torch.manual_seed(31)
+    net = ResNet10Q().to(DEV).eval()
+    with torch.no_grad():
+        net.head.weight.normal_(std=0.05)
+    blob = pack_resnet_gpu(net)
+    b = torch.from_numpy(np.random.default_rng(31).integers(0, 14, size=(40_000, 16)).astype(np.int8)).to(DEV)
+    full, _ = resnet_q_forward(b, blob)
+    for n in (1, 15, 16, 17, 63, 64, 65, 257, 256 * 64 + 1):
+        q, _ = resnet_q_forward(b[:n].contiguous(), blob)
+        assert torch.equal(q.view(torch.int32), full[:n].view(torch.int32)), n
+    q0, a0 = resnet_q_forward(b[:0].contiguous(), blob, actions=True)
+    assert q0.shape == (0, 4) and a0.shape == (0,)
