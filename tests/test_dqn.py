@@ -110,3 +110,48 @@ def test_oracle_td_target_and_huber():
     np.testing.assert_allclose(y2, r + 0.9 * (1 - d) * qt[np.arange(100), qo.argmax(1)])
     x = rng.normal(size=100) * 3
     assert abs(R.huber(x, y) - float(F.smooth_l1_loss(torch.tensor(x), torch.tensor(y)))) < 1e-12
+
+
+def test_fused_kernel_packing_layout_cpu():
+    """pack_resnet (host packing of the fused inference kernel's blob, csrc/r48_resnet.hip) against
+    an element-wise restatement of the 16x16x32 fragment layout: lane l = 16g + r, element j;
+    stem (t, o): W0[16o + r][8g + j][t] (planes >= 18 zero); conv (t, o, c):
+    W[16o + r][16(2c + (j >> 2)) + 4g + (j & 3)][t]; head (p, c): Wh[r][64p + same channel]
+    (rows >= 4 zero); each block closed by its f32 bias fragment. Runs on the CPU."""
+    from rein48_amd.dqn.fused import pack_resnet
+    from rein48_amd.dqn.nets import ResNet10Q
+    torch.manual_seed(3)
+    net = ResNet10Q().eval()
+    with torch.no_grad():
+        for m in net.bns:
+            m.running_mean.uniform_(-0.3, 0.3)
+            m.running_var.uniform_(0.5, 2.0)
+    convs, (hw, hb) = net.folded()
+    blob = pack_resnet(net).view(torch.int16).numpy().reshape(-1, 64, 8)
+    bf = lambda v: torch.tensor(float(v), dtype=torch.float32).to(torch.bfloat16).view(torch.int16).item()
+    rng = np.random.default_rng(0)
+    W0 = convs[0][0].detach().numpy()
+    for _ in range(200):
+        t, o, l, j = rng.integers(9), rng.integers(4), rng.integers(64), rng.integers(8)
+        r, g = l & 15, l >> 4
+        want = W0[16 * o + r, 8 * g + j, t // 3, t % 3] if 8 * g + j < 18 else 0.0
+        assert blob[t * 4 + o, l, j] == bf(want)
+    for L in (1, 5, 8):
+        W = convs[L][0].detach().numpy()
+        base = 37 + (L - 1) * 73
+        for _ in range(200):
+            t, o, c, l, j = rng.integers(9), rng.integers(4), rng.integers(2), rng.integers(64), rng.integers(8)
+            r, g = l & 15, l >> 4
+            ci = 16 * (2 * c + (j >> 2)) + 4 * g + (j & 3)
+            assert blob[base + (t * 4 + o) * 2 + c, l, j] == bf(W[16 * o + r, ci, t // 3, t % 3])
+        bias = pack_resnet(net).view(-1, 512)[base + 72].view(torch.float32)[:64]
+        torch.testing.assert_close(bias, convs[L][1].detach(), rtol=0, atol=0)
+    head = 37 + 8 * 73
+    H = hw.detach().numpy()
+    for _ in range(200):
+        p, c, l, j = rng.integers(16), rng.integers(2), rng.integers(64), rng.integers(8)
+        r, g = l & 15, l >> 4
+        ci = 16 * (2 * c + (j >> 2)) + 4 * g + (j & 3)
+        want = H[r, 64 * p + ci] if r < 4 else 0.0
+        assert blob[head + 2 * p + c, l, j] == bf(want)
+    torch.testing.assert_close(pack_resnet(net).view(-1, 512)[head + 32].view(torch.float32)[:4], hb.detach(), rtol=0, atol=0)
