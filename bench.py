@@ -247,7 +247,7 @@ def traffic_from_profile(n_boards):
     return d.get("hbm_bytes_per_step")
 
 
-SETTLE_S = 0.1   # minimum untimed stepping before a timed region: GPU clocks ramp over ~20 ms+
+SETTLE_S = 0.3   # minimum untimed stepping before a timed region: GPU clocks ramp over ~20 ms+
 
 
 def timed_steps(env, plan, W, chunk, world, dev):
@@ -286,7 +286,7 @@ def timed_steps(env, plan, W, chunk, world, dev):
 def main():
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3000)
+    ap.add_argument("--steps", type=int, default=6000)
     ap.add_argument("--warmup", type=int, default=10000,
                     help="untimed steps; stepping continues untimed until %.0f ms have run (GPU clock ramp)"
                     % (SETTLE_S * 1e3))
