@@ -264,8 +264,6 @@ def timed_steps(env, plan, W, chunk, world, dev):
         while time.perf_counter() - t_w < SETTLE_S:
             env.step_n(chunk, auto_reset=True)
             torch.cuda.synchronize(dev)
-    for c in sorted(set(plan)):
-        env.prepare_step_n(c, auto_reset=True)
     s = torch.cuda.current_stream(dev)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in plan]
     torch.cuda.synchronize(dev)

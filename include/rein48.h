@@ -86,26 +86,14 @@ int r48_env_reset_with_draws(r48_env *env, const uint8_t *mask, const uint8_t *r
 int r48_env_step(r48_env *env, int8_t *actions, uint32_t flags, uint8_t *done, uint8_t *changed,
                  int32_t *reward, int32_t *score, void *stream);
 
-/* n_steps consecutive r48_env_step calls with the same arguments (outputs hold the last
- * step's values), replayed from hipGraphs of n_steps step kernels captured on the first call
- * and cached per (n_steps, flags, buffers). The step counter is read from device memory, so
- * replays advance it exactly like eager calls. Envs of >= 2^18 boards run as two shard chains
- * (the second on an env-owned stream, forked from and joined back into `stream`), so one
- * shard's memory latency overlaps the other's compute. n_steps <= 4096; prefer large chunks
- * (the fork/join costs tens of microseconds per call). One caller stream per env. Envs of more
- * than 2^24 boards (past the Infinity Cache) alternate the steps between the bound array and an
- * env-owned scratch copy of it (read one, write the other; allocated at the first such call,
- * n x 16 B); the last step always writes the bound array, so results are those of in-place
- * steps. */
+/* n_steps consecutive r48_env_step calls with the same arguments (outputs hold the last step's
+ * values; the step counter advances by n_steps) in ONE kernel launch: boards are independent, so
+ * every board stays in registers for all n_steps steps and is written back once, with the last
+ * step's output planes -- bit-identical to n_steps r48_env_step calls, at a fraction of the HBM
+ * traffic (34 B per board per call instead of per step). With given actions the same action
+ * bytes apply at every step (a bad byte counts n_steps errors). n_steps >= 0. */
 int r48_env_step_n(r48_env *env, int32_t n_steps, int8_t *actions, uint32_t flags, uint8_t *done,
                    uint8_t *changed, int32_t *reward, int32_t *score, void *stream);
-/* Board count from which r48_env_step_n ping-pongs through the scratch copy (default 2^24 + 1;
- * 0 = never). For tests and experiments; drops the scratch copy when the env falls below it. */
-int r48_env_set_pingpong_min(r48_env *env, int64_t min_boards);
-/* Capture + instantiate the graphs r48_env_step_n would replay for these arguments, without
- * running anything (keeps graph construction out of a timed or latency-critical region). */
-int r48_env_prepare_step_n(r48_env *env, int32_t n_steps, int8_t *actions, uint32_t flags, uint8_t *done,
-                           uint8_t *changed, int32_t *reward, int32_t *score);
 
 /* Game.step with the spawn draws injected (parity mode, reproduces a reference trajectory
  * given the reference's randint/uniform draws): rank[i] modulo the post-move blank count,

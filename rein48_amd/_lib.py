@@ -14,7 +14,8 @@ import threading
 
 import torch  # noqa: F401  (see module docstring: HIP runtime load order)
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "librein48.so")
+# R48_LIB: an alternative build of the same library (experiments in tools/ only)
+LIB_PATH = os.environ.get("R48_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "librein48.so")
 
 R48_OK, R48_EINVAL, R48_EHIP, R48_ENOMEM = 0, -1, -2, -3
 AUTO_RESET, RANDOM_POLICY, MERGE_REWARD = 1, 2, 4
@@ -62,9 +63,7 @@ SIGNATURES = {
     "r48_env_reset_with_draws": (C.c_int, [_P, _P, _P, _P, _P]),
     "r48_env_fill_random": (C.c_int, [_P, _U32, _P]),
     "r48_env_step": (C.c_int, [_P, _P, _U32, _P, _P, _P, _P, _P]),
-    "r48_env_set_pingpong_min": (C.c_int, [_P, _I64]),
     "r48_env_step_n": (C.c_int, [_P, _I32, _P, _U32, _P, _P, _P, _P, _P]),
-    "r48_env_prepare_step_n": (C.c_int, [_P, _I32, _P, _U32, _P, _P, _P, _P]),
     "r48_env_step_with_draws": (C.c_int, [_P, _P, _P, _P, _U32, _P, _P, _P, _P]),
     "r48_env_move": (C.c_int, [_P, _P, _U32, _P, _P, _P, _P]),
     "r48_env_spawn": (C.c_int, [_P, _P, _P, _P, _P, _P]),

@@ -8,8 +8,6 @@
 // 16 B board in + 16 B board out + 1 B action out + 1 B done out = 34 B.
 #include <hip/hip_runtime.h>
 
-#include <atomic>
-#include <map>
 #include <cstdint>
 #include <cstdio>
 #include <string>
@@ -22,40 +20,20 @@ using r48::Board;
 namespace {
 
 constexpr int kBlock = 256;
-// r48_env_step_n splits an env of >= kChainMin boards into kMaxChains contiguous shards, each
-// replaying its own graph on its own stream: the two dependent-launch chains overlap one
-// shard's load latency / store drain with the other's compute (1M boards: 10.3 -> 7.2 us).
-#ifndef R48_MAX_CHAINS
-#define R48_MAX_CHAINS 2
-#endif
-constexpr int kMaxChains = R48_MAX_CHAINS;
-constexpr int64_t kChainMin = (int64_t)1 << 18;
-// 2^24 boards = 256 MiB, the Infinity Cache: above it both patterns stream from HBM and
-// ping-pong wins (2^26: 384 vs 425 us per step, tools/pingpong_bw.hip); at 2^24 the in-place
-// array still fits the cache and in-place wins (85 vs 101 us)
-constexpr int64_t kPingPongMin = ((int64_t)1 << 24) + 1;
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-
-#ifndef R48_NT_BOARDS
-#define R48_NT_BOARDS 0   // experiments: 1 = nontemporal board loads, 2 = stores, 3 = both
-#endif
 
 __device__ __forceinline__ Board load_board(const int8_t *boards, int64_t i)
 {
     const u32x4 *p = reinterpret_cast<const u32x4 *>(boards + 16 * i);
-    const u32x4 v = (R48_NT_BOARDS & 1) ? __builtin_nontemporal_load(p) : *p;
+    const u32x4 v = *p;
     return Board{v.x, v.y, v.z, v.w};
 }
 
 __device__ __forceinline__ void store_board(int8_t *boards, int64_t i, const Board &b)
 {
     u32x4 *p = reinterpret_cast<u32x4 *>(boards + 16 * i);
-    const u32x4 v = {b.w0, b.w1, b.w2, b.w3};
-    if (R48_NT_BOARDS & 2)
-        __builtin_nontemporal_store(v, p);
-    else
-        *p = v;
+    *p = u32x4{b.w0, b.w1, b.w2, b.w3};
 }
 
 __device__ __forceinline__ void philox_words(uint32_t w[4], uint64_t gid, uint32_t ctr, uint32_t tag,
@@ -69,11 +47,11 @@ __device__ __forceinline__ void philox_words(uint32_t w[4], uint64_t gid, uint32
 }
 
 // one wave-level atomic per wave that saw a bad action byte
-__device__ __forceinline__ void count_bad(bool bad, unsigned long long *err)
+__device__ __forceinline__ void count_bad(bool bad, unsigned long long *err, unsigned times = 1)
 {
     const unsigned long long m = __ballot(bad);
     if (m && (threadIdx.x & 63) == __builtin_ctzll(m))
-        atomicAdd(err, (unsigned long long)__builtin_popcountll(m));
+        atomicAdd(err, (unsigned long long)__builtin_popcountll(m) * times);
 }
 
 // ---------------------------------------------------------------- Philox-mode step
@@ -109,20 +87,23 @@ struct LaneOut {
     uint32_t a, done, changed, reward, score;
 };
 
+// One Philox-mode step of one board held in registers. `a_given` is the caller's action byte
+// (ignored under RANDOM); bad bytes (> 3) leave the board unchanged -- the caller counts them.
+// want_score: tile sum of the stepped board before any auto-reset (main.py:48).
 template <bool RANDOM, bool AUTO_RESET, bool REWARD, bool RESET_BRANCH = true>
-__device__ __forceinline__ LaneOut step_lane(Board b, int64_t i, Draw d, const int8_t *actions, bool want_score,
-                                             unsigned long long *err)
+__device__ __forceinline__ LaneOut step_lane(Board b, uint32_t a_given, Draw d, bool want_score)
 {
     LaneOut r;
-    if (RANDOM) {
-        r.a = d.x >> 30;  // uniform over {UP, DOWN, LEFT, RIGHT} (control/rand.py:9-11)
-    } else {
-        r.a = (uint32_t)(uint8_t)actions[i];
-        count_bad(r.a > 3u, err);
-    }
+    r.a = RANDOM ? d.x >> 30 : a_given;  // uniform over {UP, DOWN, LEFT, RIGHT} (control/rand.py:9-11)
     const r48::StepOut o =
         r48::step_board<REWARD, false, RANDOM>(b, r.a, d.y, (d.x & 0x3FFFFFFFu) < r48::kFourThresh30);
-    r.score = want_score ? r48::tile_sum(b) : 0u;
+    r.score = 0u;
+    if (want_score) {
+        // wave-uniform branch; the empty asm keeps the compiler from if-converting the ~40-VALU
+        // tile sum into every step
+        asm volatile("" ::: "memory");
+        r.score = r48::tile_sum(b);
+    }
     // auto-reset: ~1 board-step in 140 is done, so most waves skip it (wave-uniform branch).
     // Inside a multi-board tile (RESET_BRANCH = false) the branch would split the straight-line
     // load/compute pipeline, so there it is a select.
@@ -178,56 +159,118 @@ __device__ __forceinline__ void emit_pair(const LaneOut &e, const LaneOut &o, in
         *reinterpret_cast<uint2 *>(score + i) = make_uint2(e.score, o.score);
 }
 
-// Boards are read from `src` and written to `boards` (the same array for an in-place step; two
-// arrays when r48_env_step_n ping-pongs a large env through its scratch copy, see launch_step).
-// The Philox step counter is `step_arg` (eager launches) or `*d_ctr + step_arg` (graph
-// replays: node k of a captured chunk carries step_arg = k and the launch function sets
-// *d_ctr to the env's counter with a memset before each replay).
-//
-// NP board pairs per lane: a block owns a tile of 2 * NP * kBlock boards, lane t's pair j is
-// boards tile + 2 * kBlock * j + 2t and +1 (each pair = 32 contiguous bytes, a wave's pair slot
-// one contiguous 2 KiB), and ONE Philox call serves both boards of a pair. Full, pair-aligned
-// tiles take a straight-line path -- all loads issued back to back, each pair computed as soon
-// as its loads have landed, all stores at the end. The grid's partial last tile and envs whose
+// the pair path stores 2-byte / 8-byte pairs: caller planes must be aligned for that
+__device__ __forceinline__ bool planes_aligned(const void *actions, const void *done, const void *changed,
+                                               const void *reward, const void *score)
+{
+    return ((((uintptr_t)actions | (uintptr_t)done | (uintptr_t)changed) & 1u) |
+            (((uintptr_t)reward | (uintptr_t)score) & 7u)) == 0;
+}
+
+// ---------------------------------------------------------------- one step (r48_env_step)
+// One launch = one step of every board, boards read from and written back to HBM: 34 B per
+// board-step under the random policy, the HBM-roofline kernel.
+// A lane takes one board PAIR: boards tile + 2t and + 1 of its block's tile (32 contiguous
+// bytes; a wave's pairs are one contiguous 2 KiB) and ONE Philox call serves both boards. Full,
+// pair-aligned tiles take a straight-line path; the grid's partial last tile and envs whose
 // global board ids start odd (pairs straddling the tile) take the guarded per-board path.
-template <bool RANDOM, bool AUTO_RESET, bool REWARD, int NP>
-__global__ __launch_bounds__(kBlock) void k_step(const int8_t *src, int8_t *boards, int64_t n, int64_t gid0,
-                                                 uint32_t k0, uint32_t k1, const uint32_t *__restrict__ d_ctr,
-                                                 uint32_t step_arg, int8_t *__restrict__ actions,
+template <bool RANDOM, bool AUTO_RESET, bool REWARD>
+__global__ __launch_bounds__(kBlock) void k_step(int8_t *boards, int64_t n, int64_t gid0, uint32_t k0, uint32_t k1,
+                                                 uint32_t step, int8_t *__restrict__ actions,
                                                  uint8_t *__restrict__ done, uint8_t *__restrict__ changed,
                                                  int32_t *__restrict__ reward, int32_t *__restrict__ score,
                                                  unsigned long long *err)
 {
+    constexpr int64_t kTile = (int64_t)kBlock * 2;
+    const int64_t i = (int64_t)blockIdx.x * kTile + 2 * (int64_t)threadIdx.x;
+    const bool want_score = score != nullptr;
+    if ((int64_t)(blockIdx.x + 1) * kTile <= n && (gid0 & 1) == 0 &&
+        planes_aligned(actions, done, changed, reward, score)) {
+        const Board be = load_board(boards, i), bo = load_board(boards, i + 1);
+        uint32_t ae = 0, ao = 0;
+        if (!RANDOM) {
+            const uint16_t a2 = *reinterpret_cast<const uint16_t *>(actions + i);
+            ae = a2 & 0xffu;
+            ao = a2 >> 8;
+            count_bad(ae > 3u, err);
+            count_bad(ao > 3u, err);
+        }
+        Draw de, dd;
+        pair_draws((uint64_t)(gid0 + i) >> 1, step, k0, k1, de, dd);
+        const LaneOut re = step_lane<RANDOM, AUTO_RESET, REWARD>(be, ae, de, want_score);
+        const LaneOut ro = step_lane<RANDOM, AUTO_RESET, REWARD>(bo, ao, dd, want_score);
+        emit_pair<RANDOM, REWARD>(re, ro, i, boards, actions, done, changed, reward, score);
+    } else {
+        for (int j = 0; j < 2; j++) {
+            if (i + j < n) {
+                const uint32_t a = RANDOM ? 0u : (uint32_t)(uint8_t)actions[i + j];
+                if (!RANDOM)
+                    count_bad(a > 3u, err);
+                const Draw d = board_draw((uint64_t)(gid0 + i + j), step, k0, k1);
+                const LaneOut r =
+                    step_lane<RANDOM, AUTO_RESET, REWARD, false>(load_board(boards, i + j), a, d, want_score);
+                emit<RANDOM, REWARD>(r, i + j, boards, actions, done, changed, reward, score);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------- K steps in one launch
+// r48_env_step_n: n_steps consecutive steps of every board in ONE launch. Boards are independent,
+// so a lane keeps its NP board pairs in VGPRs for all n_steps steps (no grid barrier, no board
+// round trip through HBM between steps) and writes the boards and the last step's output planes
+// once at the end -- exactly what n_steps k_step launches leave in memory (the per-step planes
+// are overwritten by every step). Same draw contract as k_step, step counter step0 + t. Bound:
+// VALU issue (~200 VALU per board-step); HBM traffic is 34 B per board per
+// call, not per step.
+#ifndef R48_STEPN_NP
+#define R48_STEPN_NP 1
+#endif
+template <bool RANDOM, bool AUTO_RESET, bool REWARD, int NP>
+__global__ __launch_bounds__(kBlock) void k_step_n(int8_t *boards, int64_t n, int64_t gid0, uint32_t k0, uint32_t k1,
+                                                   uint32_t step0, int32_t n_steps, int8_t *__restrict__ actions,
+                                                   uint8_t *__restrict__ done, uint8_t *__restrict__ changed,
+                                                   int32_t *__restrict__ reward, int32_t *__restrict__ score,
+                                                   unsigned long long *err)
+{
     constexpr int64_t kTile = (int64_t)kBlock * 2 * NP;
     const int64_t base = (int64_t)blockIdx.x * kTile + 2 * (int64_t)threadIdx.x;
-    const uint32_t step = (d_ctr ? *d_ctr : 0u) + step_arg;
     const bool want_score = score != nullptr;
-    // the pair path stores 2-byte / 8-byte pairs: caller planes must be aligned for that
-    const bool aligned = ((((uintptr_t)actions | (uintptr_t)done | (uintptr_t)changed) & 1u) |
-                          (((uintptr_t)reward | (uintptr_t)score) & 7u)) == 0;
-    if ((int64_t)(blockIdx.x + 1) * kTile <= n && (gid0 & 1) == 0 && aligned) {
+    const int32_t last = n_steps - 1;
+    if ((int64_t)(blockIdx.x + 1) * kTile <= n && (gid0 & 1) == 0 &&
+        planes_aligned(actions, done, changed, reward, score)) {
         Board b[2 * NP];
-#pragma unroll
-        for (int j = 0; j < NP; j++) {
-            b[2 * j] = load_board(src, base + 2 * kBlock * j);
-            b[2 * j + 1] = load_board(src, base + 2 * kBlock * j + 1);
-        }
-        LaneOut r[2 * NP];
+        uint32_t a[2 * NP];
+        uint64_t q[NP];
 #pragma unroll
         for (int j = 0; j < NP; j++) {
             const int64_t i = base + 2 * kBlock * j;
-            Draw de, dd;
-#if defined(R48_ABLATE_STEP_COPY)
-            // timing floor only (tools/exp_step_variants.py): same launches and I/O, no compute
-            r[2 * j] = LaneOut{Board{b[2 * j].w0 ^ step, b[2 * j].w1, b[2 * j].w2, b[2 * j].w3}, step & 3u, 0u, 0u, 0u, 0u};
-            r[2 * j + 1] = LaneOut{Board{b[2 * j + 1].w0 ^ step, b[2 * j + 1].w1, b[2 * j + 1].w2, b[2 * j + 1].w3},
-                                   step & 3u, 0u, 0u, 0u, 0u};
-            continue;
-#endif
-            pair_draws((uint64_t)(gid0 + i) >> 1, step, k0, k1, de, dd);
-            r[2 * j] = step_lane<RANDOM, AUTO_RESET, REWARD, NP == 1>(b[2 * j], i, de, actions, want_score, err);
-            r[2 * j + 1] =
-                step_lane<RANDOM, AUTO_RESET, REWARD, NP == 1>(b[2 * j + 1], i + 1, dd, actions, want_score, err);
+            b[2 * j] = load_board(boards, i);
+            b[2 * j + 1] = load_board(boards, i + 1);
+            q[j] = (uint64_t)(gid0 + i) >> 1;
+            a[2 * j] = a[2 * j + 1] = 0u;
+            if (!RANDOM) {
+                const uint16_t a2 = *reinterpret_cast<const uint16_t *>(actions + i);
+                a[2 * j] = a2 & 0xffu;
+                a[2 * j + 1] = a2 >> 8;
+                // every step re-reads the same bad byte: n_steps errors per board, like k_step
+                count_bad(a[2 * j] > 3u, err, (unsigned)n_steps);
+                count_bad(a[2 * j + 1] > 3u, err, (unsigned)n_steps);
+            }
+        }
+        LaneOut r[2 * NP];
+        for (int32_t t = 0; t < n_steps; t++) {
+            const uint32_t step = step0 + (uint32_t)t;
+            const bool sc = want_score && t == last;
+#pragma unroll
+            for (int j = 0; j < NP; j++) {
+                Draw de, dd;
+                pair_draws(q[j], step, k0, k1, de, dd);
+                r[2 * j] = step_lane<RANDOM, AUTO_RESET, REWARD>(b[2 * j], a[2 * j], de, sc);
+                r[2 * j + 1] = step_lane<RANDOM, AUTO_RESET, REWARD>(b[2 * j + 1], a[2 * j + 1], dd, sc);
+                b[2 * j] = r[2 * j].b;
+                b[2 * j + 1] = r[2 * j + 1].b;
+            }
         }
 #pragma unroll
         for (int j = 0; j < NP; j++)
@@ -237,9 +280,16 @@ __global__ __launch_bounds__(kBlock) void k_step(const int8_t *src, int8_t *boar
         for (int j = 0; j < 2 * NP; j++) {
             const int64_t i = base + 2 * kBlock * (j >> 1) + (j & 1);
             if (i < n) {
-                const Draw d = board_draw((uint64_t)(gid0 + i), step, k0, k1);
-                const LaneOut r = step_lane<RANDOM, AUTO_RESET, REWARD, false>(load_board(src, i), i, d, actions,
-                                                                               want_score, err);
+                const uint32_t a = RANDOM ? 0u : (uint32_t)(uint8_t)actions[i];
+                if (!RANDOM)
+                    count_bad(a > 3u, err, (unsigned)n_steps);
+                Board b = load_board(boards, i);
+                LaneOut r;
+                for (int32_t t = 0; t < n_steps; t++) {
+                    const Draw d = board_draw((uint64_t)(gid0 + i), step0 + (uint32_t)t, k0, k1);
+                    r = step_lane<RANDOM, AUTO_RESET, REWARD, false>(b, a, d, want_score && t == last);
+                    b = r.b;
+                }
                 emit<RANDOM, REWARD>(r, i, boards, actions, done, changed, reward, score);
             }
         }
@@ -504,26 +554,6 @@ __global__ __launch_bounds__(kBlock) void k_values_check(const int32_t *__restri
 }  // namespace
 
 // =============================================================================== C-ABI
-struct GraphKey {
-    int32_t chain;
-    int32_t n_steps;
-    uint32_t flags;
-    const void *p[6];
-    bool operator<(const GraphKey &o) const
-    {
-        if (chain != o.chain)
-            return chain < o.chain;
-        if (n_steps != o.n_steps)
-            return n_steps < o.n_steps;
-        if (flags != o.flags)
-            return flags < o.flags;
-        for (int k = 0; k < 6; k++)
-            if (p[k] != o.p[k])
-                return p[k] < o.p[k];
-        return false;
-    }
-};
-
 struct r48_env {
     int device;
     int64_t n;
@@ -533,15 +563,6 @@ struct r48_env {
     uint32_t reset_ctr;
     int8_t *boards;
     unsigned long long *err;  // device counter of bad action bytes
-    uint32_t *d_ctr;          // step counter read by graph-replayed step kernels
-    hipStream_t chain[kMaxChains];  // private streams: one per shard chain of r48_env_step_n
-    hipEvent_t fork, join[kMaxChains];
-    std::map<GraphKey, hipGraphExec_t> graphs;
-    // r48_env_step_n on envs of >= pingpong_min boards alternates the boards between the bound
-    // array and this env-owned copy (read one, write the other): past the Infinity Cache an
-    // in-place read-modify-write sweep moves ~10 % fewer bytes per second than read-A/write-B
-    int8_t *scratch = nullptr;
-    int64_t pingpong_min = kPingPongMin;
 };
 
 namespace {
@@ -621,16 +642,10 @@ int r48_env_create(r48_env **out, int device, int64_t n_boards, uint64_t seed, i
     DeviceGuard g(device);
     if (!g.ok)
         return fail(R48_EHIP, "hipSetDevice failed");
-    r48_env *env = new r48_env{device, n_boards, seed, board_offset, 0u, 0u, nullptr, nullptr, nullptr, {}, nullptr, {},
-                               {}};
+    r48_env *env = new r48_env{device, n_boards, seed, board_offset, 0u, 0u, nullptr, nullptr};
     if (hipMalloc(&env->err, sizeof(unsigned long long)) != hipSuccess) {
         delete env;
         return fail(R48_ENOMEM, "hipMalloc(error counter) failed");
-    }
-    if (hipMalloc(&env->d_ctr, sizeof(uint32_t)) != hipSuccess) {
-        (void)hipFree(env->err);
-        delete env;
-        return fail(R48_ENOMEM, "hipMalloc(step counter) failed");
     }
     if (hipMemset(env->err, 0, sizeof(unsigned long long)) != hipSuccess) {
         (void)hipFree(env->err);
@@ -646,20 +661,7 @@ int r48_env_destroy(r48_env *env)
     if (!env)
         return R48_OK;
     DeviceGuard g(env->device);
-    for (auto &kv : env->graphs)
-        (void)hipGraphExecDestroy(kv.second);
-    for (int c = 0; c < kMaxChains; c++) {
-        if (env->chain[c])
-            (void)hipStreamDestroy(env->chain[c]);
-        if (env->join[c])
-            (void)hipEventDestroy(env->join[c]);
-    }
-    if (env->fork)
-        (void)hipEventDestroy(env->fork);
-    (void)hipFree(env->d_ctr);
     (void)hipFree(env->err);
-    if (env->scratch)
-        (void)hipFree(env->scratch);
     delete env;
     return R48_OK;
 }
@@ -670,33 +672,11 @@ int r48_env_bind_boards(r48_env *env, int8_t *boards)
         return s;
     if (!boards || (reinterpret_cast<uintptr_t>(boards) & 15u))
         return fail(R48_EINVAL, "boards must be a non-NULL 16-byte aligned device pointer");
-    if (env->boards != boards) {
-        for (auto &kv : env->graphs)
-            (void)hipGraphExecDestroy(kv.second);
-        env->graphs.clear();
-    }
     env->boards = boards;
     return R48_OK;
 }
 
 int8_t *r48_env_boards(const r48_env *env) { return env ? env->boards : nullptr; }
-
-int r48_env_set_pingpong_min(r48_env *env, int64_t min_boards)
-{
-    if (int s = check_env(env, false))
-        return s;
-    if (min_boards < 0)
-        return fail(R48_EINVAL, "min_boards < 0");
-    env->pingpong_min = min_boards == 0 ? INT64_MAX : min_boards;
-    if (env->n < env->pingpong_min && env->scratch) {
-        for (auto &kv : env->graphs)
-            (void)hipGraphExecDestroy(kv.second);
-        env->graphs.clear();
-        (void)hipFree(env->scratch);
-        env->scratch = nullptr;
-    }
-    return R48_OK;
-}
 
 int64_t r48_env_size(const r48_env *env) { return env ? env->n : 0; }
 
@@ -771,29 +751,27 @@ int validate_step(const r48_env *env, const int8_t *actions, uint32_t flags)
     return R48_OK;
 }
 
-// one k_step launch over boards [off, off+cnt) of the env; step counter =
-// (d_ctr ? *d_ctr : 0) + step_arg. A lane takes one board pair (one Philox call per two boards)
-// at every size: two pairs per lane measured slower even on the HBM-bound 2^26-board sweep
-// (437 vs 428-432 us per step), so only NP = 1 is instantiated.
-void launch_step(r48_env *env, int64_t off, int64_t cnt, const uint32_t *d_ctr, uint32_t step_arg,
-                 int8_t *actions, uint32_t flags, uint8_t *done, uint8_t *changed, int32_t *reward, int32_t *score,
-                 hipStream_t stream, const int8_t *src = nullptr, int8_t *dst = nullptr)
+// one launch over all boards: n_steps == 1 -> k_step (boards through HBM), else k_step_n
+// (boards in VGPRs for all n_steps). 8 instantiations each: policy source x auto-reset x reward.
+void launch_steps(r48_env *env, int32_t n_steps, int8_t *actions, uint32_t flags, uint8_t *done, uint8_t *changed,
+                  int32_t *reward, int32_t *score, hipStream_t stream)
 {
-    if (!src)
-        src = env->boards;
-    if (!dst)
-        dst = env->boards;
     const bool rnd = flags & R48_RANDOM_POLICY, ar = flags & R48_AUTO_RESET, rw = flags & R48_MERGE_REWARD;
     const uint32_t k0 = (uint32_t)env->seed, k1 = (uint32_t)(env->seed >> 32);
-    auto at = [off](auto *p) { return p ? p + off : p; };
-    auto go = [&](auto kern, int NP) {
-        const int64_t tile = (int64_t)kBlock * 2 * NP;
-        const dim3 grid((unsigned)((cnt + tile - 1) / tile));
-        hipLaunchKernelGGL(kern, grid, dim3(kBlock), 0, stream, src + 16 * off, dst + 16 * off, cnt, env->gid0 + off, k0,
-                           k1, d_ctr, step_arg, at(actions), at(done), at(changed), at(reward), at(score), env->err);
+    auto one = [&](auto kern) {
+        const int64_t tile = (int64_t)kBlock * 2;
+        hipLaunchKernelGGL(kern, dim3((unsigned)((env->n + tile - 1) / tile)), dim3(kBlock), 0, stream, env->boards,
+                           env->n, env->gid0, k0, k1, env->step_ctr, actions, done, changed, reward, score,
+                           env->err);
     };
-#define R48_GO(RN, AR, RW) go(k_step<RN, AR, RW, 1>, 1)
-    // 8 instantiations: policy source x auto-reset x reward mode
+    auto many = [&](auto kern) {
+        const int64_t tile = (int64_t)kBlock * 2 * R48_STEPN_NP;
+        hipLaunchKernelGGL(kern, dim3((unsigned)((env->n + tile - 1) / tile)), dim3(kBlock), 0, stream, env->boards,
+                           env->n, env->gid0, k0, k1, env->step_ctr, n_steps, actions, done, changed, reward, score,
+                           env->err);
+    };
+#define R48_GO(RN, AR, RW) \
+    (n_steps == 1 ? one(k_step<RN, AR, RW>) : many(k_step_n<RN, AR, RW, R48_STEPN_NP>))
     if (rnd) {
         if (ar) rw ? R48_GO(true, true, true) : R48_GO(true, true, false);
         else rw ? R48_GO(true, false, true) : R48_GO(true, false, false);
@@ -814,140 +792,24 @@ int r48_env_step(r48_env *env, int8_t *actions, uint32_t flags, uint8_t *done, u
     if (int s = validate_step(env, actions, flags))
         return s;
     DeviceGuard g(env->device);
-    launch_step(env, 0, env->n, nullptr, env->step_ctr, actions, flags, done, changed, reward, score,
-                (hipStream_t)stream);
+    launch_steps(env, 1, actions, flags, done, changed, reward, score, (hipStream_t)stream);
     env->step_ctr++;
     return launched("k_step");
-}
-
-}  // extern "C"
-
-namespace {
-
-// Find or capture+instantiate the per-chain graphs of n_steps step kernels.
-int chain_graphs(r48_env *env, int32_t n_steps, int8_t *actions, uint32_t flags, uint8_t *done, uint8_t *changed,
-                 int32_t *reward, int32_t *score, int chains, hipGraphExec_t *exec)
-{
-    if (env->n >= env->pingpong_min && !env->scratch) {
-        // one allocation per env; without it (out of memory) the chains simply step in place
-        if (hipMalloc(&env->scratch, (size_t)env->n * 16) != hipSuccess) {
-            (void)hipGetLastError();
-            env->scratch = nullptr;
-        } else {
-            for (auto &kv : env->graphs)   // graphs captured in place are stale now
-                (void)hipGraphExecDestroy(kv.second);
-            env->graphs.clear();
-        }
-    }
-    if (!env->fork) {
-        for (int c = 0; c < kMaxChains; c++)
-            if (hipStreamCreateWithFlags(&env->chain[c], hipStreamNonBlocking) != hipSuccess ||
-                hipEventCreateWithFlags(&env->join[c], hipEventDisableTiming) != hipSuccess)
-                return fail(R48_EHIP, "creating chain streams/events failed");
-        if (hipEventCreateWithFlags(&env->fork, hipEventDisableTiming) != hipSuccess)
-            return fail(R48_EHIP, "hipEventCreate failed");
-    }
-    for (int c = 0; c < chains; c++) {
-        // shard boundaries on even board ids: every board pair stays inside one shard
-        const int64_t off = (env->n * c / chains) & ~(int64_t)1;
-        const int64_t end = c + 1 == chains ? env->n : (env->n * (c + 1) / chains) & ~(int64_t)1;
-        const int64_t cnt = end - off;
-        const GraphKey key{c, n_steps, flags, {env->boards, actions, done, changed, reward, score}};
-        auto it = env->graphs.find(key);
-        if (it == env->graphs.end()) {
-            // capture this shard's n_steps dependent step kernels once; replays read the
-            // step counter from d_ctr
-            if (hipStreamBeginCapture(env->chain[c], hipStreamCaptureModeThreadLocal) != hipSuccess)
-                return fail(R48_EHIP, "hipStreamBeginCapture failed");
-            // ping-pong: step k writes the bound array when n_steps - 1 - k is even, else the
-            // scratch copy, and reads what step k - 1 wrote -- the last step always lands in the
-            // bound array (an odd count starts with one in-place step)
-            const int8_t *src = env->boards;
-            for (int32_t k = 0; k < n_steps; k++) {
-                int8_t *dst = (!env->scratch || ((n_steps - 1 - k) & 1) == 0) ? env->boards : env->scratch;
-                launch_step(env, off, cnt, env->d_ctr, (uint32_t)k, actions, flags, done, changed, reward, score,
-                            env->chain[c], src, dst);
-                src = dst;
-            }
-            hipGraph_t graph = nullptr;
-            const hipError_t ce = hipStreamEndCapture(env->chain[c], &graph);
-            if (ce != hipSuccess || !graph)
-                return fail(R48_EHIP, std::string("stream capture failed: ") + hipGetErrorString(ce));
-            hipGraphExec_t x = nullptr;
-            const hipError_t ie = hipGraphInstantiate(&x, graph, nullptr, nullptr, 0);
-            (void)hipGraphDestroy(graph);
-            if (ie != hipSuccess)
-                return fail(R48_EHIP, std::string("hipGraphInstantiate failed: ") + hipGetErrorString(ie));
-            // move the one-time upload of the executable graph off the first replay
-            if (hipGraphUpload(x, env->chain[c]) != hipSuccess || hipStreamSynchronize(env->chain[c]) != hipSuccess)
-                return fail(R48_EHIP, "hipGraphUpload failed");
-            it = env->graphs.emplace(key, x).first;
-        }
-        exec[c] = it->second;
-    }
-    return R48_OK;
-}
-
-int check_step_n(const r48_env *env, const int8_t *actions, uint32_t flags, int32_t n_steps)
-{
-    if (int s = validate_step(env, actions, flags))
-        return s;
-    if (n_steps < 0 || n_steps > 4096)
-        return fail(R48_EINVAL, "n_steps must be in 0..4096");
-    return R48_OK;
-}
-
-}  // namespace
-
-extern "C" {
-
-int r48_env_prepare_step_n(r48_env *env, int32_t n_steps, int8_t *actions, uint32_t flags, uint8_t *done,
-                           uint8_t *changed, int32_t *reward, int32_t *score)
-{
-    if (int s = check_step_n(env, actions, flags, n_steps))
-        return s;
-    if (n_steps == 0)
-        return R48_OK;
-    DeviceGuard g(env->device);
-    hipGraphExec_t exec[kMaxChains] = {};
-    return chain_graphs(env, n_steps, actions, flags, done, changed, reward, score,
-                        env->n >= kChainMin ? kMaxChains : 1, exec);
 }
 
 int r48_env_step_n(r48_env *env, int32_t n_steps, int8_t *actions, uint32_t flags, uint8_t *done, uint8_t *changed,
                    int32_t *reward, int32_t *score, void *stream)
 {
-    if (int s = check_step_n(env, actions, flags, n_steps))
+    if (int s = validate_step(env, actions, flags))
         return s;
+    if (n_steps < 0)
+        return fail(R48_EINVAL, "n_steps < 0");
     if (n_steps == 0)
         return R48_OK;
     DeviceGuard g(env->device);
-    const hipStream_t user = (hipStream_t)stream;
-    const int chains = env->n >= kChainMin ? kMaxChains : 1;
-    hipGraphExec_t exec[kMaxChains] = {};
-    if (int s = chain_graphs(env, n_steps, actions, flags, done, changed, reward, score, chains, exec))
-        return s;
-    // caller's stream: counter memset -> [fork] -> shard 0's graph; shard 1's graph replays on
-    // the env's own stream between one fork and one join (a cross-stream wait costs tens of
-    // microseconds, so there is exactly one of each per call)
-    if (hipMemsetD32Async((hipDeviceptr_t)env->d_ctr, (int)env->step_ctr, 1, user) != hipSuccess)
-        return fail(R48_EHIP, "hipMemsetD32Async(step counter) failed");
-    if (chains > 1 && hipEventRecord(env->fork, user) != hipSuccess)
-        return fail(R48_EHIP, "recording the fork event failed");
-    for (int c = 1; c < chains; c++)
-        if (hipStreamWaitEvent(env->chain[c], env->fork, 0) != hipSuccess)
-            return fail(R48_EHIP, "forking a shard chain failed");
-    for (int c = 0; c < chains; c++) {
-        const hipError_t le = hipGraphLaunch(exec[c], c == 0 ? user : env->chain[c]);
-        if (le != hipSuccess)
-            return fail(R48_EHIP, std::string("hipGraphLaunch failed: ") + hipGetErrorString(le));
-    }
-    for (int c = 1; c < chains; c++)
-        if (hipEventRecord(env->join[c], env->chain[c]) != hipSuccess ||
-            hipStreamWaitEvent(user, env->join[c], 0) != hipSuccess)
-            return fail(R48_EHIP, "joining a shard chain failed");
+    launch_steps(env, n_steps, actions, flags, done, changed, reward, score, (hipStream_t)stream);
     env->step_ctr += (uint32_t)n_steps;
-    return R48_OK;
+    return launched("k_step_n");
 }
 
 int r48_env_step_with_draws(r48_env *env, const int8_t *actions, const uint8_t *rank, const uint8_t *four,

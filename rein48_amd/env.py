@@ -151,23 +151,12 @@ class VecGame:
 
     def step_n(self, n_steps, actions=None, auto_reset=False, merge_reward=False, want_changed=False,
                score=None):
-        """n_steps consecutive step() calls with the same arguments, replayed from cached
-        hipGraphs (one host call for the whole chunk; 2 shard chains for >= 2^18 boards).
-        Outputs hold the last step's values. Prefer large chunks (<= 4096)."""
+        """n_steps consecutive step() calls with the same arguments in ONE kernel launch
+        (k_step_n: every board stays in registers for all n_steps steps). Outputs hold the last
+        step's values, exactly as after n_steps step() calls."""
         a = self._step_n_args(actions, auto_reset, merge_reward, want_changed, score)
         check(self._lib.r48_env_step_n(self._env, int(n_steps), a[0], a[1], *a[2:], self._s()))
         return self.boards, (self.reward if merge_reward else self._zero_reward), self.done
-
-    def set_pingpong_min(self, min_boards):
-        """Board count from which step_n alternates between the boards and an env-owned scratch
-        copy (default 2^24 + 1, past the Infinity Cache; 0 = never). Results are unchanged."""
-        check(self._lib.r48_env_set_pingpong_min(self._env, int(min_boards)))
-
-    def prepare_step_n(self, n_steps, actions=None, auto_reset=False, merge_reward=False, want_changed=False,
-                       score=None):
-        """Build (capture + instantiate) the graphs step_n would replay, without running them."""
-        a = self._step_n_args(actions, auto_reset, merge_reward, want_changed, score)
-        check(self._lib.r48_env_prepare_step_n(self._env, int(n_steps), a[0], a[1], *a[2:]))
 
     def step_with_draws(self, actions, rank, four, merge_reward=False):
         """Parity mode: Game.step with the reference's spawn draws injected."""

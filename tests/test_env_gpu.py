@@ -416,57 +416,69 @@ def test_input_validation():
         v.step(torch.zeros(8, dtype=torch.int8))  # host tensor
 
 
-def test_step_n_graph_equals_repeated_steps():
-    """r48_env_step_n (cached hipGraph replay, device-side counter) == eager steps, across
-    several replays of the same graph and interleaved eager calls."""
-    n, seed = 50_000, 77
-    rng = np.random.default_rng(9)
-    b0 = rand_boards(rng, n, emax=6)
-    a, b = vec(n, seed=seed, offset=5), vec(n, seed=seed, offset=5)
-    put(a, b0)
-    put(b, b0)
-    for chunk in (16, 16, 3, 16):
-        a.step_n(chunk, auto_reset=True)
-        a.step(None, auto_reset=True)
-        for _ in range(chunk + 1):
-            b.step(None, auto_reset=True)
-        assert torch.equal(a.boards, b.boards), chunk
-        assert torch.equal(a.done, b.done) and torch.equal(a.actions, b.actions)
-    assert a.counters == b.counters
-
-
-@pytest.mark.parametrize("off", [0, 3])
-def test_step_n_pingpong_equals_in_place(off):
-    """Above the ping-pong threshold (lowered here from 2^24 + 1 to every env) r48_env_step_n
-    alternates reads and writes between the bound boards and the env's scratch copy. Odd and
-    even chunk lengths, two shard chains, merge reward + done + actions outputs: identical to
-    eager in-place steps, and the bound array holds the result after every call."""
-    n, seed = 300_001, 91
-    rng = np.random.default_rng(12)
-    b0 = rand_boards(rng, n, emax=6)
+def _step_n_vs_steps(n, off, K, flags, seed, rng, actions=None):
+    """step_n(K) on one env vs K single-step launches (k_step) on a twin: every output plane,
+    the boards, the counters and the bad-action counter must be identical."""
+    b0 = rand_boards(rng, n, emax=8)
     a, b = vec(n, seed=seed, offset=off), vec(n, seed=seed, offset=off)
-    a.set_pingpong_min(1)
     put(a, b0)
     put(b, b0)
-    for chunk in (1, 2, 7, 8, 7):
-        _, ra, da = a.step_n(chunk, auto_reset=True, merge_reward=True)
-        for _ in range(chunk):
-            _, rb, db = b.step(None, auto_reset=True, merge_reward=True)
-        assert torch.equal(a.boards, b.boards), chunk
-        assert torch.equal(da, db) and torch.equal(ra, rb) and torch.equal(a.actions, b.actions)
-    a.set_pingpong_min(0)                                 # back to in place: same stream of results
-    a.step_n(5, auto_reset=True)
-    for _ in range(5):
-        b.step(None, auto_reset=True)
-    assert torch.equal(a.boards, b.boards) and a.counters == b.counters
+    kw = dict(auto_reset=bool(flags & O.AUTO_RESET), merge_reward=bool(flags & O.MERGE_REWARD), want_changed=True)
+    sa = torch.full((n,), -1, dtype=torch.int32, device=DEV)
+    sb = torch.full((n,), -1, dtype=torch.int32, device=DEV)
+    acts = None if actions is None else torch.from_numpy(actions).to(DEV)
+    _, ra, da = a.step_n(K, acts, score=sa, **kw)
+    for _ in range(K):
+        _, rb, db = b.step(acts, score=sb, **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(a.boards, b.boards), (n, off, K)
+    assert torch.equal(da, db) and torch.equal(ra, rb) and torch.equal(a.changed, b.changed)
+    assert torch.equal(sa, sb) and torch.equal(a.actions, b.actions)
+    assert a.counters == b.counters == (K, 0)
+    assert a.error_count() == b.error_count()
+    return a, b0
+
+
+@pytest.mark.parametrize("off", [0, 3])              # even: pair fast path; odd: guarded per-board path
+@pytest.mark.parametrize("K", [1, 2, 20, 4096])
+def test_step_n_equals_repeated_steps(K, off):
+    """r48_env_step_n (k_step_n: one launch, boards in VGPRs for all K steps) == K k_step
+    launches, random policy + auto-reset + merge reward + changed + score, on a ragged size (the
+    grid's partial last tile)."""
+    rng = np.random.default_rng(K * 10 + off)
+    _step_n_vs_steps(300_001, off, K, O.RANDOM_POLICY | O.AUTO_RESET | O.MERGE_REWARD, 77, rng)
+
+
+@pytest.mark.parametrize("flags", [0, O.AUTO_RESET | O.MERGE_REWARD])
+def test_step_n_given_actions_with_bad_bytes(flags):
+    """Given actions (constant over the K steps) incl. bytes outside 0..3: the board stays, and
+    the error counter grows by K per bad byte, exactly as K single steps."""
+    n, K = 70_001, 9
+    rng = np.random.default_rng(5)
+    acts = rng.integers(0, 4, n).astype(np.int8)
+    acts[rng.random(n) < 0.05] = 7
+    a, _ = _step_n_vs_steps(n, 0, K, flags, 12, rng, actions=acts)
+    assert a.error_count() == K * int((acts > 3).sum())
+
+
+@pytest.mark.parametrize("off", [0, 1])
+def test_step_n_past_the_infinity_cache(off):
+    """2^24 + 6 boards (268 MB of boards, more than the 256 MiB Infinity Cache; the size where
+    round 1's step_n ping-ponged through a scratch copy): K = 20 and 4096 on the pair path, K = 20
+    on the guarded path, == single steps."""
+    n = (1 << 24) + 6
+    rng = np.random.default_rng(off)
+    for K in ((20, 4096) if off == 0 else (20,)):
+        a, _ = _step_n_vs_steps(n, off, K, O.RANDOM_POLICY | O.AUTO_RESET, 4242, rng)
+        del a
+        torch.cuda.empty_cache()
 
 
 @pytest.mark.parametrize("off", [3, 0])               # odd: guarded per-board path; even: pair fast path
 @pytest.mark.parametrize("n", [300_001, 9_000_003])
-def test_step_n_chains_and_wide_tiles_match_oracle(n, off):
-    """Large envs: r48_env_step_n splits the boards into 2 shard chains (>= 2^18 boards, split
-    on an even board id); odd sizes exercise the partial tile. Result == eager steps == the
-    oracle, on both the pair fast path (even offset) and the guarded path (odd offset)."""
+def test_step_n_wide_envs_match_oracle(n, off):
+    """Large envs, odd sizes (the partial tile): two step_n calls == eager steps == the oracle, on
+    both the pair fast path (even offset) and the guarded path (odd offset)."""
     seed = 4040
     rng = np.random.default_rng(n)
     b0 = rand_boards(rng, n, emax=6)
