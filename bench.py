@@ -2,36 +2,43 @@
 """bench.py -- env steps/sec on 4x4 boards (BASELINE.json metric), MI355X.
 
 Workload (BASELINE.json configs[1], "1M parallel 4x4 int8 boards, random policy, env-only
-throughput on 1 MI355X"): 2^20 boards per GPU, every step = one gfx950 k_step launch over
-all of them (move + spawn + game-over + auto-reset, in-kernel uniform random policy,
-actions and done flags written back). Boards start from SURVEY.md 8(d)'s synthetic fill
-(each cell empty w.p. 1/2, else exponent ~U{1..7}; the reference reset start is an extra)
-and are resident in HBM before the timed region. Steps are issued in hipGraph
-chunks (r48_env_step_n) so the host never gates the GPU.
+throughput on 1 MI355X"): 2^20 boards per GPU, in-kernel uniform random policy (control/rand.py),
+move + spawn + game-over + auto-reset every step (game/GameClient.py:40-51). Boards start from
+SURVEY.md 8(d)'s synthetic fill (each cell empty w.p. 1/2, else exponent ~U{1..7}; the reference
+reset start is an extra) and are resident in HBM before the timed region. The K timed steps are
+r48_env_step_n calls (one k_step_n launch per call, every board in VGPRs for all the call's steps;
+a call covers the whole K unless --chunk splits it), bit-identical to K single-step launches.
 
-Multi-GPU: one process per GPU (torchrun), each rank owns boards [rank*N, (rank+1)*N)
-(Philox keyed by global board id); no data-path collective. Timing: barrier + sync on
-both sides of exactly K steps, max over ranks; value = all boards x K / that time.
+Multi-GPU: one process per GPU (torchrun; `--gpus N` without WORLD_SIZE launches torchrun itself
+as a child process before touching the GPU), rank r owns boards [r*N, (r+1)*N) (Philox keyed by
+global board id); no data-path collective. Timing: barrier + sync on both sides of exactly K
+steps, max over ranks; value = all boards x K / that time.
 
 Extra objects on the JSON line:
-  roofline      HBM roofline of k_step: 34 algorithmic bytes per board-step (16 B board in,
-                16 B out, 1 B action out, 1 B done out) per launch / the kernel's average
-                duration from HIP events over the timed region; peak 8 TB/s (MI355X spec).
-                `traffic` = per-launch HBM bytes from rocprofv3 PMC passes when
-                profiles/pmc_k_step.json exists (tools/pmc_traffic.py), else null.
-  cpu_baseline  oracle/game_port.py (faithful pure-Python restatement of the reference
-                Game + Rand, calibrated against the reference in BASELINE.md) on one process
-                per available host CPU (at most 16, the box's share) for a bounded sample,
-                plus the 1-process figure; rank 0, N=1 only (oracle/port_bench.py).
-  extras        N=1: HBM-honest point (2^26 boards/GPU, past the 256 MiB Infinity Cache), the
-                fused random-policy rollout kernel, config 3 (A3C + CNN), config 5 per GPU (DQN
-                + ResNet-10 + HBM replay) and the C oracle as a strong CPU line. N>1: config 4
-                (A3C, 2^20 boards per GPU) and config 5 (DQN, 2^21 boards per GPU) on all ranks
-                with the RCCL gradient all-reduce (--no-extras skips them).
+  roofline      k_step_n is VALU-issue bound (no memory traffic inside its step loop): achieved =
+                VALU wave-instructions per board-step (SQ_INSTS_VALU per dispatch / board-steps,
+                committed rocprofv3 PMC profile, cross-checked against the static ISA count) x
+                board-steps / the dispatch time from HIP events in the timed region; peak = one
+                wave-instruction per 2 cycles per SIMD at 2.4 GHz (1024 SIMDs). `hbm` holds the
+                single-step kernel k_step (boards through HBM every step, 34 algorithmic bytes per
+                board-step) at 2^20 boards and at 2^26 (past the 256 MiB Infinity Cache) against the
+                8 TB/s HBM spec, with its PMC traffic from the committed profile.
+  cpu_baseline  oracle/game_port.py (faithful pure-Python restatement of the reference Game + Rand,
+                calibrated against the reference in BASELINE.md) on one process per available host
+                CPU (at most 16, the box's share) for a bounded sample, plus the 1-process figure;
+                rank 0, N=1 only (oracle/port_bench.py).
+  extras        N=1: the fused random-policy rollout kernel, repeats of the timed region, the
+                reference reset start, config 3 (A3C + CNN), config 5 per GPU (DQN + ResNet-10 + HBM
+                replay) and the C oracle as a strong CPU line. N>1: config 4 (A3C, 2^20 boards per
+                GPU) and config 5 (DQN, 2^21 boards per GPU) on all ranks with the gradient
+                all-reduce (--no-extras skips them).
 """
 import argparse
+import datetime
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -42,9 +49,12 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "env steps/sec (whole node), 4×4 boards, at 1/2/4/8 MI355X"
-ALGO_BYTES = 34            # per board-step, see module docstring
+ALGO_BYTES = 34            # per board-step of k_step: 16 B board in + 16 B out + 1 B action + 1 B done
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
 HBM_MEASURED_GBS = 6290.0  # float4 copy measured on MI355X (same guide)
+SIMDS, CLOCK_GHZ = 1024, 2.4            # 256 CUs x 4 SIMDs; max clock (same guide)
+VALU_PEAK_G = SIMDS * CLOCK_GHZ / 2.0   # G wave-instructions/s: one VALU issue per 2 cycles per SIMD
+PROFILE_DIR = os.path.join(ROOT, "profiles", "r02")
 
 
 def shard(rank, boards_per_gpu):
@@ -72,7 +82,6 @@ def cpu_baseline(seconds):
     """oracle/port_bench.py: oracle/game_port.py on P processes (one per available CPU, at most
     the box's 16-CPU share) for ~`seconds`, plus a 1-process run -- a bounded sample. Runs as a
     child process before this process initialises the GPU."""
-    import subprocess
     out = subprocess.run([sys.executable, "-m", "oracle.port_bench", "--seconds", str(seconds),
                           "--single-seconds", str(max(1.0, seconds / 2))],
                          cwd=ROOT, capture_output=True, text=True, timeout=seconds * 3 + 120)
@@ -92,36 +101,112 @@ def strong_cpu_line(seconds=2.0):
             "sample": "%d steps, one board, CPython-compatible MT19937 draws" % n}
 
 
-def kernel_events(env, launches, chunk=None):
-    """Per-launch duration of k_step (ms) from HIP events on the env's stream."""
-    s = torch.cuda.current_stream(env.device)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(launches)]
-    for a, b in ev:
+def _load_profile(name):
+    p = os.path.join(PROFILE_DIR, name)
+    return json.load(open(p)) if os.path.exists(p) else None
+
+
+SETTLE_S = 0.3   # minimum untimed stepping before a timed region: GPU clocks ramp over ~20 ms+
+
+
+def timed_steps(env, plan, W, chunk, world, dev):
+    """W untimed warm-up steps through the same path (in calls of the timed chunk size) --
+    continued, still untimed, until at least SETTLE_S of stepping has run -- then exactly sum(plan)
+    steps bracketed by barrier + synchronize. -> (slowest rank's wall seconds, device ms of the
+    timed calls from HIP events on the launch stream, one entry per call)."""
+    t_w = time.perf_counter()
+    for c in chunks(W, chunk) if W else []:
+        env.step_n(c, auto_reset=True)
+    torch.cuda.synchronize(dev)
+    while time.perf_counter() - t_w < SETTLE_S:
+        env.step_n(chunk, auto_reset=True)
+        torch.cuda.synchronize(dev)
+    s = torch.cuda.current_stream(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in plan]
+    for a, b in ev:       # torch creates the HIP events at their first record: not inside the region
         a.record(s)
-        env.step(None, auto_reset=True)
         b.record(s)
-    torch.cuda.synchronize(env.device)
-    return [a.elapsed_time(b) for a, b in ev]
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for (a, b), c in zip(ev, plan):
+        a.record(s)
+        env.step_n(c, auto_reset=True)
+        b.record(s)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    return max_over_ranks(t1 - t0, dev, world), [a.elapsed_time(b) for a, b in ev]
+
+
+def single_step_hbm(dev, seed, n, launches):
+    """k_step (one launch per step, boards read and written through HBM every step): per-launch
+    device time from HIP events over back-to-back launches, after a settle period."""
+    from rein48_amd import VecGame
+    env = VecGame(n, device=dev, seed=seed)
+    env.fill_random(7)
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < SETTLE_S:
+        env.step(None, auto_reset=True)
+        torch.cuda.synchronize(dev)
+    s = torch.cuda.current_stream(dev)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(s)
+    for _ in range(launches):
+        env.step(None, auto_reset=True)
+    b.record(s)
+    torch.cuda.synchronize(dev)
+    ms = a.elapsed_time(b) / launches
+    del env
+    torch.cuda.empty_cache()
+    gbs = n * ALGO_BYTES / (ms * 1e-3) / 1e9
+    name = "pmc_k_step_2p%d.json" % (n.bit_length() - 1)
+    prof = _load_profile(name)
+    return {"kernel": "k_step<RANDOM=1,AUTO_RESET=1,REWARD=0>", "boards": n, "launch_ms": ms,
+            "env_steps_per_s": n / (ms * 1e-3), "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": gbs / HBM_PEAK_GBS, "frac_of_measured_copy_ceiling": gbs / HBM_MEASURED_GBS,
+            "algorithmic_bytes_per_launch": n * ALGO_BYTES,
+            "traffic": prof.get("hbm_bytes_per_launch") if prof else None,
+            "traffic_source": ("profiles/r02/%s (committed rocprofv3 FETCH_SIZE + WRITE_SIZE passes, not "
+                               "measured in this run)" % name) if prof else None}
+
+
+def roofline_step_n(n, dev_ms, steps):
+    """VALU roofline of k_step_n: wave-instructions per board-step from the committed PMC profile
+    (else the static ISA count of the shipped loop) x board-steps / device time."""
+    prof = _load_profile("pmc_k_step_n.json")
+    if prof:
+        per, src = prof["valu_wave_instr_per_board_step"], "profiles/r02/pmc_k_step_n.json (SQ_INSTS_VALU)"
+    else:
+        per, src = 392.0 / 128, "static ISA count of the shipped loop (392 VALU per lane per pair-step)"
+    bsteps_per_s = n * steps / (dev_ms * 1e-3)
+    achieved = per * bsteps_per_s / 1e9
+    out = {"bound": "valu", "achieved": achieved, "peak": VALU_PEAK_G, "unit": "G VALU wave-instr/s",
+           "frac": achieved / VALU_PEAK_G, "traffic": None,
+           "kernel": "k_step_n<RANDOM=1,AUTO_RESET=1,REWARD=0> (board pair per lane in VGPRs for all steps of "
+                     "the call, one Philox4x32-10 call per pair-step)",
+           "valu_wave_instr_per_board_step": per, "valu_count_source": src,
+           "board_steps_timed": n * steps, "device_ms_timed": dev_ms,
+           "peak_note": "1 VALU wave-instruction / 2 cycles / SIMD x 1024 SIMDs x 2.4 GHz; half-rate "
+                        "instructions (v_perm, v_cmp, v_bfi, VOP3 3-input ops, left shifts) take ~4.3 cycles "
+                        "(profiles/r02/instr_rate.txt)"}
+    if prof:
+        out["traffic"] = prof.get("hbm_bytes_per_dispatch")
+        out["traffic_source"] = "profiles/r02/pmc_k_step_n.json (committed, not measured in this run)"
+        cyc = prof.get("modelled_cycles_per_board_step")
+        if cyc:
+            # the instruction mix's own issue ceiling: modelled SIMD cycles per board-step (per-
+            # instruction issue costs measured in profiles/r02/instr_rate.txt) at 2.4 GHz
+            model_ms = cyc * n * steps / SIMDS / (CLOCK_GHZ * 1e9) * 1e3
+            out["frac_of_mix_issue_ceiling"] = model_ms / dev_ms
+    return out
 
 
 def extras(dev, seed, n_small):
     from rein48_amd import VecGame
     out = {}
-    # HBM-honest: 2^26 boards (1 GiB of boards) -- far beyond the 256 MiB Infinity Cache
-    big = 1 << 26
-    env = VecGame(big, device=dev, seed=seed)
-    env.fill_random(7)
-    K = 200
-    el, gpu_ms = timed_steps(env, [K], 50, K, 1, dev)
-    ms = kernel_events(env, 20)
-    step_ms = gpu_ms / K
-    out["hbm_honest"] = {"boards": big, "steps": K, "step_ms_graph_replay": step_ms,
-                         "env_steps_per_s": big * K / el,
-                         "achieved_GBs": big * ALGO_BYTES / (step_ms * 1e-3) / 1e9,
-                         "frac_of_peak": big * ALGO_BYTES / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                         "single_launch_ms_eager_avg": sum(ms) / len(ms)}
-    del env
-    torch.cuda.empty_cache()
     # fused rollout: K steps per launch with the per-step trajectory (action, done) written
     env = VecGame(n_small, device=dev, seed=seed)
     env.reset()
@@ -150,9 +235,16 @@ def _sync_max(ms_list, dev, world):
     return max_over_ranks(sum(ms_list) / len(ms_list), dev, world)
 
 
+def _allreduce_label(world):
+    if world <= 1:
+        return None
+    b = dist.get_backend()
+    return "%s all_reduce(SUM)/world" % ("RCCL (torch backend 'nccl')" if b == "nccl" else "torch backend '%s'" % b)
+
+
 def a3c_config3(dev, seed, n_boards, updates=2, world=1):
     """BASELINE configs[2] (world 1: 2^20 boards + 2-layer CNN policy on 1 MI355X) and configs[3]
-    (world > 1: 2^20 boards per GPU, 8M boards on 8 GPUs, one RCCL all-reduce of the flat fp32
+    (world > 1: 2^20 boards per GPU, 8M boards on 8 GPUs, one all-reduce of the flat fp32
     gradient per update): A3C rollout (MAX_STEP_NUM = 100 steps: fused CNN inference + softmax +
     Philox sampling -> env kernel) and the synchronous update (fused MFMA gradient pass,
     all-reduce, TF1 RMSProp kernel)."""
@@ -179,10 +271,10 @@ def a3c_config3(dev, seed, n_boards, updates=2, world=1):
         steps += int(tr.lengths.sum())
     r, u = _sync_max(roll_ms, dev, world), _sync_max(upd_ms, dev, world)
     board_steps = world * n_boards * cfg.max_steps  # every board is stepped every rollout step
+    lab = _allreduce_label(world)
     return {"boards": world * n_boards, "boards_per_gpu": n_boards, "n_gpus": world,
             "net": "cnn (conv2x2x32, conv2x2x64, heads 256->4/1), bf16",
-            "gradient_allreduce": ("RCCL all_reduce(SUM)/world of %d fp32 per update" % tr.flat.grad.numel())
-            if world > 1 else None,
+            "gradient_allreduce": ("%s of %d fp32 per update" % (lab, tr.flat.grad.numel())) if lab else None,
             "rollout_ms": r, "update_ms": u,
             "rollout_env_steps_per_s": board_steps / (r * 1e-3),
             "train_env_steps_per_s": board_steps / ((r + u) * 1e-3),
@@ -194,8 +286,8 @@ def dqn_config5(dev, seed, n_boards, steps=3, world=1):
     """BASELINE configs[4] (16M boards over 8 GPUs = 2^21 per GPU): ResNet-10 Q-network in bf16
     (fused MFMA inference kernel for acting, structured-GEMM training path), epsilon-greedy acting
     on every board, env step with merge reward + auto-reset, (s, a, r, s', done) of every board
-    into the HBM replay ring, one 64K-transition double-DQN update per env step (gradient
-    all-reduced over RCCL when world > 1; each rank samples its own ring shard)."""
+    into the HBM replay ring, one 64K-transition double-DQN update per env step (gradient and BN
+    running statistics all-reduced when world > 1; each rank samples its own ring shard)."""
     from rein48_amd.dqn import DQNConfig, DQNTrainer
     cfg = DQNConfig(n_boards=n_boards, replay_capacity=1 << 25, batch=1 << 16, learn_start=1, seed=seed,
                     act_chunk=1 << 18)
@@ -225,11 +317,12 @@ def dqn_config5(dev, seed, n_boards, steps=3, world=1):
     a_ms, e_ms, u_ms = (_sync_max(x, dev, world) for x in (act, env, upd))
     C = cfg.channels
     useful = 2 * 100 * (18 * C + 2 * cfg.blocks * C * C) + 2 * 16 * C * 4     # valid taps only
+    lab = _allreduce_label(world)
     return {"boards": world * n_boards, "boards_per_gpu": n_boards, "n_gpus": world,
             "net": "ResNet-10 (stem + 4 basic blocks, C=%d, BN) bf16" % C,
             "replay_capacity_per_gpu": cfg.replay_capacity, "batch_per_gpu": cfg.batch,
-            "gradient_allreduce": ("RCCL all_reduce(SUM)/world of %d fp32 per update" % tr.flat.grad.numel())
-            if world > 1 else None,
+            "gradient_allreduce": ("%s of %d fp32 per update (+ %d BN running-statistics floats)"
+                                   % (lab, tr.flat.grad.numel(), tr.bn_buffers.data.numel())) if lab else None,
             "act_ms": a_ms, "env_step_store_ms": e_ms, "update_ms": u_ms,
             "env_steps_per_s": world * n_boards / ((a_ms + e_ms + u_ms) * 1e-3),
             "act_useful_TFLOPs": n_boards * useful / (a_ms * 1e-3) / 1e12,
@@ -237,48 +330,45 @@ def dqn_config5(dev, seed, n_boards, steps=3, world=1):
             "loss": out["loss"]}
 
 
-def traffic_from_profile(n_boards):
-    p = os.path.join(ROOT, "profiles", "pmc_k_step.json")
-    if not os.path.exists(p):
-        return None
-    d = json.load(open(p))
-    if int(d.get("boards", -1)) != n_boards:
-        return None
-    return d.get("hbm_bytes_per_step")
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
 
 
-SETTLE_S = 0.3   # minimum untimed stepping before a timed region: GPU clocks ramp over ~20 ms+
+def launch_ranks(n):
+    """`--gpus N` without torchrun: run torchrun (one rank per GPU) as a CHILD process -- this
+    process never touches the GPU -- and return its exit status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % n,
+           "--master-addr=127.0.0.1", "--master-port=%d" % _free_port(), os.path.abspath(__file__)] + sys.argv[1:]
+    print("bench.py: --gpus %d without WORLD_SIZE -> %s" % (n, " ".join(cmd)), file=sys.stderr, flush=True)
+    return subprocess.call(cmd)
 
 
-def timed_steps(env, plan, W, chunk, world, dev):
-    """W untimed warm-up steps through the same replay path (in chunks of the timed chunk
-    size, so the timed region replays graphs that have already run) -- continued, still untimed,
-    until at least SETTLE_S of stepping has run -- then exactly sum(plan) steps bracketed by
-    barrier + synchronize. -> (slowest rank's wall seconds, device ms from HIP events on the
-    launch stream)."""
-    t_w = time.perf_counter()
-    for c in chunks(W, chunk) if W else []:
-        env.step_n(c, auto_reset=True)
-    if W:
-        torch.cuda.synchronize(dev)
-        while time.perf_counter() - t_w < SETTLE_S:
-            env.step_n(chunk, auto_reset=True)
-            torch.cuda.synchronize(dev)
-    s = torch.cuda.current_stream(dev)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in plan]
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for (a, b), c in zip(ev, plan):
-        a.record(s)
-        env.step_n(c, auto_reset=True)
-        b.record(s)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
-    return max_over_ranks(t1 - t0, dev, world), sum(a.elapsed_time(b) for a, b in ev)
+def run_extras_all_ranks(world, rank, items):
+    """Trainer extras on every rank (each issues collectives). After each one every rank posts
+    its status to the rendezvous store and reads everyone's; on any failure the remaining extras
+    are skipped on all ranks, so no rank enters a collective its peers will never join. (A rank
+    that fails INSIDE a collective leaves its peers blocked until the process group's timeout.)"""
+    store = dist.distributed_c10d._get_default_store()
+    ex = {}
+    for i, (key, fn) in enumerate(items):
+        try:
+            ex[key] = fn()
+            ok = b"1"
+        except Exception as e:      # recorded in the line; the check below keeps the ranks in step
+            ex[key] = {"error": repr(e)}
+            ok = b"0"
+        store.set("r48/%s/%d" % (key, rank), ok)
+        keys = ["r48/%s/%d" % (key, r) for r in range(world)]
+        store.wait(keys, datetime.timedelta(seconds=900))
+        if any(store.get(k) != b"1" for k in keys):
+            if ok == b"1":
+                ex[key]["error"] = "failed on another rank"
+            for k2, _ in items[i + 1:]:
+                ex[k2] = {"skipped": "an earlier extra failed on some rank"}
+            break
+    return ex
 
 
 def main():
@@ -289,30 +379,35 @@ def main():
                     help="untimed steps; stepping continues untimed until %.0f ms have run (GPU clock ramp)"
                     % (SETTLE_S * 1e3))
     ap.add_argument("--boards", type=int, default=1 << 20, help="boards per GPU")
-    ap.add_argument("--chunk", type=int, default=4096, help="max steps per r48_env_step_n call (<= 4096)")
+    ap.add_argument("--chunk", type=int, default=0, help="steps per r48_env_step_n call (0 = all K in one call)")
     ap.add_argument("--seed", type=int, default=0x20485EED)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
-    if world != args.gpus and not (world == 1 and args.gpus == 1):
-        print("warning: --gpus %d but WORLD_SIZE=%d; using WORLD_SIZE" % (args.gpus, world), file=sys.stderr)
+    if world != args.gpus:
+        print("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world), file=sys.stderr)
+        sys.exit(2)
     cpu_line = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu_line = cpu_baseline(args.cpu_seconds)          # before this process touches the GPU
     # R48_DIST_BACKEND=gloo only rehearses several ranks sharing one GPU (RCCL refuses two ranks
     # on one device); the product path is RCCL ("nccl" on ROCm), one rank per GPU
     backend = os.environ.get("R48_DIST_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
     if backend != "nccl":
-        local %= max(1, torch.cuda.device_count())
+        local %= max(1, ndev)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group(backend, device_id=dev if backend == "nccl" else None)
+        dist.init_process_group(backend, device_id=dev if backend == "nccl" else None,
+                                timeout=datetime.timedelta(seconds=900))
 
     from rein48_amd import VecGame
 
@@ -320,18 +415,10 @@ def main():
     offset, n = shard(rank, n)
     env = VecGame(n, device=dev, seed=args.seed, board_offset=offset)
     env.fill_random(7)                                    # SURVEY.md 8(d) synthetic start boards
-    chunk = max(1, min(args.chunk, K, 4096))
+    chunk = K if args.chunk <= 0 else max(1, min(args.chunk, K))
     plan = chunks(K, chunk)
-    elapsed, gpu_ms = timed_steps(env, plan, W, chunk, world, dev)
-    step_ms_dev = gpu_ms / K                              # per step (all boards), device time
-
-    # per-launch kernel duration (eager launches of the same kernel, HIP events per launch)
-    ms = kernel_events(env, 50)
-    kern_ms = sorted(ms)[len(ms) // 2]
-
+    elapsed, dev_ms = timed_steps(env, plan, W, chunk, world, dev)
     value = world * n * K / elapsed
-    bytes_per_launch = n * ALGO_BYTES
-    achieved = bytes_per_launch / (step_ms_dev * 1e-3) / 1e9
     line = {
         "metric": METRIC,
         "value": value,
@@ -348,55 +435,49 @@ def main():
                 "r48_env_fill_random), in-kernel uniform random policy and spawns from Philox4x32-10, "
                 "auto-reset on game over",
         "config": {"workload": "BASELINE configs[1]: 2^20 4x4 int8 boards per GPU, random policy, env-only",
-                   "boards_per_gpu": n, "global_boards": n * world, "parallelism": "env shards x%d, no collective"
-                   % world, "graph_chunk": chunk},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic_from_profile(n),
-                     "kernel": "k_step<RANDOM=1,AUTO_RESET=1,REWARD=0,NP=1> (one board pair per lane, "
-                               "one Philox4x32-10 call per pair)",
-                     "algorithmic_bytes_per_step": bytes_per_launch,
-                     "step_ms_device_events_timed_region": step_ms_dev,
-                     "chains": 2 if n >= (1 << 18) else 1,
-                     "single_launch_ms_eager_events_median": kern_ms,
-                     "frac_of_measured_copy_ceiling": achieved / HBM_MEASURED_GBS},
+                   "boards_per_gpu": n, "global_boards": n * world,
+                   "parallelism": "env shards x%d, no collective" % world,
+                   "steps_per_launch": chunk, "launches": len(plan),
+                   "world_size": dist.get_world_size() if world > 1 else 1,
+                   "dist_backend": dist.get_backend() if world > 1 else None,
+                   "visible_devices": ndev},
+        "roofline": roofline_step_n(n, sum(dev_ms), K),
     }
     if cpu_line is not None:
         line["cpu_baseline"] = cpu_line
     if rank == 0 and world == 1 and not args.no_extras:
+        # the single-step HBM kernel: at 2^20 (cache-resident) and 2^26 boards (1 GiB, past the
+        # 256 MiB Infinity Cache: the HBM-honest point)
+        line["roofline"]["hbm"] = {"k_step_2p20": single_step_hbm(dev, args.seed, 1 << 20, 400),
+                                   "k_step_2p26": single_step_hbm(dev, args.seed, 1 << 26, 30)}
         ex = extras(dev, args.seed, n)
-        # median of 5 repeats of the same K-step region, and the reference
+        # 5 repeats of the same K-step region (each re-warmed), and the reference
         # reset-distribution start (one tile per board) instead of the synthetic fill
-        reps = [timed_steps(env, plan, chunk, chunk, world, dev)[0] for _ in range(5)]   # each re-warmed
-        ex["repeat_5"] = {"values": [n * K / r for r in reps], "median": n * K / sorted(reps)[2]}
+        reps = [timed_steps(env, plan, chunk, chunk, world, dev)[0] for _ in range(5)]
+        vals = [n * K / r for r in reps]
+        ex["repeat_5"] = {"values": vals, "median": sorted(vals)[2],
+                          "spread": (max(vals) - min(vals)) / sorted(vals)[2]}
         env2 = VecGame(n, device=dev, seed=args.seed, board_offset=offset)
         env2.reset()
         el2, _ = timed_steps(env2, plan, W, chunk, world, dev)
         ex["reset_start"] = {"value": n * K / el2, "note": "boards start from Game.reset (one 2/4 tile)"}
         del env2
-        try:
-            ex["a3c_config3"] = a3c_config3(dev, args.seed, n)
-        except Exception as e:  # the env bench line must print even if the trainer fails
-            ex["a3c_config3"] = {"error": repr(e)}
-        try:
-            ex["dqn_config5"] = dqn_config5(dev, args.seed, 1 << 21)
-        except Exception as e:
-            ex["dqn_config5"] = {"error": repr(e)}
+        for key, fn in (("a3c_config3", lambda: a3c_config3(dev, args.seed, n)),
+                        ("dqn_config5", lambda: dqn_config5(dev, args.seed, 1 << 21))):
+            try:
+                ex[key] = fn()
+            except Exception as e:  # one rank: the env bench line must print even if a trainer fails
+                ex[key] = {"error": repr(e)}
         if not args.no_cpu_baseline:
             ex["cpu_strong_line"] = strong_cpu_line()
         line["extras"] = ex
     if world > 1 and not args.no_extras:
         # BASELINE configs[3] (A3C, 2^20 boards per GPU: 8M on 8 GPUs) and configs[4] (DQN,
         # 2^21 boards per GPU: 16M on 8 GPUs), every rank stepping its own shard, gradients
-        # all-reduced over RCCL. Every rank issues the same collective sequence (barriers, one
-        # broadcast per trainer, one all-reduce per update, max-reductions of the phase times).
-        ex = {}
-        for key, fn in (("a3c_config4", lambda: a3c_config3(dev, args.seed, n, world=world)),
-                        ("dqn_config5", lambda: dqn_config5(dev, args.seed, 1 << 21, world=world))):
-            try:              # the env bench line must print even if a trainer fails (on every rank alike)
-                ex[key] = fn()
-            except Exception as e:
-                ex[key] = {"error": repr(e)}
-        line["extras"] = ex
+        # all-reduced over the process group's backend
+        line["extras"] = run_extras_all_ranks(world, rank, [
+            ("a3c_config4", lambda: a3c_config3(dev, args.seed, n, world=world)),
+            ("dqn_config5", lambda: dqn_config5(dev, args.seed, 1 << 21, world=world))])
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

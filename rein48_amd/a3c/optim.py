@@ -48,6 +48,41 @@ class FlatParams:
             dist.broadcast(self.data, src=src, group=group)
 
 
+class FlatBuffers:
+    """The floating-point buffers of a module (BatchNorm running_mean / running_var) re-pointed at
+    views of ONE contiguous buffer. Each replica updates them from its own minibatch; averaging
+    them over the group after every update (one all-reduce) keeps the replicas identical -- the
+    running statistics are a linear function of the batch statistics, so the average equals what
+    one replica would hold after the same update on the union of the minibatches' means. Integer
+    buffers (num_batches_tracked) advance identically on every replica and are left alone."""
+
+    def __init__(self, module):
+        bufs = [b for b in module.buffers() if b.is_floating_point()]
+        self.buffers = bufs
+        if not bufs:
+            self.data = torch.zeros(0)
+            return
+        dev, dt = bufs[0].device, bufs[0].dtype
+        self.data = torch.zeros(sum(b.numel() for b in bufs), dtype=dt, device=dev)
+        off = 0
+        for b in bufs:
+            k = b.numel()
+            self.data[off:off + k].copy_(b.data.view(-1))
+            b.data = self.data[off:off + k].view_as(b)
+            off += k
+
+    def allreduce_mean_(self, group=None):
+        if self.data.numel() and dist.is_available() and dist.is_initialized():
+            world = dist.get_world_size(group)
+            if world > 1:
+                dist.all_reduce(self.data, op=dist.ReduceOp.SUM, group=group)
+                self.data.div_(world)
+
+    def broadcast_(self, src=0, group=None):
+        if self.data.numel() and dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+            dist.broadcast(self.data, src=src, group=group)
+
+
 class RMSPropTF1:
     """tf.train.RMSPropOptimizer semantics: ms slot initialised to ONES, eps inside the sqrt,
     decay 0.9, momentum 0 (a3c.py:264-265 uses the defaults with lr 1e-3)."""

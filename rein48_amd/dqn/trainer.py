@@ -12,7 +12,9 @@ One train_step per env step, per GPU:
            For a done board s' is the auto-reset board: the target masks it, (1 - done)
   update   `updates_per_step` minibatches sampled uniformly from the ring, TD target from the
            target net (double DQN by default; r48_td_target), Huber loss, ONE all-reduce of
-           the flat fp32 gradient across GPUs (RCCL), Adam; target net synced every
+           the flat fp32 gradient across GPUs (RCCL), Adam, ONE all-reduce-mean of the BN
+           running statistics (so the eval-mode nets, whose BN is folded into the acting
+           kernel's weights, stay identical on every rank); target net synced every
            `target_sync` updates
 Rewards enter the loss as log2(1 + merged value) (reward_transform="log2") or raw.
 Each rank owns boards [rank*N, (rank+1)*N) and its own ring shard; no replay traffic crosses
@@ -26,7 +28,7 @@ import torch
 import torch.distributed as dist
 import torch.nn.functional as F
 
-from ..a3c.optim import FlatParams
+from ..a3c.optim import FlatBuffers, FlatParams
 from ..env import VecGame
 from ..replay import ReplayStore
 from .kernels import board_onehot, egreedy_actions, td_target
@@ -77,32 +79,67 @@ class Adam:
         self.flat.data.addcdiv_(self.m, denom, value=-self.lr / c1)
 
 
-class DQNTrainer:
+class DQNLearner:
+    """The data-parallel learning half of DQN: online and target ResNet-10, flat parameters and
+    gradient (one all-reduce), Adam, the BN running statistics as one flat buffer (one
+    all-reduce-mean per update). Device-agnostic -- tests/test_dqn.py runs two gloo ranks of it on
+    the CPU; DQNTrainer adds the GPU env, the replay ring and the fused kernels."""
+
     def __init__(self, cfg: DQNConfig, device="cuda:0"):
         self.cfg = cfg
         self.device = torch.device(device)
         self.rank = dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
+        torch.manual_seed(cfg.seed)                       # identical init on every replica
+        dt = torch.bfloat16 if cfg.bf16 else torch.float32
+        self.net = ResNet10Q(cfg.channels, cfg.blocks, cfg.bn, dtype=dt).to(self.device)
+        self.flat = FlatParams(self.net)
+        self.bn_buffers = FlatBuffers(self.net)
+        self.flat.broadcast_()                            # rank 0's replica everywhere
+        self.bn_buffers.broadcast_()
+        self.target = copy.deepcopy(self.net).eval()
+        for p in self.target.parameters():
+            p.requires_grad_(False)
+        self.opt = Adam(self.flat, cfg.lr)
+        self.updates = 0
+        self._version = 0                                 # bumped by every optimizer step / sync
+
+    def learn(self, x, action, y):
+        """One synchronous step: Huber loss of Q(x)[action] against the TD target y, gradient
+        averaged over the group, Adam, BN running statistics averaged over the group; the target
+        net follows every `target_sync` updates."""
+        self.net.train()
+        self.flat.zero_grad()
+        q = self.net(x)
+        q_sa = q.gather(1, action.long().view(-1, 1)).squeeze(1)
+        loss = F.smooth_l1_loss(q_sa, y)
+        loss.backward()
+        self.flat.allreduce_grad()
+        self.opt.step()
+        self.bn_buffers.allreduce_mean_()
+        self._version += 1
+        self.updates += 1
+        if self.updates % self.cfg.target_sync == 0:
+            self.sync_target()
+        return {"loss": float(loss.detach()), "q_mean": float(q_sa.detach().mean())}
+
+    def sync_target(self):
+        self.target.load_state_dict(self.net.state_dict())
+        self._version += 1
+
+
+class DQNTrainer(DQNLearner):
+    def __init__(self, cfg: DQNConfig, device="cuda:0"):
+        super().__init__(cfg, device)
         n = cfg.n_boards
         self.env = VecGame(n, device=self.device, seed=cfg.seed, board_offset=self.rank * n)
         self.env.reset()
         self.replay = ReplayStore(cfg.replay_capacity, self.device, mode="ring",
                                   seed=(cfg.seed * 0x9E3779B97F4A7C15 + self.rank + 1) & (2 ** 64 - 1))
-        torch.manual_seed(cfg.seed)                       # identical init on every replica
-        dt = torch.bfloat16 if cfg.bf16 else torch.float32
-        self.net = ResNet10Q(cfg.channels, cfg.blocks, cfg.bn, dtype=dt).to(self.device)
-        self.target = copy.deepcopy(self.net).eval()
-        for p in self.target.parameters():
-            p.requires_grad_(False)
-        self.flat = FlatParams(self.net)
-        self.flat.broadcast_()
-        self.opt = Adam(self.flat, cfg.lr)
         self.steps = 0
-        self.updates = 0
         self.q = torch.empty((n, 4), dtype=torch.float32, device=self.device)
         self.actions = torch.empty(n, dtype=torch.int8, device=self.device)
         self.use_fused = cfg.fused and cfg.bf16 and cfg.channels == 64 and cfg.blocks == 4
         self._packed = {}                                   # id(net) -> (version, packed weights)
-        self._version = 0                                   # bumped by every optimizer step / sync
 
     def epsilon(self):
         c = self.cfg
@@ -175,23 +212,9 @@ class DQNTrainer:
             qt = self.q_eval(self.target, b["next_state"]).contiguous()
             qo = self.q_eval(self.net, b["next_state"]).contiguous() if c.double else None
             y = td_target(self._reward(b["reward"]).contiguous(), b["done"], qt, qo, c.gamma)
-        self.net.train()
-        self.flat.zero_grad()
-        q = self.net(x)
-        q_sa = q.gather(1, b["action"].long().view(-1, 1)).squeeze(1)
-        loss = F.smooth_l1_loss(q_sa, y)
-        loss.backward()
-        self.flat.allreduce_grad()
-        self.opt.step()
-        self._version += 1
-        self.updates += 1
-        if self.updates % c.target_sync == 0:
-            self.sync_target()
-        return {"loss": float(loss.detach()), "q_mean": float(q_sa.detach().mean()), "batch": b}
-
-    def sync_target(self):
-        self.target.load_state_dict(self.net.state_dict())
-        self._version += 1
+        out = self.learn(x, b["action"], y)
+        out["batch"] = b
+        return out
 
     def train_step(self):
         reward, done = self.env_step()

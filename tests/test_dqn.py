@@ -155,3 +155,119 @@ def test_fused_kernel_packing_layout_cpu():
         want = H[r, 64 * p + ci] if r < 4 else 0.0
         assert blob[head + 2 * p + c, l, j] == bf(want)
     torch.testing.assert_close(pack_resnet(net).view(-1, 512)[head + 32].view(torch.float32)[:4], hb.detach(), rtol=0, atol=0)
+
+
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _dqn_learner_worker(rank, world, port, q):
+    """One rank of the DQN learner (rein48_amd/dqn/trainer.py:DQNLearner) on the CPU over gloo."""
+    import copy
+    import os
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from rein48_amd.dqn import DQNConfig, DQNLearner
+        cfg = DQNConfig(channels=8, blocks=2, bf16=False, seed=100 + rank, target_sync=2, lr=1e-3)
+        lr = DQNLearner(cfg, device="cpu")             # different seeds: the broadcast makes them equal
+        init = lr.flat.data.numpy().copy()
+        g = torch.Generator().manual_seed(7 + rank)     # each rank its own minibatch
+        B = 32
+        x = F.one_hot(torch.randint(0, 18, (B, 16), generator=g), 18).float().view(B, 16 * 18)
+        a = torch.randint(0, 4, (B,), generator=g, dtype=torch.int8)
+        y = torch.randn(B, generator=g)
+        out1 = lr.learn(x, a, y)
+        out2 = lr.learn(x, a, y)                        # second update: target sync (target_sync = 2)
+        folded, head = lr.net.eval().folded()
+        fold = np.concatenate([t.detach().numpy().ravel() for wb in folded for t in wb] + [t.detach().numpy().ravel() for t in head])
+        tgt = torch.cat([p.detach().view(-1) for p in lr.target.parameters()]).numpy().copy()
+        q.put((rank, init, None, None, lr.flat.grad.numpy().copy(), lr.flat.data.numpy().copy(),
+               lr.bn_buffers.data.numpy().copy(), fold, tgt, out1["loss"], out2["loss"], lr.updates))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_dqn_learner_gloo():
+    """DQN's multi-rank sequence on two gloo ranks: rank 0's initial weights broadcast, ONE
+    all-reduce of the flat gradient (= the mean of the ranks' local gradients), an identical Adam
+    step, the BN running statistics averaged over the ranks, so the BN-folded eval weights (the
+    fused acting kernel's input) and the target net are identical on every rank."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dqn_learner_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=90) for _ in range(2)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    r0, r1 = res
+    np.testing.assert_array_equal(r0[1], r1[1])                           # broadcast initial weights
+    np.testing.assert_array_equal(r0[5], r1[5])                           # parameters after 2 updates
+    np.testing.assert_array_equal(r0[4], r1[4])                           # last averaged gradient
+    np.testing.assert_array_equal(r0[6], r1[6])                           # BN running statistics
+    np.testing.assert_array_equal(r0[7], r1[7])                           # folded eval weights
+    np.testing.assert_array_equal(r0[8], r1[8])                           # target net (synced at update 2)
+    np.testing.assert_array_equal(r0[8], r0[5])                           # target == online after the sync
+    assert r0[11] == r1[11] == 2
+    assert np.isfinite(r0[9]) and np.isfinite(r1[10])
+
+
+def _dqn_first_update_worker(rank, world, port, q):
+    import copy
+    import os
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from rein48_amd.dqn import DQNConfig, DQNLearner
+        cfg = DQNConfig(channels=8, blocks=2, bf16=False, seed=100 + rank, lr=1e-3)
+        lr = DQNLearner(cfg, device="cpu")
+        g = torch.Generator().manual_seed(7 + rank)
+        B = 32
+        x = F.one_hot(torch.randint(0, 18, (B, 16), generator=g), 18).float().view(B, 16 * 18)
+        a = torch.randint(0, 4, (B,), generator=g, dtype=torch.int8)
+        y = torch.randn(B, generator=g)
+        # what this rank alone would compute: local gradient (the conv biases feeding a BN get none,
+        # like the flat buffer's zeros) and local BN running statistics
+        twin = copy.deepcopy(lr.net).train()
+        for p in twin.parameters():
+            p.grad = None
+        qs = twin(x).gather(1, a.long().view(-1, 1)).squeeze(1)
+        F.smooth_l1_loss(qs, y).backward()
+        local_g = torch.cat([(p.grad if p.grad is not None else torch.zeros_like(p)).view(-1)
+                             for p in twin.parameters() if p.requires_grad]).numpy().copy()
+        local_bn = torch.cat([b.view(-1) for b in twin.buffers() if b.is_floating_point()]).numpy().copy()
+        lr.learn(x, a, y)
+        q.put((rank, local_g, local_bn, lr.flat.grad.numpy().copy(), lr.bn_buffers.data.numpy().copy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_dqn_first_update_averages_gradient_and_bn_stats():
+    """After one update on two gloo ranks: flat gradient == mean of the ranks' local gradients, BN
+    running statistics == mean of what each rank's own forward would have left."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dqn_first_update_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=90) for _ in range(2)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (_, g0, b0, G0, B0), (_, g1, b1, G1, B1) = res
+    np.testing.assert_allclose(G0, (g0 + g1) / 2, rtol=1e-5, atol=1e-7)
+    np.testing.assert_array_equal(G0, G1)
+    np.testing.assert_allclose(B0, (b0 + b1) / 2, rtol=1e-6, atol=1e-7)
+    np.testing.assert_array_equal(B0, B1)
+    assert not np.allclose(b0, b1)          # the ranks' own statistics did differ
