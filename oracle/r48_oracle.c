@@ -191,6 +191,29 @@ ORC_API int orc_spawn(int8_t *b, int rank, int four)
     return -1;
 }
 
+/* The build's Philox-mode spawn: the same uniform choice among the
+ * blanks, counted in LINE order for action a instead of row-major: k = 0..3 cells from the
+ * wall the tiles moved toward, then line l = 0..3 -- cell (k, l) is (row k, col l) for UP,
+ * (row 3-k, col l) DOWN, (row l, col k) LEFT, (row l, col 3-k) RIGHT. */
+ORC_API int orc_spawn_lines(int8_t *b, int a, int rank, int four)
+{
+    int seen = 0;
+    for (int k = 0; k < 4; k++)
+        for (int l = 0; l < 4; l++) {
+            int r = a == 0 ? k : a == 1 ? 3 - k : l;
+            int c = a < 2 ? l : a == 2 ? k : 3 - k;
+            int cell = 4 * r + c;
+            if (b[cell] == 0) {
+                if (seen == rank) {
+                    b[cell] = four ? 2 : 1;
+                    return cell;
+                }
+                seen++;
+            }
+        }
+    return -1;
+}
+
 /* ------------------------------------------------------------------------------------
  * CPython `random` (Python 3.10, Modules/_randommodule.c + Lib/random.py semantics):
  * MT19937 seeded by init_by_array over the 32-bit words of abs(seed), getrandbits(k<=32) =
@@ -379,7 +402,8 @@ static inline uint32_t mulhi32(uint32_t a, uint32_t b)
 /* Batched step in the kernel's Philox mode (r48_env_step; draw contract in DESIGN.md section 7):
  * boards with global ids 2q and 2q+1 share Philox4x32-10({q lo, q hi, step, 0x2048}); the even
  * board takes (x, y) = (w0, w1), the odd one (w2, w3). action = x >> 30, spawn a 4 iff
- * (x & 0x3FFFFFFF) < 0x06666666, blank rank = mulhi(y, n_blank), auto-reset cell = y >> 28 with
+ * (x & 0x3FFFFFFF) < 0x06666666, blank rank = mulhi(y, n_blank) with the blanks in line order
+ * (orc_spawn_lines), auto-reset cell = y >> 28 (row-major) with
  * a 4 iff (y & 0x0FFFFFFF) < 0x0199999A. actions are read, or written in random-policy mode.
  * Outputs may be NULL. Returns the number of boards with a bad action. */
 ORC_API int64_t orc_step_philox(int8_t *boards, int64_t n, uint64_t seed, int64_t board_offset,
@@ -409,9 +433,9 @@ ORC_API int64_t orc_step_philox(int8_t *boards, int64_t n, uint64_t seed, int64_
             bad++;
             c = 0;
         }
-        if (c) {
+        if (c) {   /* c > 0 implies 0 <= a < 4 */
             int nb = orc_blank_count(b);
-            orc_spawn(b, (int)mulhi32(y, (uint32_t)nb), (x & 0x3FFFFFFFu) < 0x06666666u);
+            orc_spawn_lines(b, a, (int)mulhi32(y, (uint32_t)nb), (x & 0x3FFFFFFFu) < 0x06666666u);
         }
         int d = orc_game_over(b);
         if (score) {

@@ -71,18 +71,35 @@ R48_HD uint32_t popc(uint32_t x)
 
 R48_HD uint32_t mulhi(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a * b) >> 32); }
 
+// v_bitop3_b32: any bitwise function of three words in ONE full-rate instruction (truth table
+// TT, bit index 4*a + 2*b + c). The compiler otherwise picks half-rate forms for some of them
+// (v_bfi_b32 for selects, v_or3_b32; measured issue costs in profiles/r02/instr_rate.txt).
+template <unsigned TT>
+R48_HD uint32_t bitop3(uint32_t a, uint32_t b, uint32_t c)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_bitop3_b32(a, b, c, TT);
+#else
+    uint32_t r = 0;
+    for (int i = 0; i < 8; i++)
+        if ((TT >> i) & 1u)
+            r |= ((i & 4) ? a : ~a) & ((i & 2) ? b : ~b) & ((i & 1) ? c : ~c);
+    return r;
+#endif
+}
+// bytewise select m ? x : y (one v_bitop3_b32)
+R48_HD uint32_t bsel(uint32_t m, uint32_t x, uint32_t y) { return bitop3<0xCAu>(m, x, y); }
+R48_HD uint32_t or3(uint32_t a, uint32_t b, uint32_t c) { return bitop3<0xFEu>(a, b, c); }
+
 // Byte-lane predicates, valid while every byte is <= 0x80 (cell exponents are 0..30):
 // 0x80 in each byte that is nonzero / zero.
 R48_HD uint32_t nz80(uint32_t x) { return (x + 0x7F7F7F7Fu) & 0x80808080u; }
 R48_HD uint32_t z80(uint32_t x) { return ~(x + 0x7F7F7F7Fu) & 0x80808080u; }
-// Bit 7 of each byte -> 0xFF/0x00 byte mask (other bits ignored): v_perm_b32's selectors
-// 8..11 replicate the sign bit of pool bytes 1, 3, 5, 7; with pool {f<<8 : f} those are
-// f's bytes 1, 3, 0, 2.  Two instructions (shift + perm).
-R48_HD uint32_t ff(uint32_t f) { return perm(f << 8, f, 0x090B080Au); }
-// 0xFF in each nonzero byte of x (bytes <= 0x80): add + shift + perm
-R48_HD uint32_t nzff(uint32_t x) { return ff(x + 0x7F7F7F7Fu); }
-// bytewise select: m ? x : y   (v_bfi_b32)
-R48_HD uint32_t bsel(uint32_t m, uint32_t x, uint32_t y) { return (x & m) | (y & ~m); }
+// Bit-7 flags f -> 0x7F byte masks (f - f >> 7: two full-rate instructions). A 0x7F mask selects
+// a whole cell: cells are exponents <= 30, so bit 7 of every board byte is 0.
+R48_HD uint32_t m7f(uint32_t f) { return f - (f >> 7); }
+// 0x7F in each nonzero byte of x (bytes <= 0x80)
+R48_HD uint32_t nz7f(uint32_t x) { return m7f(nz80(x)); }
 
 // Four row words as named scalars (no arrays: a selected array index would be lowered to
 // a dynamically indexed private array, which hipcc promotes to LDS).
@@ -123,58 +140,62 @@ R48_HD Board from_lines(const Board &l, uint32_t a)
 }
 
 // Slide + merge all four lines toward L[0]. Returns the merge reward (sum of merged tile
-// values) when REWARD, else 0.
+// values) when REWARD, else 0. Every instruction is full rate (add/sub/shift/bitop3; byte masks
+// are 0x7F from m7f, not 0xFF from v_perm): ~50 VALU for all four lines.
 template <bool REWARD>
 R48_HD uint32_t move_lines(Board &L)
 {
     uint32_t l0 = L.w0, l1 = L.w1, l2 = L.w2, l3 = L.w3;
     // (1) compaction, from the far side in: where line cell i is empty, the cells behind it
     //     shift one place toward L[0] (GameClient.py:147-160: j skips empties, i takes j).
-    uint32_t k = nzff(l2);
+    //     Where cell i is empty it is 0, so "i takes i+1" is i | (i+1 & ~k).
+    uint32_t k = nz7f(l2);
+    l2 = bitop3<0xF4u>(l2, l3, k);   // l2 | (l3 & ~k)
+    l3 &= k;
+    k = nz7f(l1);
+    l1 = bitop3<0xF4u>(l1, l2, k);
     l2 = bsel(k, l2, l3);
     l3 &= k;
-    k = nzff(l1);
-    l1 = bsel(k, l1, l2);
-    l2 = bsel(k, l2, l3);
-    l3 &= k;
-    k = nzff(l0);
-    l0 = bsel(k, l0, l1);
+    k = nz7f(l0);
+    l0 = bitop3<0xF4u>(l0, l1, k);
     l1 = bsel(k, l1, l2);
     l2 = bsel(k, l2, l3);
     l3 &= k;
     // (2) merge adjacent equal tiles once, nearest the wall first (GameClient.py:162-167):
     //     (0,1) always wins, (1,2) only if (0,1) did not, (2,3) unless (1,2) merged.
-    //     Flags live in bit 7 of each byte: equal = bit 7 of (a^b)+0x7F clear, nonzero =
-    //     bit 7 of b+0x7F set.
-    const uint32_t e01 = ~((l0 ^ l1) + 0x7F7F7F7Fu) & (l1 + 0x7F7F7F7Fu);
-    const uint32_t e12 = ~((l1 ^ l2) + 0x7F7F7F7Fu) & (l2 + 0x7F7F7F7Fu);
-    const uint32_t e23 = ~((l2 ^ l3) + 0x7F7F7F7Fu) & (l3 + 0x7F7F7F7Fu);
-    const uint32_t f01 = ff(e01);
-    const uint32_t f12 = ff(e12 & ~e01);
-    const uint32_t f23 = ff(e23 & (e01 | ~e12));
+    //     Flags live in bit 7 of each byte: equal = bit 7 of 0x80 - (a^b) set, nonzero = bit 7
+    //     of b + 0x7F set (after compaction a nonzero b has a nonzero a before it).
+    const uint32_t e01 = bitop3<0x80u>(0x80808080u - (l0 ^ l1), l1 + 0x7F7F7F7Fu, 0x80808080u);
+    const uint32_t e12 = bitop3<0x80u>(0x80808080u - (l1 ^ l2), l2 + 0x7F7F7F7Fu, 0x80808080u);
+    const uint32_t e23 = bitop3<0x80u>(0x80808080u - (l2 ^ l3), l3 + 0x7F7F7F7Fu, 0x80808080u);
+    const uint32_t f01 = e01;
+    const uint32_t f12 = e12 & ~e01;
+    const uint32_t f23 = bitop3<0xD0u>(e23, e01, e12);   // e23 & (e01 | ~e12)
+    const uint32_t i01 = f01 >> 7, i12 = f12 >> 7, i23 = f23 >> 7;   // 0x01 per merging pair
+    const uint32_t m01 = f01 - i01, m12 = f12 - i12, m23 = f23 - i23;  // 0x7F per merging pair
     uint32_t reward = 0;
     // apply the far pair first so the nearer pairs' shifts carry its result along
-    l2 += f23 & 0x01010101u;
+    l2 += i23;
     if (REWARD) {
         for (int b = 0; b < 4; b++)
-            reward += ((f23 >> (8 * b)) & 1u) << ((l2 >> (8 * b)) & 31u);
+            reward += ((i23 >> (8 * b)) & 1u) << ((l2 >> (8 * b)) & 31u);
     }
-    l3 &= ~f23;
-    l1 += f12 & 0x01010101u;
+    l3 &= ~m23;
+    l1 += i12;
     if (REWARD) {
         for (int b = 0; b < 4; b++)
-            reward += ((f12 >> (8 * b)) & 1u) << ((l1 >> (8 * b)) & 31u);
+            reward += ((i12 >> (8 * b)) & 1u) << ((l1 >> (8 * b)) & 31u);
     }
-    l2 = bsel(f12, l3, l2);
-    l3 &= ~f12;
-    l0 += f01 & 0x01010101u;
+    l2 = bsel(m12, l3, l2);
+    l3 &= ~m12;
+    l0 += i01;
     if (REWARD) {
         for (int b = 0; b < 4; b++)
-            reward += ((f01 >> (8 * b)) & 1u) << ((l0 >> (8 * b)) & 31u);
+            reward += ((i01 >> (8 * b)) & 1u) << ((l0 >> (8 * b)) & 31u);
     }
-    l1 = bsel(f01, l2, l1);
-    l2 = bsel(f01, l3, l2);
-    l3 &= ~f01;
+    l1 = bsel(m01, l2, l1);
+    l2 = bsel(m01, l3, l2);
+    l3 &= ~m01;
     L = Board{l0, l1, l2, l3};
     return reward;
 }
@@ -216,25 +237,41 @@ R48_HD uint32_t select_blank(const Blanks &b, uint32_t rank)
     return 4u * row + col;
 }
 
-// select_blank + place in one: the row of the rank-th blank is where the prefix counts
-// cross `rank`; the three comparisons are lane masks, so the row-hit masks are SGPR logic
-// and each row word takes one v_cndmask + v_or (no row index, no per-row compares).
+// select_blank + place in one, full-rate VALU only. The row of the rank-th blank is the last k
+// with rank >= p_k: n_k = (rank - p_k) >> 31 (arithmetic) is -1 for the rows after it, and
+// three bitop3 selects each pick the row's blank flags z and the rank within the row j. In the
+// row, the blank whose inclusive byte prefix count (f * 0x01010101, f = 0x01 per blank) equals
+// j + 1 is the one: its byte of P ^ splat(j + 1) is 0. `on` is a lane mask (0 / ~0): nothing
+// is placed where it is 0 (an unchanged move spawns nothing, GameClient.py:48-49).
+R48_HD void spawn_at_rank_m(Board &r, const Blanks &b, uint32_t rank, uint32_t e, uint32_t on)
+{
+    const uint32_t d1 = rank - b.p1, d2 = rank - b.p2, d3 = rank - b.p3;
+    uint32_t n1 = (uint32_t)((int32_t)d1 >> 31), n2 = (uint32_t)((int32_t)d2 >> 31),
+             n3 = (uint32_t)((int32_t)d3 >> 31);
+#if defined(__HIP_DEVICE_COMPILE__)
+    // opaque to the optimiser: knowing they are sign masks, it rebuilds n2 & ~n1 as a
+    // compare + v_cndmask (two instructions, one half rate) instead of one v_bitop3
+    asm("" : "+v"(n1), "+v"(n2), "+v"(n3));
+#endif
+    uint32_t z = bsel(n1, b.z0, b.z1);
+    z = bsel(n2, z, b.z2);
+    z = bsel(n3, z, b.z3);
+    uint32_t j = bsel(n1, rank, d1);
+    j = bsel(n2, j, d2);
+    j = bsel(n3, j, d3);
+    const uint32_t P = (z >> 7) * 0x01010101u;
+    const uint32_t S = (j + 1u) * 0x01010101u;
+    const uint32_t hit = bitop3<0x80u>(0x80808080u - (P ^ S), z, on);   // 0x80 in the chosen cell
+    const uint32_t v = hit >> (8u - e);                                   // e = 1 (tile 2) or 2 (tile 4)
+    r.w0 = bitop3<0xF8u>(r.w0, v, n1);        // w | (v & n1): row 0
+    r.w1 = bitop3<0xF8u>(r.w1, v, n2 & ~n1);  // row 1
+    r.w2 = bitop3<0xF8u>(r.w2, v, n3 & ~n2);  // row 2
+    r.w3 = bitop3<0xF4u>(r.w3, v, n3);        // w | (v & ~n3): row 3
+}
+
 R48_HD void spawn_at_rank(Board &r, const Blanks &b, uint32_t rank, uint32_t e, bool on)
 {
-    const bool s1 = rank >= b.p1, s2 = rank >= b.p2, s3 = rank >= b.p3;
-    const uint32_t base = sel(s3, b.p3, sel(s2, b.p2, sel(s1, b.p1, 0u)));
-    uint32_t z = sel(s3, b.z3, sel(s2, b.z2, sel(s1, b.z1, b.z0)));
-    uint32_t j = rank - base;
-    const uint32_t lo = popc(z & 0x8080u);
-    const bool hi = j >= lo;
-    j -= hi ? lo : 0u;
-    z = hi ? (z >> 16) : z;
-    const uint32_t col = (hi ? 2u : 0u) + ((j >= ((z >> 7) & 1u)) ? 1u : 0u);
-    const uint32_t v = (e & (0u - (uint32_t)on)) << (8u * col);   // arithmetic, not a select: no branch
-    r.w0 |= sel(!s1, v, 0u);
-    r.w1 |= sel(s1 && !s2, v, 0u);
-    r.w2 |= sel(s2 && !s3, v, 0u);
-    r.w3 |= sel(s3, v, 0u);
+    spawn_at_rank_m(r, b, rank, e, on ? ~0u : 0u);
 }
 
 // Put exponent e (1 = tile 2, 2 = tile 4) into cell `cell` when `on` (GameClient.py:125).
@@ -252,10 +289,13 @@ R48_HD void place(Board &r, uint32_t cell, uint32_t e, bool on)
 // over iff full and no two orthogonal neighbours are equal.
 R48_HD bool game_over(const Board &r, uint32_t n_blank)
 {
-    uint32_t eq = z80(r.w0 ^ (r.w0 >> 8)) | z80(r.w1 ^ (r.w1 >> 8)) | z80(r.w2 ^ (r.w2 >> 8)) |
-                  z80(r.w3 ^ (r.w3 >> 8));  // (r,c) == (r,c+1)
-    eq &= 0x00808080u;
-    eq |= z80(r.w0 ^ r.w1) | z80(r.w1 ^ r.w2) | z80(r.w2 ^ r.w3);  // (r,c) == (r+1,c)
+    // bit 7 of 0x80 - x per byte: that byte of x is 0. Horizontal pairs: w ^ (w >> 8), whose
+    // top byte is the last cell itself (0 only on a board that is not full anyway).
+    const uint32_t h = or3(0x80808080u - (r.w0 ^ (r.w0 >> 8)), 0x80808080u - (r.w1 ^ (r.w1 >> 8)),
+                           0x80808080u - (r.w2 ^ (r.w2 >> 8)));
+    const uint32_t v = or3(0x80808080u - (r.w3 ^ (r.w3 >> 8)), 0x80808080u - (r.w0 ^ r.w1),
+                           0x80808080u - (r.w1 ^ r.w2));
+    const uint32_t eq = or3(h, v, 0x80808080u - (r.w2 ^ r.w3)) & 0x80808080u;
     return n_blank == 0u && eq == 0u;
 }
 
@@ -334,18 +374,98 @@ struct StepOut {
     uint32_t changed, done, n_blank, reward, score;
 };
 
-// One env step on registers (Game.step, GameClient.py:40-51) given the action and the
-// two spawn draws. `rank_word` is either a Philox word (rank = mulhi(word, n_blank)) or,
-// when RANK_IS_INDEX, the injected rank itself (taken modulo n_blank). VALID_ACTION: the
-// caller guarantees a < 4 (in-kernel random policy), so the moved board is taken as is -- an
-// unchanged move maps back to the same board (from_lines inverts to_lines exactly).
+// ---- Orientations ---------------------------------------------------------------------
+// A board may be held in the line form of any action o (to_lines(rows, o)) instead of in
+// rows. Going from the line form of o to that of action a is one element of the 4x4
+// board's symmetry group, M = P(a) o P(o)^-1 with P(UP) = I, P(DOWN) = Rev (word order
+// reversed), P(LEFT) = T, P(RIGHT) = Rev T. The six elements that occur (I, Rev, T, Rev T,
+// Br T = T Rev, Rev Br T; Br = byte order reversed within each word) all fit one 8-perm
+// network with per-lane selectors:
+//     X0 = perm(w1, w0, x0)   X1 = perm(w1, w0, x1)   Y0 = perm(w3, w2, x0)   Y1 = perm(w3, w2, x1)
+//     L0 = perm(Y0, X0, te)   L1 = perm(Y1, X1, te)   L2 = perm(Y0, X0, to)   L3 = perm(Y1, X1, to)
+// so a step needs 8 v_perm_b32 and one 16-byte selector record {x0, x1, te, to} per board
+// (the k_step_n kernels read it from a 256-byte LDS table, kOrient[o][a]) instead of
+// to_lines + from_lines (16 perms + 16 per-lane selects).
+struct Orient {
+    uint32_t x0, x1, te, to;
+};
+
+#define R48_OR_I {0x03020100u, 0x07060504u, 0x03020100u, 0x07060504u}
+#define R48_OR_REV {0x07060504u, 0x03020100u, 0x07060504u, 0x03020100u}
+#define R48_OR_T {0x06020400u, 0x07030501u, 0x05040100u, 0x07060302u}
+#define R48_OR_REVT {0x05010703u, 0x04000602u, 0x05040100u, 0x07060302u}
+#define R48_OR_BRT {0x06020400u, 0x07030501u, 0x00010405u, 0x02030607u}
+#define R48_OR_REVBRT {0x05010703u, 0x04000602u, 0x00010405u, 0x02030607u}
+// kOrient[4 * o + a]: from the line form of o (0 UP = rows, 1 DOWN, 2 LEFT, 3 RIGHT) to that of a
+static constexpr Orient kOrient[16] = {
+    R48_OR_I,   R48_OR_REV,    R48_OR_T,   R48_OR_REVT,     // o = UP (rows)
+    R48_OR_REV, R48_OR_I,      R48_OR_BRT, R48_OR_REVBRT,   // o = DOWN
+    R48_OR_T,   R48_OR_REVT,   R48_OR_I,   R48_OR_REV,      // o = LEFT
+    R48_OR_BRT, R48_OR_REVBRT, R48_OR_REV, R48_OR_I,        // o = RIGHT
+};
+#undef R48_OR_I
+#undef R48_OR_REV
+#undef R48_OR_T
+#undef R48_OR_REVT
+#undef R48_OR_BRT
+#undef R48_OR_REVBRT
+
+R48_HD Board reorient(const Board &w, const Orient &s)
+{
+    const uint32_t X0 = perm(w.w1, w.w0, s.x0), X1 = perm(w.w1, w.w0, s.x1);
+    const uint32_t Y0 = perm(w.w3, w.w2, s.x0), Y1 = perm(w.w3, w.w2, s.x1);
+    return Board{perm(Y0, X0, s.te), perm(Y1, X1, s.te), perm(Y0, X0, s.to), perm(Y1, X1, s.to)};
+}
+
+// The move + spawn + game-over of one Philox-mode step on a board ALREADY in the line form
+// of action a (Game.step, GameClient.py:40-51). The spawn rank counts blanks in line order --
+// L[0] bytes 0..3, then L[1], ... (distance from the wall the tiles move toward, then line
+// index) -- the build's Philox contract: the rank is uniform, so the
+// spawned cell is uniform over the blanks in any fixed order, as random_fill_grid's is
+// (GameClient.py:109-122); the reference's row-major order is kept by the injected-draw path
+// (step_board<.., RANK_IS_INDEX = true>). Game over is invariant under the board's symmetries.
+// VALID_ACTION: a < 4 is guaranteed (in-kernel random policy), so the moved lines are taken as
+// they are (an unchanged move leaves them as they were).
+template <bool REWARD, bool VALID_ACTION>
+R48_HD StepOut step_lines(Board &L, uint32_t a, uint32_t rank_word, bool four)
+{
+    StepOut o;
+    const Board L0 = L;
+    o.reward = move_lines<REWARD>(L);
+    const uint32_t diff = or3(L.w0 ^ L0.w0, L.w1 ^ L0.w1, L.w2 ^ L0.w2) | (L.w3 ^ L0.w3);
+    // changed as a lane mask (0 / ~0) without a compare + select: bit 31 of diff | -diff
+    uint32_t on = (uint32_t)((int32_t)(diff | (0u - diff)) >> 31);
+    if (!VALID_ACTION) {
+        on = a < 4u ? on : 0u;
+        L = Board{bsel(on, L.w0, L0.w0), bsel(on, L.w1, L0.w1), bsel(on, L.w2, L0.w2), bsel(on, L.w3, L0.w3)};
+    }
+    o.reward = REWARD ? (o.reward & on) : 0u;
+    const Blanks bl = blanks(L);
+    o.n_blank = bl.n;
+    spawn_at_rank_m(L, bl, mulhi(rank_word, bl.n), four ? 2u : 1u, on);
+    o.changed = on & 1u;
+    o.done = game_over(L, bl.n + on);   // blanks after the spawn: n - 1 where one was placed
+    return o;
+}
+
+// One env step on row words (Game.step, GameClient.py:40-51) given the action and the two
+// spawn draws. `rank_word` is either a Philox word (rank = mulhi(word, n_blank), blanks in
+// line order: step_lines) or, when RANK_IS_INDEX, the injected rank itself (taken modulo
+// n_blank, blanks in the reference's row-major order, GameClient.py:109-114). VALID_ACTION:
+// the caller guarantees a < 4 (in-kernel random policy), so the moved board is taken as is --
+// an unchanged move maps back to the same board (from_lines inverts to_lines exactly).
 template <bool REWARD, bool RANK_IS_INDEX, bool VALID_ACTION = false>
 R48_HD StepOut step_board(Board &r, uint32_t a, uint32_t rank_word, bool four)
 {
-    StepOut o;
-    const bool valid = VALID_ACTION || a < 4u;
     const uint32_t ac = a & 3u;
     Board L = to_lines(r, ac);
+    if (!RANK_IS_INDEX) {
+        const StepOut o = step_lines<REWARD, VALID_ACTION>(L, a, rank_word, four);
+        r = from_lines(L, ac);
+        return o;
+    }
+    StepOut o;
+    const bool valid = VALID_ACTION || a < 4u;
     const Board L0 = L;
     o.reward = move_lines<REWARD>(L);
     const uint32_t diff = (L.w0 ^ L0.w0) | (L.w1 ^ L0.w1) | (L.w2 ^ L0.w2) | (L.w3 ^ L0.w3);
@@ -359,11 +479,7 @@ R48_HD StepOut step_board(Board &r, uint32_t a, uint32_t rank_word, bool four)
     o.reward = changed ? o.reward : 0u;
     const Blanks bl = blanks(r);
     o.n_blank = bl.n;
-    uint32_t rank;
-    if (RANK_IS_INDEX)
-        rank = bl.n ? rank_word % bl.n : 0u;
-    else
-        rank = mulhi(rank_word, bl.n);
+    const uint32_t rank = bl.n ? rank_word % bl.n : 0u;
     spawn_at_rank(r, bl, rank, four ? 2u : 1u, changed);
     o.changed = changed;
     o.done = game_over(r, bl.n - (changed ? 1u : 0u));

@@ -120,6 +120,56 @@ __device__ __forceinline__ LaneOut step_lane(Board b, uint32_t a_given, Draw d, 
     return r;
 }
 
+// ---------------------------------------------------------------- orientation-tracked step
+// k_step_n keeps each board in the line form of its last action (r48_board.h "Orientations"):
+// `ob` = 64 x that action (0 = rows, after a load or a reset), so the selector record taking the
+// board to the line form of action a sits at byte ob + 16a of the 256-byte LDS table. A step is
+// then one reorient (8 v_perm) + step_lines -- no to_lines / from_lines round trip, no per-lane
+// selects on the action -- and the boards go back to rows once, when the call ends.
+__device__ __forceinline__ r48::Orient orient_at(const r48::Orient *tab, uint32_t off)
+{
+    // one ds_read_b128 (the table is 16-byte aligned, off a multiple of 16)
+    const u32x4 v = *reinterpret_cast<const u32x4 *>(
+        __builtin_assume_aligned(reinterpret_cast<const char *>(tab) + off, 16));
+    return r48::Orient{v.x, v.y, v.z, v.w};
+}
+
+__device__ __forceinline__ void load_orient_table(r48::Orient *tab)
+{
+    if (threadIdx.x < 16)
+        tab[threadIdx.x] = r48::kOrient[threadIdx.x];
+    __syncthreads();
+}
+
+template <bool RANDOM, bool AUTO_RESET, bool REWARD>
+__device__ __forceinline__ LaneOut step_lane_lines(Board &L, uint32_t &ob, const r48::Orient *tab, uint32_t a_given,
+                                                   Draw d, bool want_score)
+{
+    LaneOut r;
+    r.a = RANDOM ? d.x >> 30 : a_given;  // uniform over {UP, DOWN, LEFT, RIGHT} (control/rand.py:9-11)
+    const uint32_t a16 = RANDOM ? (d.x >> 26) & 0x30u : (a_given & 3u) << 4;
+    L = r48::reorient(L, orient_at(tab, ob + a16));
+    ob = a16 << 2;
+    const r48::StepOut o =
+        r48::step_lines<REWARD, RANDOM>(L, r.a, d.y, (d.x & 0x3FFFFFFFu) < r48::kFourThresh30);
+    r.score = 0u;
+    if (want_score) {
+        asm volatile("" ::: "memory");   // keep the tile sum out of the other steps (see step_lane)
+        r.score = r48::tile_sum(L);      // order-free: any orientation
+    }
+    if (AUTO_RESET && __ballot(o.done) != 0) {
+        Board z;
+        r48::reset_board(z, d.y >> 28, (d.y & 0x0FFFFFFFu) < r48::kFourThresh28);   // rows
+        L = Board{r48::sel(o.done, z.w0, L.w0), r48::sel(o.done, z.w1, L.w1), r48::sel(o.done, z.w2, L.w2),
+                  r48::sel(o.done, z.w3, L.w3)};
+        ob = o.done ? 0u : ob;
+    }
+    r.done = o.done;
+    r.changed = o.changed;
+    r.reward = o.reward;
+    return r;
+}
+
 template <bool RANDOM, bool REWARD>
 __device__ __forceinline__ void emit(const LaneOut &r, int64_t i, int8_t *boards, int8_t *actions, uint8_t *done,
                                      uint8_t *changed, int32_t *reward, int32_t *score)
@@ -237,10 +287,12 @@ __global__ __launch_bounds__(kBlock) void k_step_n(int8_t *boards, int64_t n, in
     const int64_t base = (int64_t)blockIdx.x * kTile + 2 * (int64_t)threadIdx.x;
     const bool want_score = score != nullptr;
     const int32_t last = n_steps - 1;
+    __shared__ __attribute__((aligned(16))) r48::Orient tab[16];
+    load_orient_table(tab);
     if ((int64_t)(blockIdx.x + 1) * kTile <= n && (gid0 & 1) == 0 &&
         planes_aligned(actions, done, changed, reward, score)) {
         Board b[2 * NP];
-        uint32_t a[2 * NP];
+        uint32_t a[2 * NP], ob[2 * NP];
         uint64_t q[NP];
 #pragma unroll
         for (int j = 0; j < NP; j++) {
@@ -249,6 +301,7 @@ __global__ __launch_bounds__(kBlock) void k_step_n(int8_t *boards, int64_t n, in
             b[2 * j + 1] = load_board(boards, i + 1);
             q[j] = (uint64_t)(gid0 + i) >> 1;
             a[2 * j] = a[2 * j + 1] = 0u;
+            ob[2 * j] = ob[2 * j + 1] = 0u;   // rows
             if (!RANDOM) {
                 const uint16_t a2 = *reinterpret_cast<const uint16_t *>(actions + i);
                 a[2 * j] = a2 & 0xffu;
@@ -266,16 +319,18 @@ __global__ __launch_bounds__(kBlock) void k_step_n(int8_t *boards, int64_t n, in
             for (int j = 0; j < NP; j++) {
                 Draw de, dd;
                 pair_draws(q[j], step, k0, k1, de, dd);
-                r[2 * j] = step_lane<RANDOM, AUTO_RESET, REWARD>(b[2 * j], a[2 * j], de, sc);
-                r[2 * j + 1] = step_lane<RANDOM, AUTO_RESET, REWARD>(b[2 * j + 1], a[2 * j + 1], dd, sc);
-                b[2 * j] = r[2 * j].b;
-                b[2 * j + 1] = r[2 * j + 1].b;
+                r[2 * j] = step_lane_lines<RANDOM, AUTO_RESET, REWARD>(b[2 * j], ob[2 * j], tab, a[2 * j], de, sc);
+                r[2 * j + 1] =
+                    step_lane_lines<RANDOM, AUTO_RESET, REWARD>(b[2 * j + 1], ob[2 * j + 1], tab, a[2 * j + 1], dd, sc);
             }
         }
 #pragma unroll
-        for (int j = 0; j < NP; j++)
+        for (int j = 0; j < NP; j++) {
+            r[2 * j].b = r48::reorient(b[2 * j], orient_at(tab, ob[2 * j]));   // back to rows
+            r[2 * j + 1].b = r48::reorient(b[2 * j + 1], orient_at(tab, ob[2 * j + 1]));
             emit_pair<RANDOM, REWARD>(r[2 * j], r[2 * j + 1], base + 2 * kBlock * j, boards, actions, done, changed,
                                       reward, score);
+        }
     } else {
         for (int j = 0; j < 2 * NP; j++) {
             const int64_t i = base + 2 * kBlock * (j >> 1) + (j & 1);

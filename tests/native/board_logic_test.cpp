@@ -162,6 +162,62 @@ int main()
         delete[] boards; delete[] ob; delete[] act; delete[] rank; delete[] four; delete[] done; delete[] chg;
         delete[] rw; delete[] sc;
     }
+    // 6. orientation table: from the line form of o, kOrient[4o + a] gives the line form of a
+    //    (every (o, a), random boards with distinct cells so any misplaced byte shows)
+    {
+        std::mt19937 g(7);
+        for (int it = 0; it < 2000; it++) {
+            int8_t b[16];
+            for (int k = 0; k < 16; k++) b[k] = (int8_t)(g() & 0x3f);
+            const Board R = load(b);
+            for (uint32_t o = 0; o < 4; o++)
+                for (uint32_t a = 0; a < 4; a++) {
+                    const Board got = r48::reorient(r48::to_lines(R, o), r48::kOrient[4 * o + a]);
+                    const Board want = r48::to_lines(R, a);
+                    CHECK(memcmp(&got, &want, 16) == 0, "kOrient o=%u a=%u", o, a);
+                }
+            // back to rows from any line form: kOrient[4o + UP]
+            for (uint32_t o = 0; o < 4; o++) {
+                const Board got = r48::reorient(r48::to_lines(R, o), r48::kOrient[4 * o]);
+                CHECK(memcmp(&got, &R, 16) == 0, "kOrient back to rows o=%u", o);
+            }
+        }
+    }
+    // 7. k_step_n's orientation-tracked loop (step_lane_lines in r48_env.hip, restated here on
+    //    the host): boards stay in the line form of their last action for many steps, back to
+    //    rows at the end == orc_step_philox repeated, random policy + auto-reset
+    {
+        const int n = 4096, steps = 300;
+        int8_t *boards = new int8_t[16 * (size_t)n], *ob = new int8_t[16 * (size_t)n];
+        std::mt19937 g(11);
+        for (int i = 0; i < n; i++)
+            for (int k = 0; k < 16; k++) boards[16 * i + k] = (g() & 1) ? (int8_t)(1 + g() % 7) : 0;
+        memcpy(ob, boards, 16 * (size_t)n);
+        const uint64_t seed = 0x5EED'2048ull;
+        const int64_t off = 2;
+        for (uint32_t step = 0; step < (uint32_t)steps; step++)
+            orc_step_philox(ob, n, seed, off, 100 + step, 1u | 2u, nullptr, nullptr, nullptr, nullptr, nullptr);
+        for (int i = 0; i < n; i++) {
+            Board L = load(boards + 16 * i);
+            uint32_t o = 0;
+            const uint64_t gid = (uint64_t)(off + i), q = gid >> 1;
+            for (uint32_t step = 0; step < (uint32_t)steps; step++) {
+                uint32_t w[4] = {(uint32_t)q, (uint32_t)(q >> 32), 100 + step, r48::kStepTag};
+                r48::philox4x32_10(w, (uint32_t)seed, (uint32_t)(seed >> 32));
+                const uint32_t x = w[2 * (gid & 1)], y = w[2 * (gid & 1) + 1], a = x >> 30;
+                L = r48::reorient(L, r48::kOrient[4 * o + a]);
+                o = a;
+                const r48::StepOut s = r48::step_lines<false, true>(L, a, y, (x & 0x3FFFFFFFu) < r48::kFourThresh30);
+                if (s.done) {
+                    r48::reset_board(L, y >> 28, (y & 0x0FFFFFFFu) < r48::kFourThresh28);
+                    o = 0;
+                }
+            }
+            L = r48::reorient(L, r48::kOrient[4 * o]);
+            CHECK(memcmp(&L, ob + 16 * i, 16) == 0, "orientation-tracked board i=%d", i);
+        }
+        delete[] boards; delete[] ob;
+    }
     printf("board_logic_test: %s (%d failures)\n", fails ? "FAIL" : "OK", fails);
     return fails ? 1 : 0;
 }

@@ -63,6 +63,23 @@ OP2(o_mov, "v_mov_b32 %0, %1")
 OP2(o_cmp_vcc, "v_cmp_ne_u32 vcc, %0, %1\n\tv_add_u32 %0, %0, %1")
 OP2(o_addco, "v_add_co_u32 %0, vcc, %0, %1")
 OP2(o_sdwa_add, "v_add_u32_sdwa %0, %0, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:DWORD")
+__device__ __forceinline__ void o_cnd64(uint32_t &x, uint32_t k, uint32_t k2)
+{
+    const uint64_t m = 0x5555555555555555ull ^ k2;
+    asm volatile("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(x) : "v"(k), "s"(m));
+}
+__device__ __forceinline__ void o_cmp64_cnd64(uint32_t &x, uint32_t k, uint32_t)
+{
+    uint64_t m;
+    asm volatile("v_cmp_gt_u32_e64 %1, %0, %2\n\tv_cndmask_b32_e64 %0, %0, %2, %1" : "+v"(x), "=&s"(m) : "v"(k));
+}
+OP2(o_sub_lit, "v_sub_u32 %0, 0x80808080, %0")
+OP2(o_and_lit, "v_and_b32 %0, 0x80808080, %0")
+OP2(o_bitop3_vvs, "v_bitop3_b32 %0, %0, %1, %2 bitop3:0xc8")
+__device__ __forceinline__ void o_nop_add(uint32_t &x, uint32_t k, uint32_t)
+{
+    asm volatile("s_nop 0\n\tv_add_u32 %0, %0, %1" : "+v"(x) : "v"(k));
+}
 __device__ __forceinline__ void o_mad64(uint32_t &x, uint32_t k, uint32_t)
 {
     uint64_t r;
@@ -80,7 +97,8 @@ __device__ __forceinline__ void o_mad64(uint32_t &x, uint32_t k, uint32_t)
 #define LIST(X) X(o_add) X(o_sub) X(o_and) X(o_or) X(o_xor) X(o_not) X(o_xor3) X(o_bfi) X(o_perm) X(o_mulhi) \
     X(o_mulu24) X(o_bcnt) X(o_cnd) X(o_cmp_cnd) X(o_lshl) X(o_lshr) X(o_lshlv) X(o_ashr) X(o_lshl_or)         \
     X(o_lshl_add) X(o_and_or) X(o_or3) X(o_add3) X(o_alignbit) X(o_bfe) X(o_min) X(o_max3) X(o_sad) X(o_msad)  \
-    X(o_pkadd) X(o_pkmax) X(o_dot4) X(o_mov) X(o_cmp_vcc) X(o_addco) X(o_sdwa_add) X(o_mad64)
+    X(o_pkadd) X(o_pkmax) X(o_dot4) X(o_mov) X(o_cmp_vcc) X(o_addco) X(o_sdwa_add) X(o_mad64) X(o_cnd64) X(o_cmp64_cnd64) \
+    X(o_sub_lit) X(o_and_lit) X(o_bitop3_vvs) X(o_nop_add)
 #define DEF(N) KERNEL(N, N)
 LIST(DEF)
 
