@@ -347,6 +347,12 @@ R48_HD void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1)
         c[2] = n2;
         k0 += 0x9E3779B9u;
         k1 += 0xBB67AE85u;
+#if defined(__HIP_DEVICE_COMPILE__)
+        // the round keys are recomputed by two s_add per round instead of being hoisted out of
+        // the callers' step loops into 20 SGPRs: the k_step_n kernels must stay under the SGPR
+        // budget of 8 waves per SIMD (measured: 87 SGPRs + the trap handler's allocate 7)
+        asm volatile("" : "+s"(k0), "+s"(k1));
+#endif
     }
 }
 

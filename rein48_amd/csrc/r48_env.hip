@@ -265,6 +265,30 @@ __global__ __launch_bounds__(kBlock) void k_step(int8_t *boards, int64_t n, int6
     }
 }
 
+#ifdef R48_STAMP
+// Diagnostic build only (tools/exp_stamps.py): per wave of k_step_n, the core clock (s_memtime)
+// and the 100 MHz reference clock (s_memrealtime) at entry and exit, and HW_ID (CU / SIMD).
+__device__ unsigned long long r48_stamp_buf[65536 * 4];
+#define R48_STAMP_BEGIN                                                                  \
+    const unsigned long long st_t0 = __builtin_amdgcn_s_memtime(), st_r0 = __builtin_amdgcn_s_memrealtime();
+#define R48_STAMP_END                                                                    \
+    if ((threadIdx.x & 63) == 0) {                                                       \
+        const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime(); \
+        const unsigned w = blockIdx.x * (kBlock / 64) + threadIdx.x / 64;                \
+        if (w < 65536) {                                                                 \
+            unsigned hw, xcc;                                                            \
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));             \
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));           \
+            hw = (hw & 0x0FFFFFFFu) | ((xcc & 0xFu) << 28);                              \
+            r48_stamp_buf[4 * w] = st_t0; r48_stamp_buf[4 * w + 1] = st_r0;              \
+            r48_stamp_buf[4 * w + 2] = t1 - st_t0; r48_stamp_buf[4 * w + 3] = ((r1 - st_r0) << 32) | hw; \
+        }                                                                                \
+    }
+#else
+#define R48_STAMP_BEGIN
+#define R48_STAMP_END
+#endif
+
 // ---------------------------------------------------------------- K steps in one launch
 // r48_env_step_n: n_steps consecutive steps of every board in ONE launch. Boards are independent,
 // so a lane keeps its NP board pairs in VGPRs for all n_steps steps (no grid barrier, no board
@@ -287,6 +311,7 @@ __global__ __launch_bounds__(kBlock) void k_step_n(int8_t *boards, int64_t n, in
     const int64_t base = (int64_t)blockIdx.x * kTile + 2 * (int64_t)threadIdx.x;
     const bool want_score = score != nullptr;
     const int32_t last = n_steps - 1;
+    R48_STAMP_BEGIN
     __shared__ __attribute__((aligned(16))) r48::Orient tab[16];
     load_orient_table(tab);
     if ((int64_t)(blockIdx.x + 1) * kTile <= n && (gid0 & 1) == 0 &&
@@ -312,9 +337,27 @@ __global__ __launch_bounds__(kBlock) void k_step_n(int8_t *boards, int64_t n, in
             }
         }
         LaneOut r[2 * NP];
+        // Progress-ordered issue priority. The SIMD's VALU is the bound and its arbiter prefers
+        // the oldest wave: left alone, the 8 waves of a SIMD finish one after another and the
+        // last ones run with too few partners to fill the VALU. Dropping a wave's priority as it
+        // passes each quarter of the call lets the laggards catch up, so all 8 stay to the end.
+        const int32_t q1 = n_steps >> 2, q2 = n_steps >> 1, q3 = q1 + q2;
+#ifdef R48_NO_PRIO   // ablation build (tools/exp_stepn.py A/B)
+        constexpr bool kPrio = false;
+#else
+        constexpr bool kPrio = true;
+#endif
+        if (kPrio)
+            __builtin_amdgcn_s_setprio(3);
         for (int32_t t = 0; t < n_steps; t++) {
             const uint32_t step = step0 + (uint32_t)t;
             const bool sc = want_score && t == last;
+            if (kPrio && t == q1)
+                __builtin_amdgcn_s_setprio(2);
+            if (kPrio && t == q2)
+                __builtin_amdgcn_s_setprio(1);
+            if (kPrio && t == q3)
+                __builtin_amdgcn_s_setprio(0);
 #pragma unroll
             for (int j = 0; j < NP; j++) {
                 Draw de, dd;
@@ -349,6 +392,7 @@ __global__ __launch_bounds__(kBlock) void k_step_n(int8_t *boards, int64_t n, in
             }
         }
     }
+    R48_STAMP_END
 }
 
 // ---------------------------------------------------------------- injected-draw step
@@ -791,6 +835,13 @@ int r48_env_reset_with_draws(r48_env *env, const uint8_t *mask, const uint8_t *r
     return launched("k_reset_draws");
 }
 
+#ifdef R48_STAMP
+int r48_debug_stamps(unsigned long long *out, int64_t n_waves)
+{
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(r48_stamp_buf), sizeof(unsigned long long) * 4 * n_waves) == hipSuccess
+               ? 0 : -1;
+}
+#endif
 }  // extern "C"
 
 namespace {

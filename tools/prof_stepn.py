@@ -16,8 +16,8 @@ n = int(sys.argv[3]) if len(sys.argv) > 3 else 1 << 20
 env = VecGame(n, device="cuda:0", seed=1)
 env.fill_random(7)
 t0 = time.perf_counter()
-while time.perf_counter() - t0 < 0.3:
-    env.step_n(100, auto_reset=True)
+while time.perf_counter() - t0 < 0.3:       # settle with the same K, so every dispatch is alike
+    env.step_n(K, auto_reset=True)
     torch.cuda.synchronize()
 for _ in range(reps):
     env.step_n(K, auto_reset=True)
