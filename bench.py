@@ -15,23 +15,25 @@ global board id); no data-path collective. Timing: barrier + sync on both sides 
 steps, max over ranks; value = all boards x K / that time.
 
 Extra objects on the JSON line:
-  roofline      k_step_n is VALU-issue bound (no memory traffic inside its step loop): achieved =
-                VALU wave-instructions per board-step (SQ_INSTS_VALU per dispatch / board-steps,
-                committed rocprofv3 PMC profile, cross-checked against the static ISA count) x
-                board-steps / the dispatch time from HIP events in the timed region; peak = one
-                wave-instruction per 2 cycles per SIMD at 2.4 GHz (1024 SIMDs). `hbm` holds the
-                single-step kernel k_step (boards through HBM every step, 34 algorithmic bytes per
-                board-step) at 2^20 boards and at 2^26 (past the 256 MiB Infinity Cache) against the
-                8 TB/s HBM spec, with its PMC traffic from the committed profile.
+  roofline      k_step_n is VALU-issue bound (boards in VGPRs, no memory traffic inside its step
+                loop): achieved = VALU issue cycles per board-step (the shipped loop's instruction
+                mix x measured per-instruction issue costs, committed in profiles/r02/
+                pmc_k_step_n.json with its SQ_INSTS_VALU cross-check) x board-steps / the dispatch
+                time from HIP events in the timed region; peak = one issue cycle per SIMD per clock
+                (1024 SIMDs x 2.4 GHz). `valu_instr_rate` gives the plain instruction-rate fraction.
+                `hbm` holds the single-step kernel k_step (boards through HBM every step, 34
+                algorithmic bytes per board-step) at 2^20 boards (Infinity-Cache resident) and at
+                2^26 (past the 256 MiB cache: the HBM point) against the 8 TB/s spec, with PMC
+                traffic from the committed profiles.
+  repeat_5      5 repeats of the timed region (rank 0, N=1).
   cpu_baseline  oracle/game_port.py (faithful pure-Python restatement of the reference Game + Rand,
                 calibrated against the reference in BASELINE.md) on one process per available host
                 CPU (at most 16, the box's share) for a bounded sample, plus the 1-process figure;
                 rank 0, N=1 only (oracle/port_bench.py).
-  extras        N=1: the fused random-policy rollout kernel, repeats of the timed region, the
-                reference reset start, config 3 (A3C + CNN), config 5 per GPU (DQN + ResNet-10 + HBM
-                replay) and the C oracle as a strong CPU line. N>1: config 4 (A3C, 2^20 boards per
-                GPU) and config 5 (DQN, 2^21 boards per GPU) on all ranks with the gradient
-                all-reduce (--no-extras skips them).
+  extras        N=1: the fused random-policy rollout kernel, the reference reset start, config 3
+                (A3C + CNN), config 5 per GPU (DQN + ResNet-10 + HBM replay) and the C oracle as a
+                strong CPU line. N>1: config 4 (A3C, 2^20 boards per GPU) and config 5 (DQN, 2^21
+                boards per GPU) on all ranks with the gradient all-reduce (--no-extras skips them).
 """
 import argparse
 import datetime
@@ -53,7 +55,8 @@ ALGO_BYTES = 34            # per board-step of k_step: 16 B board in + 16 B out 
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
 HBM_MEASURED_GBS = 6290.0  # float4 copy measured on MI355X (same guide)
 SIMDS, CLOCK_GHZ = 1024, 2.4            # 256 CUs x 4 SIMDs; max clock (same guide)
-VALU_PEAK_G = SIMDS * CLOCK_GHZ / 2.0   # G wave-instructions/s: one VALU issue per 2 cycles per SIMD
+VALU_PEAK_G = SIMDS * CLOCK_GHZ / 2.0   # G wave-instructions/s: one full-rate wave64 VALU instr per 2 cycles
+VALU_ISSUE_PEAK_G = SIMDS * CLOCK_GHZ   # G VALU issue-cycles/s
 PROFILE_DIR = os.path.join(ROOT, "profiles", "r02")
 
 
@@ -107,6 +110,7 @@ def _load_profile(name):
 
 
 SETTLE_S = 0.3   # minimum untimed stepping before a timed region: GPU clocks ramp over ~20 ms+
+SYNC_POLL = False  # --sync: poll the region's last HIP event before the closing synchronize
 
 
 def timed_steps(env, plan, W, chunk, world, dev):
@@ -134,6 +138,12 @@ def timed_steps(env, plan, W, chunk, world, dev):
         a.record(s)
         env.step_n(c, auto_reset=True)
         b.record(s)
+    if SYNC_POLL:
+        # spin on the last event instead of sleeping in the driver's blocking wait: a ~80 us
+        # region otherwise measures the wake-up jitter of the waiting thread
+        last = ev[-1][1]
+        while not last.query():
+            pass
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -164,44 +174,52 @@ def single_step_hbm(dev, seed, n, launches):
     gbs = n * ALGO_BYTES / (ms * 1e-3) / 1e9
     name = "pmc_k_step_2p%d.json" % (n.bit_length() - 1)
     prof = _load_profile(name)
-    return {"kernel": "k_step<RANDOM=1,AUTO_RESET=1,REWARD=0>", "boards": n, "launch_ms": ms,
-            "env_steps_per_s": n / (ms * 1e-3), "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": gbs / HBM_PEAK_GBS, "frac_of_measured_copy_ceiling": gbs / HBM_MEASURED_GBS,
-            "algorithmic_bytes_per_launch": n * ALGO_BYTES,
-            "traffic": prof.get("hbm_bytes_per_launch") if prof else None,
-            "traffic_source": ("profiles/r02/%s (committed rocprofv3 FETCH_SIZE + WRITE_SIZE passes, not "
-                               "measured in this run)" % name) if prof else None}
+    out = {"kernel": "k_step<RANDOM=1,AUTO_RESET=1,REWARD=0>", "boards": n, "launch_ms": ms,
+           "env_steps_per_s": n / (ms * 1e-3), "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": gbs / HBM_PEAK_GBS, "frac_of_measured_copy_ceiling": gbs / HBM_MEASURED_GBS,
+           "algorithmic_bytes_per_launch": n * ALGO_BYTES,
+           "traffic": prof.get("hbm_bytes_per_launch") if prof else None,
+           "traffic_source": ("profiles/r02/%s (committed rocprofv3 FETCH_SIZE + WRITE_SIZE passes, not "
+                              "measured in this run)" % name) if prof else None}
+    if n * ALGO_BYTES < 256 * 2 ** 20:
+        out["bound"] = "mall"
+        out["note"] = ("%d MB per step stays in the 256 MiB Infinity Cache: a cache-resident rate, not HBM; the "
+                       "2^26-board entry is the HBM point" % (n * ALGO_BYTES // 10 ** 6))
+    else:
+        out["bound"] = "hbm"
+    return out
 
 
 def roofline_step_n(n, dev_ms, steps):
-    """VALU roofline of k_step_n: wave-instructions per board-step from the committed PMC profile
-    (else the static ISA count of the shipped loop) x board-steps / device time."""
+    """VALU roofline of k_step_n (boards stay in VGPRs for all steps of a call: no memory traffic
+    inside the step loop). Work = VALU issue cycles: the shipped loop's static instruction mix x
+    each instruction's measured issue cost (modelled_cycles_per_board_step, profiles/r02/
+    pmc_k_step_n.json, made by tools/make_r02_profiles.py from build/r48_env.s and
+    profiles/r02/instr_rate.txt); peak = one issue cycle per SIMD per clock (1024 SIMDs x 2.4 GHz).
+    Also reported: SQ_INSTS_VALU per board-step (PMC) against the full-rate instruction peak."""
     prof = _load_profile("pmc_k_step_n.json")
-    if prof:
-        per, src = prof["valu_wave_instr_per_board_step"], "profiles/r02/pmc_k_step_n.json (SQ_INSTS_VALU)"
-    else:
-        per, src = 392.0 / 128, "static ISA count of the shipped loop (392 VALU per lane per pair-step)"
+    if prof is None:
+        raise SystemExit("profiles/r02/pmc_k_step_n.json missing (tools/prof_r02.sh + tools/make_r02_profiles.py)")
+    cyc, per = prof["modelled_cycles_per_board_step"], prof["valu_wave_instr_per_board_step"]
     bsteps_per_s = n * steps / (dev_ms * 1e-3)
-    achieved = per * bsteps_per_s / 1e9
-    out = {"bound": "valu", "achieved": achieved, "peak": VALU_PEAK_G, "unit": "G VALU wave-instr/s",
-           "frac": achieved / VALU_PEAK_G, "traffic": None,
-           "kernel": "k_step_n<RANDOM=1,AUTO_RESET=1,REWARD=0> (board pair per lane in VGPRs for all steps of "
-                     "the call, one Philox4x32-10 call per pair-step)",
-           "valu_wave_instr_per_board_step": per, "valu_count_source": src,
-           "board_steps_timed": n * steps, "device_ms_timed": dev_ms,
-           "peak_note": "1 VALU wave-instruction / 2 cycles / SIMD x 1024 SIMDs x 2.4 GHz; half-rate "
-                        "instructions (v_perm, v_cmp, v_bfi, VOP3 3-input ops, left shifts) take ~4.3 cycles "
-                        "(profiles/r02/instr_rate.txt)"}
-    if prof:
-        out["traffic"] = prof.get("hbm_bytes_per_dispatch")
-        out["traffic_source"] = "profiles/r02/pmc_k_step_n.json (committed, not measured in this run)"
-        cyc = prof.get("modelled_cycles_per_board_step")
-        if cyc:
-            # the instruction mix's own issue ceiling: modelled SIMD cycles per board-step (per-
-            # instruction issue costs measured in profiles/r02/instr_rate.txt) at 2.4 GHz
-            model_ms = cyc * n * steps / SIMDS / (CLOCK_GHZ * 1e9) * 1e3
-            out["frac_of_mix_issue_ceiling"] = model_ms / dev_ms
-    return out
+    achieved = cyc * bsteps_per_s / 1e9
+    instr = per * bsteps_per_s / 1e9
+    return {"bound": "valu", "achieved": achieved, "peak": VALU_ISSUE_PEAK_G, "unit": "G VALU issue-cycles/s",
+            "frac": achieved / VALU_ISSUE_PEAK_G, "traffic": prof["hbm_bytes_per_dispatch"] * n / prof["boards"],
+            "traffic_unit": "bytes per launch (HBM/fabric; the boards are read and written once per call)",
+            "traffic_source": "profiles/r02/pmc_k_step_n.json: rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE passes of the "
+                              "same 2^20-board K=20 dispatch (committed profile, not measured in this run)",
+            "kernel": "k_step_n<RANDOM=1,AUTO_RESET=1,REWARD=0> (board pair per lane in VGPRs for all steps of the call, "
+                      "one Philox4x32-10 call per pair-step, line-form orientation tracking)",
+            "issue_cycles_per_board_step": cyc,
+            "issue_cycles_source": "build/r48_env.s hot loop (tools/isa_hist.py) x profiles/r02/instr_rate.txt",
+            "valu_wave_instr_per_board_step": per,
+            "valu_instr_source": "profiles/r02/pmc_k_step_n.json (SQ_INSTS_VALU per dispatch / board-steps)",
+            "valu_instr_rate": {"achieved": instr, "peak": VALU_PEAK_G, "unit": "G VALU wave-instr/s",
+                                "frac": instr / VALU_PEAK_G,
+                                "note": "peak = one wave64 instruction per 2 cycles per SIMD; half-rate instructions "
+                                        "(v_perm, v_mad_u64_u32, v_bcnt, v_mul, v_lshlrev...) take ~4.3 cycles"},
+            "board_steps_timed": n * steps, "device_ms_timed": dev_ms}
 
 
 def extras(dev, seed, n_small):
@@ -384,7 +402,12 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
+    ap.add_argument("--sync", choices=("poll", "block"), default="block",
+                    help="end of the timed region: spin on its last event, then synchronize (poll) or only "
+                         "synchronize (block)")
     args = ap.parse_args()
+    global SYNC_POLL
+    SYNC_POLL = args.sync == "poll"
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(launch_ranks(args.gpus))
@@ -445,18 +468,19 @@ def main():
     }
     if cpu_line is not None:
         line["cpu_baseline"] = cpu_line
+    if rank == 0 and world == 1:
+        # 5 repeats of the same K-step region, each re-warmed
+        reps = [timed_steps(env, plan, chunk, chunk, world, dev)[0] for _ in range(5)]
+        vals = [n * K / r for r in reps]
+        line["repeat_5"] = {"values": vals, "median": sorted(vals)[2],
+                            "spread": (max(vals) - min(vals)) / sorted(vals)[2], "sync": args.sync}
     if rank == 0 and world == 1 and not args.no_extras:
         # the single-step HBM kernel: at 2^20 (cache-resident) and 2^26 boards (1 GiB, past the
         # 256 MiB Infinity Cache: the HBM-honest point)
         line["roofline"]["hbm"] = {"k_step_2p20": single_step_hbm(dev, args.seed, 1 << 20, 400),
                                    "k_step_2p26": single_step_hbm(dev, args.seed, 1 << 26, 30)}
         ex = extras(dev, args.seed, n)
-        # 5 repeats of the same K-step region (each re-warmed), and the reference
-        # reset-distribution start (one tile per board) instead of the synthetic fill
-        reps = [timed_steps(env, plan, chunk, chunk, world, dev)[0] for _ in range(5)]
-        vals = [n * K / r for r in reps]
-        ex["repeat_5"] = {"values": vals, "median": sorted(vals)[2],
-                          "spread": (max(vals) - min(vals)) / sorted(vals)[2]}
+        # the reference reset-distribution start (one tile per board) instead of the synthetic fill
         env2 = VecGame(n, device=dev, seed=args.seed, board_offset=offset)
         env2.reset()
         el2, _ = timed_steps(env2, plan, W, chunk, world, dev)

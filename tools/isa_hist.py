@@ -1,7 +1,11 @@
 """Instruction histogram of chosen basic blocks of one kernel in an assembly file, with a modelled
 issue cost per SIMD (cycles per wave-instruction measured by tools/instr_rate.hip on MI355X,
 profiles/r02/instr_rate.txt; unknown opcodes count as full rate).
-usage: python tools/isa_hist.py build/r48_env.s <kernel substring> <block label> [<block label> ...]"""
+usage: python tools/isa_hist.py build/r48_env.s <kernel substring> <block label> [<block label> ...]
+       python tools/isa_hist.py build/r48_env.s <kernel substring> --auto-loop
+--auto-loop: the loop (by its "Loop: Header=" annotations) holding the most VALU, its
+unconditional blocks only (the .LBB-labelled ones; the %bb fall-through blocks of that loop are
+its conditional branches: tile sum on the last step, auto-reset)."""
 import collections
 import re
 import sys
@@ -25,19 +29,41 @@ def cost(op):
     return FULL
 
 
-s = open(sys.argv[1]).read()
-m = re.search(r"^(_Z\S*%s\S*):\s*;" % re.escape(sys.argv[2]), s, re.M)
-body = s[m.end():s.index(".Lfunc_end", m.end())]
-want = set(sys.argv[3:])
-c = collections.Counter()
-for b in re.split(r"^(?=\.LBB\S+:|; %bb\.)", body, flags=re.M):
-    if b.split(":")[0].split()[-1] in want:
-        for ln in b.splitlines():
-            t = ln.split()
-            if t and t[0].startswith("v_"):
-                c[t[0]] += 1
-tot = sum(c.values())
-cyc = sum(cost(k) * v for k, v in c.items())
-for k, v in sorted(c.items(), key=lambda x: -x[1] * cost(x[0])):
-    print("%4d %-26s %6.1f cyc" % (v, k, v * cost(k)))
-print("VALU %d, modelled %.0f SIMD cycles per wave pass (%.2f per instruction)" % (tot, cyc, cyc / tot))
+def loop_blocks(body):
+    """.LBB blocks of the loop with the most VALU (header included)."""
+    loops = collections.defaultdict(list)
+    for b in re.split(r"^(?=\.LBB\S+:|; %bb\.)", body, flags=re.M):
+        lab = b.split(":")[0].split()[-1]
+        head = b[:300]
+        mm = re.search(r"Header=(BB\S+) Depth", head)
+        hd = mm.group(1) if mm else (lab[2:] if "Loop Header" in head else None)
+        if hd:
+            loops[hd].append((lab, len(re.findall(r"^\s+v_", b, re.M))))
+    best = max(loops.values(), key=lambda bl: sum(v for _, v in bl))
+    return [lab for lab, _ in best if lab.startswith(".LBB")]
+
+
+def analyse(path, kernel, blocks=None):
+    s = open(path).read()
+    m = re.search(r"^(_Z\S*%s\S*):\s*;" % re.escape(kernel), s, re.M)
+    body = s[m.end():s.index(".Lfunc_end", m.end())]
+    want = set(blocks) if blocks else set(loop_blocks(body))
+    c = collections.Counter()
+    for b in re.split(r"^(?=\.LBB\S+:|; %bb\.)", body, flags=re.M):
+        if b.split(":")[0].split()[-1] in want:
+            for ln in b.splitlines():
+                t = ln.split()
+                if t and t[0].startswith("v_"):
+                    c[t[0]] += 1
+    return c, sorted(want)
+
+
+if __name__ == "__main__":
+    args = [a for a in sys.argv[3:] if a != "--auto-loop"]
+    c, blocks = analyse(sys.argv[1], sys.argv[2], args or None)
+    tot = sum(c.values())
+    cyc = sum(cost(k) * v for k, v in c.items())
+    for k, v in sorted(c.items(), key=lambda x: -x[1] * cost(x[0])):
+        print("%4d %-26s %6.1f cyc" % (v, k, v * cost(k)))
+    print("blocks %s" % " ".join(blocks))
+    print("VALU %d, modelled %.0f SIMD cycles per wave pass (%.2f per instruction)" % (tot, cyc, cyc / tot))

@@ -1,0 +1,103 @@
+"""Assemble the committed round-2 profile summaries that bench.py reads, from a tools/prof_r02.sh
+run (gpurun_out/prof) and the shipped build's assembly (make asm -> build/r48_env.s).
+
+Writes under profiles/r02/:
+  pmc_k_step_n.json      k_step_n (2^20 boards, K = 20 steps per dispatch, the bench's dispatch):
+                         SQ counters per dispatch, VALU wave-instructions per board-step
+                         (SQ_INSTS_VALU), HBM bytes per dispatch (FETCH_SIZE x 2 + WRITE_SIZE, the
+                         gfx950 corrections of /opt/skills/guides/MI355X_MICROARCH.md), and the
+                         modelled VALU issue cycles of the shipped loop (tools/isa_hist.py: static
+                         instruction mix x measured issue costs, profiles/r02/instr_rate.txt)
+  pmc_k_step_2p20.json   k_step (one step per launch, boards through HBM), 2^20 boards
+  pmc_k_step_2p26.json   same, 2^26 boards (past the 256 MiB Infinity Cache)
+  kernel_stats_bench.csv rocprofv3 --kernel-trace --stats of `python3 bench.py --gpus 1 --steps 20
+                         --warmup 5` (the driver's command)
+  roofline_from_trace.json  the bench roofline recomputed from that trace (median k_step_n dispatch)
+usage: python tools/make_r02_profiles.py [gpurun_out/prof]"""
+import csv
+import json
+import os
+import shutil
+import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import isa_hist  # noqa: E402
+from pmc_summary import summarize  # noqa: E402
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OUT = os.path.join(ROOT, "profiles", "r02")
+SIMDS, CLOCK_GHZ = 1024, 2.4
+BOARDS, K = 1 << 20, 20
+KSTEPN = "k_step_nILb1ELb1ELb0ELi1"
+
+
+def hbm_bytes(pm):
+    return (2.0 * pm["FETCH_SIZE"] + pm["WRITE_SIZE"]) * 1024.0
+
+
+def main():
+    d = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "gpurun_out", "prof")
+    os.makedirs(OUT, exist_ok=True)
+    # ---- k_step_n
+    s = summarize("k_step_n", BOARDS // 2, [os.path.join(d, x) for x in ("sqa", "sqb", "stepn_fetch", "stepn_write")])
+    pm = s["per_dispatch_mean"]
+    bsteps = BOARDS * K
+    hist, blocks = isa_hist.analyse(os.path.join(ROOT, "build", "r48_env.s"), KSTEPN)
+    valu = sum(hist.values())
+    cyc = sum(isa_hist.cost(k) * v for k, v in hist.items())
+    s.update({
+        "kernel": "k_step_n<RANDOM=1,AUTO_RESET=1,REWARD=0,NP=1>",
+        "boards": BOARDS, "steps_per_dispatch": K, "board_steps_per_dispatch": bsteps,
+        "source": "rocprofv3 --pmc passes (one counter group each) of tools/prof_stepn.py 20 300, tools/prof_r02.sh",
+        "valu_wave_instr_per_board_step": pm["SQ_INSTS_VALU"] / bsteps,
+        "hbm_bytes_per_dispatch": hbm_bytes(pm),
+        "algorithmic_bytes_per_dispatch": 34 * BOARDS,
+        "isa_loop": {"asm": "build/r48_env.s (make asm)", "blocks": blocks, "valu_per_wave_pass": valu,
+                     "board_steps_per_wave_pass": 128, "modelled_issue_cycles_per_wave_pass": cyc,
+                     "histogram": dict(hist.most_common())},
+        "modelled_cycles_per_board_step": cyc / 128.0,
+        "note": "a wave pass = one step of the 128 boards of a wave (64 lanes x a board pair); issue costs per "
+                "instruction from profiles/r02/instr_rate.txt (8 independent chains x 8 waves per SIMD)",
+    })
+    json.dump(s, open(os.path.join(OUT, "pmc_k_step_n.json"), "w"), indent=1)
+    # ---- k_step at 2^20 and 2^26
+    for tag, n in (("2p20", 1 << 20), ("2p26", 1 << 26)):
+        k = summarize("k_step<", n // 2, [os.path.join(d, "k%s_fetch" % tag[2:]), os.path.join(d, "k%s_write" % tag[2:])])
+        pk = k["per_dispatch_mean"]
+        k.update({"kernel": "k_step<RANDOM=1,AUTO_RESET=1,REWARD=0>", "boards": n,
+                  "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of tools/prof_kstep.py, tools/prof_r02.sh",
+                  "hbm_bytes_per_launch": hbm_bytes(pk), "algorithmic_bytes_per_launch": 34 * n,
+                  "traffic_over_algorithmic": hbm_bytes(pk) / (34.0 * n),
+                  "correction": "bytes = (2 x FETCH_SIZE + WRITE_SIZE) x 1024 (KiB; gfx950 FETCH_SIZE halving)"})
+        if n <= (1 << 22):
+            k["cache_note"] = ("36 MB per step fits the 256 MiB Infinity Cache: these fabric-side counters include "
+                               "MALL hits, so this is traffic past L2, not HBM traffic")
+        json.dump(k, open(os.path.join(OUT, "pmc_k_step_%s.json" % tag), "w"), indent=1)
+    # ---- kernel trace of the driver's bench command
+    shutil.copy(os.path.join(d, "kt", "kt_kernel_stats.csv"), os.path.join(OUT, "kernel_stats_bench.csv"))
+    durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+            for r in csv.DictReader(open(os.path.join(d, "kt", "kt_kernel_trace.csv")))
+            if "k_step_n" in r["Kernel_Name"] and int(r["Grid_Size_X"]) == BOARDS // 2]
+    med = statistics.median(durs)
+    cyc_bs = cyc / 128.0
+    ach = cyc_bs * bsteps / (med * 1e-9) / 1e9
+    rt = {"kernel": "k_step_n<RANDOM=1,AUTO_RESET=1,REWARD=0,NP=1>", "dispatches": len(durs),
+          "median_dispatch_ns": med, "mean_dispatch_ns": sum(durs) / len(durs),
+          "board_steps_per_dispatch": bsteps,
+          "modelled_issue_cycles_per_board_step": cyc_bs,
+          "achieved_G_issue_cycles_per_s": ach, "peak_G_issue_cycles_per_s": SIMDS * CLOCK_GHZ,
+          "frac": ach / (SIMDS * CLOCK_GHZ),
+          "valu_wave_instr_per_board_step_pmc": pm["SQ_INSTS_VALU"] / bsteps,
+          "instr_rate_frac": pm["SQ_INSTS_VALU"] / (med * 1e-9) / 1e9 / (SIMDS * CLOCK_GHZ / 2.0),
+          "formula": "frac = modelled issue cycles per board-step x 2^20 x 20 / median dispatch time / "
+                     "(1024 SIMDs x 2.4 GHz); instr_rate_frac = SQ_INSTS_VALU per dispatch / median dispatch time / "
+                     "(1024 SIMDs x 2.4 GHz / 2 cycles per full-rate wave64 instruction)",
+          "trace": "profiles/r02/kernel_stats_bench.csv (rocprofv3 --kernel-trace --stats of python3 bench.py --gpus 1 "
+                   "--steps 20 --warmup 5)"}
+    json.dump(rt, open(os.path.join(OUT, "roofline_from_trace.json"), "w"), indent=1)
+    print(json.dumps(rt, indent=1))
+
+
+if __name__ == "__main__":
+    main()
