@@ -140,6 +140,16 @@ int r48_values_move(int32_t *boards, const int8_t *actions, int64_t n, uint8_t *
 int r48_values_check(const int32_t *boards, int64_t n, int32_t rows, int32_t cols,
                      uint8_t *filled, uint8_t *over, void *stream);
 
+/* Any board shape (Game(table_matrix_size) for sizes > 4, GameClient.py:19-27): boards
+ * int32[n][rows][cols] of raw values, rows and cols in 1..R48_GRID_MAX.
+ * r48_values_move_grid = update_matrix (:129-254), in place, changed uint8[n] (nullable);
+ * r48_values_check_grid = has_table_filled (:96-100) / has_game_over (:65-94). */
+#define R48_GRID_MAX 4096
+int r48_values_move_grid(int32_t *boards, int64_t n, int32_t rows, int32_t cols, const int8_t *actions,
+                         uint8_t *changed, void *stream);
+int r48_values_check_grid(const int32_t *boards, int64_t n, int32_t rows, int32_t cols, uint8_t *filled,
+                          uint8_t *over, void *stream);
+
 /* ---- A3C pieces around the env step (algorithm/a3c/a3c.py) ---- */
 #define R48_FEAT_VALUES 0     /* raw tile values 2^e, as a3c.py:37-39,139 feed the network */
 #define R48_FEAT_EXPONENTS 1  /* the exponent e (a normalised input for the corrected mode) */

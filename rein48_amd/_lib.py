@@ -73,6 +73,8 @@ SIGNATURES = {
     "r48_env_clear_errors": (C.c_int, [_P, _P]),
     "r48_values_move": (C.c_int, [_P, _P, _I64, _P, _P, _P]),
     "r48_values_check": (C.c_int, [_P, _I64, _I32, _I32, _P, _P, _P]),
+    "r48_values_move_grid": (C.c_int, [_P, _I64, _I32, _I32, _P, _P, _P]),
+    "r48_values_check_grid": (C.c_int, [_P, _I64, _I32, _I32, _P, _P, _P]),
     "r48_board_features": (C.c_int, [_P, _I64, _I32, _I32, _P, _P]),
     "r48_sample_actions": (C.c_int, [_P, _I64, _U64, _I64, _U32, _P, _P, _P, _P]),
     "r48_discounted_returns": (C.c_int, [_P, _P, _P, _I32, _I64, C.c_float, _I32, _P, _P]),

@@ -650,6 +650,90 @@ __global__ __launch_bounds__(kBlock) void k_values_check(const int32_t *__restri
         over[i] = (uint8_t)(full && !eq);
 }
 
+// Any rows x cols (Game(n) for n > 4, GameClient.py:19-27): boards int32[n][rows][cols] of raw
+// values, one thread per (board, line) -- the lines of a move are independent. The reference's
+// two-pointer walk (GameClient.py:141-179) along the line's cells from the wall; `changed`
+// (zeroed by the caller) gets 1 from any line that moved a tile.
+__global__ __launch_bounds__(kBlock) void k_values_move_grid(int32_t *__restrict__ boards, int64_t n, int32_t rows,
+                                                             int32_t cols, const int8_t *__restrict__ actions,
+                                                             uint8_t *__restrict__ changed)
+{
+    const int32_t lines = rows > cols ? rows : cols;
+    const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t i = t / lines;
+    const int32_t line = (int32_t)(t % lines);
+    if (i >= n)
+        return;
+    const int a = actions[i];
+    if (a < 0 || a > 3)
+        return;
+    const bool vert = a < 2, rev = (a & 1) != 0;
+    const int32_t len = vert ? rows : cols;
+    if (line >= (vert ? cols : rows))
+        return;
+    int32_t *m = boards + i * (int64_t)rows * cols;
+    // element offset of cell k of this line counted from the wall
+    const int64_t step = vert ? (rev ? -(int64_t)cols : cols) : (rev ? -1 : 1);
+    const int64_t first = vert ? (rev ? (int64_t)(rows - 1) * cols + line : line)
+                               : (int64_t)line * cols + (rev ? cols - 1 : 0);
+    int32_t *p = m + first;
+    bool moved = false;
+    int32_t ii = 0, j = 1;
+    while (j < len) {
+        while (j < len && p[j * step] == 0)
+            j++;
+        if (j == len)
+            break;
+        const int32_t vj = p[j * step];
+        const int32_t vi = p[ii * step];
+        if (vi == 0) {                 // switch: the tile slides into the empty cell
+            p[ii * step] = vj;
+            p[j * step] = 0;
+            moved = true;
+        } else if (vi == vj) {         // merge
+            p[ii * step] = vi + vj;
+            p[j * step] = 0;
+            ii++;
+            moved = true;
+        } else {                       // move behind i (a no-op when it already is there)
+            if (ii + 1 != j) {
+                p[(ii + 1) * step] = vj;
+                p[j * step] = 0;
+                moved = true;
+            }
+            ii++;
+        }
+        j++;
+    }
+    if (moved && changed)
+        changed[i] = 1;
+}
+
+// has_table_filled / has_game_over (GameClient.py:65-100) on any rows x cols, one thread per board
+__global__ __launch_bounds__(kBlock) void k_values_check_grid(const int32_t *__restrict__ boards, int64_t n,
+                                                              int32_t rows, int32_t cols,
+                                                              uint8_t *__restrict__ filled, uint8_t *__restrict__ over)
+{
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n)
+        return;
+    const int32_t *m = boards + i * (int64_t)rows * cols;
+    bool full = true, eq = false;
+    for (int32_t r = 0; r < rows; r++)
+        for (int32_t c = 0; c < cols; c++) {
+            const int32_t v = m[(int64_t)r * cols + c];
+            full &= v != 0;
+            if (r + 1 < rows)
+                eq |= v == m[(int64_t)(r + 1) * cols + c];
+            if (c + 1 < cols)
+                eq |= v == m[(int64_t)r * cols + c + 1];
+        }
+    if (filled)
+        filled[i] = (uint8_t)full;
+    if (over)
+        over[i] = (uint8_t)(full && !eq);
+}
+
 }  // namespace
 
 // =============================================================================== C-ABI
@@ -1043,6 +1127,33 @@ int r48_values_check(const int32_t *boards, int64_t n, int32_t rows, int32_t col
     hipLaunchKernelGGL(k_values_check, grid_for(n), dim3(kBlock), 0, (hipStream_t)stream, boards, n, rows, cols,
                        filled, over);
     return launched("k_values_check");
+}
+
+int r48_values_move_grid(int32_t *boards, int64_t n, int32_t rows, int32_t cols, const int8_t *actions,
+                         uint8_t *changed, void *stream)
+{
+    if (!boards || !actions || n < 0 || rows < 1 || cols < 1 || rows > R48_GRID_MAX || cols > R48_GRID_MAX)
+        return fail(R48_EINVAL, "boards/actions NULL, n < 0 or rows/cols outside 1..R48_GRID_MAX");
+    if (n == 0)
+        return R48_OK;
+    if (changed && hipMemsetAsync(changed, 0, (size_t)n, (hipStream_t)stream) != hipSuccess)
+        return fail(R48_EHIP, "hipMemsetAsync failed");
+    const int64_t threads = n * (int64_t)(rows > cols ? rows : cols);
+    hipLaunchKernelGGL(k_values_move_grid, grid_for(threads), dim3(kBlock), 0, (hipStream_t)stream, boards, n, rows,
+                       cols, actions, changed);
+    return launched("k_values_move_grid");
+}
+
+int r48_values_check_grid(const int32_t *boards, int64_t n, int32_t rows, int32_t cols, uint8_t *filled,
+                          uint8_t *over, void *stream)
+{
+    if (!boards || n < 0 || rows < 1 || cols < 1 || rows > R48_GRID_MAX || cols > R48_GRID_MAX)
+        return fail(R48_EINVAL, "boards NULL, n < 0 or rows/cols outside 1..R48_GRID_MAX");
+    if (n == 0)
+        return R48_OK;
+    hipLaunchKernelGGL(k_values_check_grid, grid_for(n), dim3(kBlock), 0, (hipStream_t)stream, boards, n, rows,
+                       cols, filled, over);
+    return launched("k_values_check_grid");
 }
 
 }  // extern "C"

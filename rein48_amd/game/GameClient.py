@@ -18,8 +18,11 @@ row-major blank list, then uniform(0,1) > 0.1 -> 2 else 4, GameClient.py:121-125
 `random.seed(s)` gives the reference's trajectory bit for bit. The batched VecGame draws
 on device instead (Philox).
 
-The GPU env kernel is 4x4: Game(n) with n > 4 raises
-NotImplementedError. The static helpers accept any integer tiles on matrices up to 4x4
+Board sizes: the exponent kernels are 4x4. Game(n) with n > 4 runs
+on the value-domain grid kernels (r48_values_move_grid / r48_values_check_grid: any rows x
+cols, one GPU thread per line of the move), composed like GameClient.py:45-51 with the spawn
+drawn from the global `random` on the host, so it follows the reference's trajectories under
+`random.seed` as well. The static helpers accept any integer tiles on any rectangular matrix
 (the reference's own tests use 4x1 / 1x4 matrices and the value 1).
 """
 import copy
@@ -80,6 +83,33 @@ def _pad(matrix, code):
     return board, r0, c0
 
 
+def _grid_tensor(matrix):
+    rows, cols = len(matrix), len(matrix[0])
+    if any(len(r) != cols for r in matrix):
+        raise ValueError("rein48 kernels need a rectangular matrix")
+    return torch.tensor(matrix, dtype=torch.int32, device=_device()).contiguous(), rows, cols
+
+
+def _grid_move(matrix, code):
+    """update_matrix on any rows x cols (r48_values_move_grid), written back in place."""
+    b, rows, cols = _grid_tensor(matrix)
+    a = torch.tensor([code], dtype=torch.int8, device=b.device)
+    check(_lib.load().r48_values_move_grid(ptr(b), 1, rows, cols, ptr(a), None,
+                                           torch.cuda.current_stream(b.device).cuda_stream))
+    out = b.cpu().tolist()
+    for i in range(rows):
+        matrix[i][:] = out[i]
+
+
+def _grid_check(matrix):
+    b, rows, cols = _grid_tensor(matrix)
+    out = torch.empty(2, dtype=torch.uint8, device=b.device)
+    check(_lib.load().r48_values_check_grid(ptr(b), 1, rows, cols, ptr(out[0:1]), ptr(out[1:2]),
+                                            torch.cuda.current_stream(b.device).cuda_stream))
+    filled, over = out.cpu().tolist()
+    return bool(filled), bool(over)
+
+
 class Game:
 
     state_matrix, state_space_size = None, 0
@@ -88,11 +118,19 @@ class Game:
         self.reward_space_size = 1
         self.action_space_size = 4
         self.state_space_size = 4 if table_matrix_size < 4 else table_matrix_size
-        if self.state_space_size != 4:
-            raise NotImplementedError("the MI355X env kernel is 4x4 (got table_matrix_size=%r)"
-                                      % table_matrix_size)
-        self._vec = VecGame(1, device=_device())
-        self._one = torch.ones(1, dtype=torch.uint8, device=self._vec.device)
+        dev = _device()
+        # 4x4: the exponent env kernels on a one-board env whose board is byte 0..15 of a 32-byte
+        # device scratch ([16] action, [17] rank, [18] four, [19] spawn mask, [20] changed,
+        # [21] blanks after the move, [22] done), staged through one pinned host buffer: a step
+        # is 2 kernels, 3 small copies in, 2 out, 2 stream synchronisations. Larger boards: the
+        # value-domain grid kernels.
+        self._vec = VecGame(1, device=dev) if self.state_space_size == 4 else None
+        if self._vec is not None:
+            self._d = torch.zeros(32, dtype=torch.int8, device=dev)
+            self._h = torch.zeros(32, dtype=torch.int8).pin_memory()
+            self._hn = self._h.numpy()
+            check(self._vec._lib.r48_env_bind_boards(self._vec._env, ptr(self._d)))
+            self._vec.boards = self._d[:16].view(1, 16)
         self.reset()
 
     # ---------------------------------------------------------------- public (GameClient.py:33-51)
@@ -105,31 +143,35 @@ class Game:
 
     def step(self, action):
         code = action_code(action)
-        exps = [_exponent(v) for row in self.state_matrix for v in row]
+        exps = [_exponent(v) for row in self.state_matrix for v in row] if self._vec is not None else [None]
         if any(e is None for e in exps):
             # tiles outside 2^e: the value-domain kernels, composed like GameClient.py:45-51
             self.state_matrix, reward, changed = self.update_matrix(self.state_matrix, code)
             if changed:
                 self.state_matrix = Game.random_fill_grid(self.state_matrix)
             return self.state_matrix, reward, Game.has_game_over(self.state_matrix)
-        vec = self._vec
-        dev = vec.device
-        vec.boards.copy_(torch.tensor(exps, dtype=torch.int8).view(1, 16))
-        act = torch.tensor([code], dtype=torch.int8, device=dev)
-        changed_t, n_blank_t = vec.move(act)
-        changed, n_blank = (int(x) for x in torch.stack([changed_t, n_blank_t]).view(2).cpu())
+        vec, d, h, hn = self._vec, self._d, self._h, self._hn
+        lib, st = vec._lib, torch.cuda.current_stream(vec.device)
+        base = d.data_ptr()
+        hn[:16] = exps
+        hn[16] = code
+        d[:17].copy_(h[:17], non_blocking=True)
+        check(lib.r48_env_move(vec._env, base + 16, 0, base + 20, base + 21, None, st.cuda_stream))
+        h[20:22].copy_(d[20:22], non_blocking=True)
+        st.synchronize()
+        changed, n_blank = int(hn[20]), int(hn[21])
         if changed:
-            rank = random.randint(0, n_blank - 1)                # GameClient.py:121
-            four = 0 if random.uniform(0, 1) > 0.1 else 1         # GameClient.py:125
-            done_t = vec.spawn(torch.tensor([rank], dtype=torch.uint8, device=dev),
-                               torch.tensor([four], dtype=torch.uint8, device=dev), mask=self._one)
-        else:
-            done_t = vec.spawn(self._one, self._one, mask=self._one * 0)
-        host = torch.cat([vec.boards.view(16).to(torch.int16), done_t.to(torch.int16)]).cpu().tolist()
+            hn[17] = random.randint(0, n_blank - 1)                 # GameClient.py:121
+            hn[18] = 0 if random.uniform(0, 1) > 0.1 else 1         # GameClient.py:125
+        hn[19] = changed                                           # unchanged: no spawn, only game over
+        d[17:20].copy_(h[17:20], non_blocking=True)
+        check(lib.r48_env_spawn(vec._env, base + 19, base + 17, base + 18, base + 22, st.cuda_stream))
+        h[:23].copy_(d[:23], non_blocking=True)
+        st.synchronize()
         for k in range(16):  # write back into the SAME lists (aliasing, GameClient.py:45)
-            e = host[k]
+            e = int(hn[k])
             self.state_matrix[k // 4][k % 4] = (1 << e) if e else 0
-        return self.state_matrix, 0, bool(host[16])
+        return self.state_matrix, 0, bool(hn[22])
 
     # ---------------------------------------------------------------- static helpers (:55-269)
     @staticmethod
@@ -139,6 +181,8 @@ class Game:
     @staticmethod
     def _check(game_matrix):
         rows, cols = len(game_matrix), len(game_matrix[0])
+        if rows > 4 or cols > 4:
+            return _grid_check(game_matrix)
         board, _, _ = _pad(game_matrix, 0)
         dev = _device()
         b = torch.tensor(board, dtype=torch.int32, device=dev)
@@ -174,6 +218,9 @@ class Game:
         returns (matrix, 0, changed)."""
         code = action_code(action)
         origin = copy.deepcopy(matrix)
+        if len(matrix) > 4 or len(matrix[0]) > 4:
+            _grid_move(matrix, code)
+            return matrix, 0, (origin != matrix)
         board, r0, c0 = _pad(matrix, code)
         dev = _device()
         b = torch.tensor(board, dtype=torch.int32, device=dev)

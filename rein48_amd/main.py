@@ -9,8 +9,18 @@ from .control.hand import Hand
 from .control.rand import Rand
 from .game.GameClient import Game
 
-BANNER = "PLEASE INPUT [ACTION DIRECTION] TO PLAY THIS GAME.\n" \
-         "Left: [L] or [l] \nRight:[R] or [r] \nUp:   [U] or [u] \nDown: [D] or [d] "
+# hand-mode banner, the same text main.py:22-33 prints (a "2048" in ASCII art + the key help)
+_ART = (r"    ---         ------           /|       /-------\  ",
+        r"  /     \     /        \        / |      |         | ",
+        r" |       |   |          |      /  |      |         | ",
+        r"        /    |          |     /   |       \_______/  ",
+        r"      /      |          |    /    |       /       \  ",
+        r"    /        |          |   /_____|_____ |         | ",
+        r"  /           \        /          |      |         | ",
+        r" ---------      ------            |       \_______/  ")
+BANNER = "\n".join(("#" * 53,) + _ART + (
+    "PLEASE INPUT [ACTION DIRECTION] TO PLAY THIS GAME.",
+    "Left: [L] or [l] ", "Right:[R] or [r] ", "Up:   [U] or [u] ", "Down: [D] or [d] ", "#" * 53))
 
 
 def play(game, control="hand", show_state=False, show_result=True):

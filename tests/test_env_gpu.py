@@ -177,9 +177,65 @@ def test_drop_in_game_surface():
             g.step(bad)
     for alias in ("Up", "d", "LEFT", "r", 0, 1, 2, 3, True, 2.0):
         g.step(alias)
-    with pytest.raises(NotImplementedError):
-        Game(5)
+    g5 = Game(5)
+    assert g5.state_space_size == 5 and len(g5.state_matrix) == 5 and len(g5.state_matrix[0]) == 5
+    assert sum(v != 0 for r in g5.state_matrix for v in r) == 1
     assert Game(3).state_space_size == 4
+
+
+@pytest.mark.parametrize("size", [5, 6, 9])
+def test_drop_in_game_larger_boards_follow_reference_rules(size):
+    """Game(n > 4) (GameClient.py:19-27 accepts any n >= 4): the value-domain grid kernels + the
+    host spawn draws reproduce the reference rules under random.seed -- checked against
+    oracle/game_port.PortGame(n), the pure-Python restatement of the reference Game, step for
+    step with the same seeds (parity pinned to the 4x4 reference fixtures through the port;
+    the reference ships no n > 4 fixtures)."""
+    import random
+    from oracle.game_port import PortGame, random_action
+    from rein48_amd.game import Game
+    for seed in range(3):
+        random.seed(seed)
+        g = Game(size)
+        state = [r[:] for r in g.state_matrix]
+        random.seed(seed)
+        p = PortGame(size)
+        assert p.state_matrix == state
+        for t in range(400):
+            st = random.getstate()
+            a = random_action()
+            s1, _, d1 = g.step(a)
+            random.setstate(st)
+            a2 = random_action()
+            s2, _, d2 = p.step(a2)
+            assert a == a2 and s1 == s2 and d1 == d2, (size, seed, t)
+            if d1:
+                break
+
+
+def test_static_helpers_on_any_shape():
+    """update_matrix / has_game_over / has_table_filled on rectangular matrices beyond 4x4
+    (r48_values_move_grid / r48_values_check_grid) == the port's restatement."""
+    from oracle.game_port import PortGame
+    from rein48_amd.game import Game
+    rng = np.random.default_rng(3)
+    for rows, cols in ((5, 7), (1, 9), (9, 1), (6, 6), (12, 5)):
+        for _ in range(30):
+            m = (2 ** rng.integers(0, 4, size=(rows, cols))) * (rng.random((rows, cols)) < 0.6)
+            m = m.astype(int).tolist()
+            for a in range(4):
+                want = [r[:] for r in m]
+                _, _, wc = PortGame.move(want, a)
+                got = [r[:] for r in m]
+                rows_before = [id(r) for r in got]
+                _, rw, gc = Game.update_matrix(got, a)
+                assert got == want and gc == wc and rw == 0, (rows, cols, a)
+                assert [id(r) for r in got] == rows_before          # mutated in place
+        full = (2 ** (1 + (np.arange(36).reshape(6, 6) % 5))).tolist()     # no equal neighbours? check
+        assert Game.has_table_filled(full)
+        over_want = PortGame.over(full)
+        assert Game.has_game_over(full) == over_want
+        full[2][3] = 0
+        assert not Game.has_table_filled(full) and not Game.has_game_over(full)
 
 
 # ---------------------------------------------------------------- Philox mode vs oracle
