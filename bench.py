@@ -116,8 +116,9 @@ SYNC_POLL = False  # --sync: poll the region's last HIP event before the closing
 def timed_steps(env, plan, W, chunk, world, dev):
     """W untimed warm-up steps through the same path (in calls of the timed chunk size) --
     continued, still untimed, until at least SETTLE_S of stepping has run -- then exactly sum(plan)
-    steps bracketed by barrier + synchronize. -> (slowest rank's wall seconds, device ms of the
-    timed calls from HIP events on the launch stream, one entry per call)."""
+    steps bracketed by barrier + synchronize (opening: synchronize, barrier, synchronize, t0;
+    closing: synchronize, t1, barrier). -> (slowest rank's wall seconds t1 - t0, max over ranks;
+    device ms of the timed calls from HIP events on the launch stream, one entry per call)."""
     t_w = time.perf_counter()
     for c in chunks(W, chunk) if W else []:
         env.step_n(c, auto_reset=True)
@@ -133,6 +134,7 @@ def timed_steps(env, plan, W, chunk, world, dev):
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
+        torch.cuda.synchronize(dev)          # the barrier's own device work done before t0
     t0 = time.perf_counter()
     for (a, b), c in zip(ev, plan):
         a.record(s)
@@ -145,9 +147,12 @@ def timed_steps(env, plan, W, chunk, world, dev):
         while not last.query():
             pass
     torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    # each rank's K steps end at its own synchronize; the job's time is the slowest rank's
+    # (max over ranks below), so the closing barrier's collective latency (tens of us with RCCL,
+    # against a ~100 us region at --steps 20) is not counted as stepping time
     if world > 1:
         dist.barrier()
-    t1 = time.perf_counter()
     return max_over_ranks(t1 - t0, dev, world), [a.elapsed_time(b) for a, b in ev]
 
 

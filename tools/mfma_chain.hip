@@ -1,0 +1,81 @@
+// MFMA issue vs dependent-accumulation latency on gfx950, one wave per SIMD (256 CUs x 4 waves):
+// chains of v_mfma_f32_32x32x16_bf16 / v_mfma_f32_16x16x32_bf16 accumulating into 1, 2 or 4
+// independent accumulators (C = previous D of the same accumulator).
+//   hipcc -O3 --offload-arch=gfx950 tools/mfma_chain.hip -o build/mfma_chain && build/mfma_chain
+#include <hip/hip_runtime.h>
+#include <cstdio>
+
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+constexpr int N = 2048;
+
+template <int ACC>
+__global__ __launch_bounds__(256, 1) void k32(float *out, int n)
+{
+    bf16x8 a, b;
+    for (int j = 0; j < 8; j++) { a[j] = (short)(threadIdx.x + j); b[j] = (short)(threadIdx.x * 3 + j); }
+    f32x16 c[ACC];
+    for (int q = 0; q < ACC; q++) c[q] = f32x16{};
+    for (int i = 0; i < n; i += ACC) {
+#pragma unroll
+        for (int q = 0; q < ACC; q++)
+            c[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c[q], 0, 0, 0);
+    }
+    float s = 0;
+    for (int q = 0; q < ACC; q++) for (int r = 0; r < 16; r++) s += c[q][r];
+    out[blockIdx.x * 256 + threadIdx.x] = s;
+}
+
+template <int ACC>
+__global__ __launch_bounds__(256, 1) void k16(float *out, int n)
+{
+    bf16x8 a, b;
+    for (int j = 0; j < 8; j++) { a[j] = (short)(threadIdx.x + j); b[j] = (short)(threadIdx.x * 3 + j); }
+    f32x4 c[ACC];
+    for (int q = 0; q < ACC; q++) c[q] = f32x4{};
+    for (int i = 0; i < n; i += ACC) {
+#pragma unroll
+        for (int q = 0; q < ACC; q++)
+            c[q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c[q], 0, 0, 0);
+    }
+    float s = 0;
+    for (int q = 0; q < ACC; q++) for (int r = 0; r < 4; r++) s += c[q][r];
+    out[blockIdx.x * 256 + threadIdx.x] = s;
+}
+
+template <typename K>
+void run(const char *name, K kern, float *out, int cus)
+{
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    float best = 1e30f;
+    for (int r = 0; r < 5; r++) {
+        hipEventRecord(a);
+        hipLaunchKernelGGL(kern, dim3(cus), dim3(256), 0, 0, out, N);
+        hipEventRecord(b);
+        hipEventSynchronize(b);
+        float ms;
+        hipEventElapsedTime(&ms, a, b);
+        best = ms < best ? ms : best;
+    }
+    printf("%-24s %.4f ms  %.1f cycles per MFMA per wave @2.4GHz\n", name, best, best * 1e-3 * 2.4e9 / N);
+}
+
+int main()
+{
+    int cus = 256;
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
+    float *out;
+    hipMalloc(&out, cus * 256 * 4);
+    for (int w = 0; w < 20; w++) hipLaunchKernelGGL(k32<4>, dim3(cus), dim3(256), 0, 0, out, N);
+    hipDeviceSynchronize();
+    run("32x32x16 1 chain", k32<1>, out, cus);
+    run("32x32x16 2 chains", k32<2>, out, cus);
+    run("32x32x16 4 chains", k32<4>, out, cus);
+    run("16x16x32 1 chain", k16<1>, out, cus);
+    run("16x16x32 2 chains", k16<2>, out, cus);
+    run("16x16x32 4 chains", k16<4>, out, cus);
+    return 0;
+}
