@@ -248,8 +248,8 @@ def extras(dev, seed, n_small):
     ms = a.elapsed_time(b) / reps
     out["rollout_fused"] = {"boards": n_small, "steps_per_launch": K, "kernel_ms": ms,
                             "env_steps_per_s": n_small * K / (ms * 1e-3),
-                            "note": "k_rollout: boards stay in VGPRs for K steps; writes action+done per "
-                                    "step (2 B) and the board once per launch"}
+                            "note": "r48_env_rollout (k_step_n with trajectory rows): boards stay in VGPRs for K "
+                                    "steps; writes action+done per step (2 B) and the board once per launch"}
     return out
 
 

@@ -300,12 +300,15 @@ __device__ unsigned long long r48_stamp_buf[65536 * 4];
 #ifndef R48_STEPN_NP
 #define R48_STEPN_NP 1
 #endif
-template <bool RANDOM, bool AUTO_RESET, bool REWARD, int NP>
+// TRAJ (r48_env_rollout): also every step's action and done into row t of traj_actions /
+// traj_done ([n_steps][n], each nullable) -- one 2-byte store per plane per pair and step.
+template <bool RANDOM, bool AUTO_RESET, bool REWARD, int NP, bool TRAJ = false>
 __global__ __launch_bounds__(kBlock) void k_step_n(int8_t *boards, int64_t n, int64_t gid0, uint32_t k0, uint32_t k1,
                                                    uint32_t step0, int32_t n_steps, int8_t *__restrict__ actions,
                                                    uint8_t *__restrict__ done, uint8_t *__restrict__ changed,
                                                    int32_t *__restrict__ reward, int32_t *__restrict__ score,
-                                                   unsigned long long *err)
+                                                   unsigned long long *err, int8_t *__restrict__ traj_actions = nullptr,
+                                                   uint8_t *__restrict__ traj_done = nullptr)
 {
     constexpr int64_t kTile = (int64_t)kBlock * 2 * NP;
     const int64_t base = (int64_t)blockIdx.x * kTile + 2 * (int64_t)threadIdx.x;
@@ -315,7 +318,8 @@ __global__ __launch_bounds__(kBlock) void k_step_n(int8_t *boards, int64_t n, in
     __shared__ __attribute__((aligned(16))) r48::Orient tab[16];
     load_orient_table(tab);
     if ((int64_t)(blockIdx.x + 1) * kTile <= n && (gid0 & 1) == 0 &&
-        planes_aligned(actions, done, changed, reward, score)) {
+        planes_aligned(actions, done, changed, reward, score) &&
+        (!TRAJ || ((n | (int64_t)((uintptr_t)traj_actions | (uintptr_t)traj_done)) & 1) == 0)) {
         Board b[2 * NP];
         uint32_t a[2 * NP], ob[2 * NP];
         uint64_t q[NP];
@@ -365,6 +369,14 @@ __global__ __launch_bounds__(kBlock) void k_step_n(int8_t *boards, int64_t n, in
                 r[2 * j] = step_lane_lines<RANDOM, AUTO_RESET, REWARD>(b[2 * j], ob[2 * j], tab, a[2 * j], de, sc);
                 r[2 * j + 1] =
                     step_lane_lines<RANDOM, AUTO_RESET, REWARD>(b[2 * j + 1], ob[2 * j + 1], tab, a[2 * j + 1], dd, sc);
+                if (TRAJ) {
+                    const int64_t at = (int64_t)t * n + base + 2 * kBlock * j;
+                    if (traj_actions)
+                        *reinterpret_cast<uint16_t *>(traj_actions + at) = (uint16_t)(r[2 * j].a | (r[2 * j + 1].a << 8));
+                    if (traj_done)
+                        *reinterpret_cast<uint16_t *>(traj_done + at) =
+                            (uint16_t)(r[2 * j].done | (r[2 * j + 1].done << 8));
+                }
             }
         }
 #pragma unroll
@@ -387,6 +399,10 @@ __global__ __launch_bounds__(kBlock) void k_step_n(int8_t *boards, int64_t n, in
                     const Draw d = board_draw((uint64_t)(gid0 + i), step0 + (uint32_t)t, k0, k1);
                     r = step_lane<RANDOM, AUTO_RESET, REWARD, false>(b, a, d, want_score && t == last);
                     b = r.b;
+                    if (TRAJ && traj_actions)
+                        traj_actions[(int64_t)t * n + i] = (int8_t)r.a;
+                    if (TRAJ && traj_done)
+                        traj_done[(int64_t)t * n + i] = (uint8_t)r.done;
                 }
                 emit<RANDOM, REWARD>(r, i, boards, actions, done, changed, reward, score);
             }
@@ -524,30 +540,6 @@ __global__ __launch_bounds__(kBlock) void k_fill_random(int8_t *__restrict__ boa
         row[r] = word;
     }
     store_board(boards, i, Board{row[0], row[1], row[2], row[3]});
-}
-
-// ---------------------------------------------------------------- rollout (K steps in registers)
-__global__ __launch_bounds__(kBlock) void k_rollout(int8_t *__restrict__ boards, int64_t n, int64_t gid0,
-                                                    uint32_t k0, uint32_t k1, uint32_t step0, int32_t n_steps,
-                                                    int8_t *__restrict__ actions, uint8_t *__restrict__ done)
-{
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n)
-        return;
-    Board b = load_board(boards, i);
-    const uint64_t gid = (uint64_t)(gid0 + i);
-    for (int32_t t = 0; t < n_steps; t++) {
-        const Draw d = board_draw(gid, step0 + (uint32_t)t, k0, k1);   // the k_step contract
-        const uint32_t a = d.x >> 30;
-        const r48::StepOut o = r48::step_board<false, false, true>(b, a, d.y, (d.x & 0x3FFFFFFFu) < r48::kFourThresh30);
-        if (o.done)
-            r48::reset_board(b, d.y >> 28, (d.y & 0x0FFFFFFFu) < r48::kFourThresh28);
-        if (actions)
-            actions[(int64_t)t * n + i] = (int8_t)a;
-        if (done)
-            done[(int64_t)t * n + i] = (uint8_t)o.done;
-    }
-    store_board(boards, i, b);
 }
 
 // ---------------------------------------------------------------- score
@@ -958,7 +950,7 @@ void launch_steps(r48_env *env, int32_t n_steps, int8_t *actions, uint32_t flags
         const int64_t tile = (int64_t)kBlock * 2 * R48_STEPN_NP;
         hipLaunchKernelGGL(kern, dim3((unsigned)((env->n + tile - 1) / tile)), dim3(kBlock), 0, stream, env->boards,
                            env->n, env->gid0, k0, k1, env->step_ctr, n_steps, actions, done, changed, reward, score,
-                           env->err);
+                           env->err, (int8_t *)nullptr, (uint8_t *)nullptr);
     };
 #define R48_GO(RN, AR, RW) \
     (n_steps == 1 ? one(k_step<RN, AR, RW>) : many(k_step_n<RN, AR, RW, R48_STEPN_NP>))
@@ -1062,11 +1054,14 @@ int r48_env_rollout(r48_env *env, int32_t n_steps, int8_t *actions, uint8_t *don
     if (n_steps == 0)
         return R48_OK;
     DeviceGuard g(env->device);
-    hipLaunchKernelGGL(k_rollout, grid_for(env->n), dim3(kBlock), 0, (hipStream_t)stream, env->boards, env->n,
-                       env->gid0, (uint32_t)env->seed, (uint32_t)(env->seed >> 32), env->step_ctr, n_steps,
-                       actions, done);
+    // = r48_env_step_n(random policy, auto-reset) that also writes every step's action and done
+    const int64_t tile = (int64_t)kBlock * 2 * R48_STEPN_NP;
+    hipLaunchKernelGGL((k_step_n<true, true, false, R48_STEPN_NP, true>), dim3((unsigned)((env->n + tile - 1) / tile)),
+                       dim3(kBlock), 0, (hipStream_t)stream, env->boards, env->n, env->gid0, (uint32_t)env->seed,
+                       (uint32_t)(env->seed >> 32), env->step_ctr, n_steps, (int8_t *)nullptr, (uint8_t *)nullptr,
+                       (uint8_t *)nullptr, (int32_t *)nullptr, (int32_t *)nullptr, env->err, actions, done);
     env->step_ctr += (uint32_t)n_steps;
-    return launched("k_rollout");
+    return launched("k_step_n (rollout)");
 }
 
 int r48_env_score(r48_env *env, int32_t *out, void *stream)

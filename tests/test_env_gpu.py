@@ -355,11 +355,12 @@ def test_fill_random_matches_oracle(max_exp):
         v.fill_random(0)
 
 
-def test_rollout_equals_repeated_steps():
-    n, K, seed = 30_000, 37, 4242
+@pytest.mark.parametrize("n,offset", [(30_000, 98), (30_001, 97)])   # pair fast path / guarded per-board path
+def test_rollout_equals_repeated_steps(n, offset):
+    K, seed = 37, 4242
     rng = np.random.default_rng(3)
     b0 = rand_boards(rng, n, emax=6, p_empty=0.4)
-    a, b = vec(n, seed=seed, offset=98), vec(n, seed=seed, offset=98)   # even: k_step's pair fast path
+    a, b = vec(n, seed=seed, offset=offset), vec(n, seed=seed, offset=offset)
     put(a, b0)
     put(b, b0)
     acts = torch.empty((K, n), dtype=torch.int8, device=DEV)
