@@ -234,9 +234,11 @@ __global__ __launch_bounds__(kBlock) void k_step(int8_t *boards, int64_t n, int6
     constexpr int64_t kTile = (int64_t)kBlock * 2;
     const int64_t i = (int64_t)blockIdx.x * kTile + 2 * (int64_t)threadIdx.x;
     const bool want_score = score != nullptr;
+    __shared__ __attribute__((aligned(16))) r48::Orient tab[16];
+    load_orient_table(tab);
     if ((int64_t)(blockIdx.x + 1) * kTile <= n && (gid0 & 1) == 0 &&
         planes_aligned(actions, done, changed, reward, score)) {
-        const Board be = load_board(boards, i), bo = load_board(boards, i + 1);
+        Board be = load_board(boards, i), bo = load_board(boards, i + 1);
         uint32_t ae = 0, ao = 0;
         if (!RANDOM) {
             const uint16_t a2 = *reinterpret_cast<const uint16_t *>(actions + i);
@@ -247,8 +249,13 @@ __global__ __launch_bounds__(kBlock) void k_step(int8_t *boards, int64_t n, int6
         }
         Draw de, dd;
         pair_draws((uint64_t)(gid0 + i) >> 1, step, k0, k1, de, dd);
-        const LaneOut re = step_lane<RANDOM, AUTO_RESET, REWARD>(be, ae, de, want_score);
-        const LaneOut ro = step_lane<RANDOM, AUTO_RESET, REWARD>(bo, ao, dd, want_score);
+        // rows -> line form of the action and back through the LDS selector table (k_step_n's
+        // orientation machinery with o = rows on entry and exit)
+        uint32_t obe = 0, obo = 0;
+        LaneOut re = step_lane_lines<RANDOM, AUTO_RESET, REWARD>(be, obe, tab, ae, de, want_score);
+        LaneOut ro = step_lane_lines<RANDOM, AUTO_RESET, REWARD>(bo, obo, tab, ao, dd, want_score);
+        re.b = r48::reorient(be, orient_at(tab, obe));
+        ro.b = r48::reorient(bo, orient_at(tab, obo));
         emit_pair<RANDOM, REWARD>(re, ro, i, boards, actions, done, changed, reward, score);
     } else {
         for (int j = 0; j < 2; j++) {
