@@ -19,10 +19,18 @@ g = torch.Generator(device="cpu").manual_seed(0)
 boards = torch.randint(0, 12, (n, 16), generator=g, dtype=torch.int8).to(dev)
 torch.manual_seed(0)
 net = ActorCriticCNN(dtype=torch.bfloat16).to(dev)
+ref = None
 for path in libs:
     _lib.LIB_PATH, _lib._lib = path, None
     wfrag, bias = pack_cnn(net)
-    run = lambda: cnn_forward(boards, wfrag, bias, exponents=True, logits=False, value=True, actions=True, seed=1)
+    run = lambda: cnn_forward(boards, wfrag, bias, exponents=True, logits=True, value=True, actions=True, seed=1)
+    lg, v, a = run()
+    torch.cuda.synchronize()
+    got = (lg.clone(), v.clone(), a.clone())
+    if ref is None:
+        ref, same = got, "ref"
+    else:
+        same = "bit-identical" if all(torch.equal(x, y) for x, y in zip(got, ref)) else "DIFFERS"
     for _ in range(5):
         run()
     torch.cuda.synchronize()
@@ -34,4 +42,4 @@ for path in libs:
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / reps
-    print("%-50s %.4f ms per %d boards (%.1f G boards/s)" % (path, ms, n, n / ms / 1e6), flush=True)
+    print("%-50s %.4f ms per %d boards (%.1f G boards/s)  %s" % (path, ms, n, n / ms / 1e6, same), flush=True)
