@@ -11,7 +11,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int N = 2048;
 
 template <int ACC>
-__global__ __launch_bounds__(256, 1) void k32(float *out, int n)
+__global__ __launch_bounds__(512, 1) void k32(float *out, int n)
 {
     bf16x8 a, b;
     for (int j = 0; j < 8; j++) { a[j] = (short)(threadIdx.x + j); b[j] = (short)(threadIdx.x * 3 + j); }
@@ -24,7 +24,7 @@ __global__ __launch_bounds__(256, 1) void k32(float *out, int n)
     }
     float s = 0;
     for (int q = 0; q < ACC; q++) for (int r = 0; r < 16; r++) s += c[q][r];
-    out[blockIdx.x * 256 + threadIdx.x] = s;
+    out[blockIdx.x * blockDim.x + threadIdx.x] = s;
 }
 
 template <int ACC>
@@ -41,11 +41,11 @@ __global__ __launch_bounds__(256, 1) void k16(float *out, int n)
     }
     float s = 0;
     for (int q = 0; q < ACC; q++) for (int r = 0; r < 4; r++) s += c[q][r];
-    out[blockIdx.x * 256 + threadIdx.x] = s;
+    out[blockIdx.x * blockDim.x + threadIdx.x] = s;
 }
 
 template <typename K>
-void run(const char *name, K kern, float *out, int cus)
+void run(const char *name, K kern, float *out, int cus, int threads = 256)
 {
     hipEvent_t a, b;
     hipEventCreate(&a);
@@ -53,14 +53,16 @@ void run(const char *name, K kern, float *out, int cus)
     float best = 1e30f;
     for (int r = 0; r < 5; r++) {
         hipEventRecord(a);
-        hipLaunchKernelGGL(kern, dim3(cus), dim3(256), 0, 0, out, N);
+        hipLaunchKernelGGL(kern, dim3(cus), dim3(threads), 0, 0, out, N);
         hipEventRecord(b);
         hipEventSynchronize(b);
         float ms;
         hipEventElapsedTime(&ms, a, b);
         best = ms < best ? ms : best;
     }
-    printf("%-24s %.4f ms  %.1f cycles per MFMA per wave @2.4GHz\n", name, best, best * 1e-3 * 2.4e9 / N);
+    // per SIMD: threads/256 waves each issue N MFMAs
+    printf("%-28s %.4f ms  %.1f cycles per MFMA per SIMD @2.4GHz (%d waves/SIMD)\n", name, best,
+           best * 1e-3 * 2.4e9 / (N * (threads / 256)), threads / 256);
 }
 
 int main()
@@ -68,12 +70,14 @@ int main()
     int cus = 256;
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
     float *out;
-    hipMalloc(&out, cus * 256 * 4);
+    hipMalloc(&out, cus * 512 * 4);
     for (int w = 0; w < 20; w++) hipLaunchKernelGGL(k32<4>, dim3(cus), dim3(256), 0, 0, out, N);
     hipDeviceSynchronize();
     run("32x32x16 1 chain", k32<1>, out, cus);
     run("32x32x16 2 chains", k32<2>, out, cus);
     run("32x32x16 4 chains", k32<4>, out, cus);
+    run("32x32x16 1 chain x2 waves", k32<1>, out, cus, 512);
+    run("32x32x16 2 chains x2 waves", k32<2>, out, cus, 512);
     run("16x16x32 1 chain", k16<1>, out, cus);
     run("16x16x32 2 chains", k16<2>, out, cus);
     run("16x16x32 4 chains", k16<4>, out, cus);
