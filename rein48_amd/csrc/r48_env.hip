@@ -351,8 +351,13 @@ __global__ __launch_bounds__(kBlock) void k_step_n(int8_t *boards, int64_t n, in
         // Progress-ordered issue priority. The SIMD's VALU is the bound and its arbiter prefers
         // the oldest wave: left alone, the 8 waves of a SIMD finish one after another and the
         // last ones run with too few partners to fill the VALU. Dropping a wave's priority as it
-        // passes each quarter of the call lets the laggards catch up, so all 8 stay to the end.
-        const int32_t q1 = n_steps >> 2, q2 = n_steps >> 1, q3 = q1 + q2;
+        // passes 1/8, 3/8 and 3/4 of the call lets the laggards catch up at each boundary, so all
+        // 8 stay to the end (boundaries measured on three boxes: profiles/r02/exp_stepn_priority*).
+#ifndef R48_PRIO_Q   // priority boundaries in eighths of the call (ablation builds: tools/exp_stepn.py A/B)
+#define R48_PRIO_Q 1, 3, 6
+#endif
+        constexpr int kQ[3] = {R48_PRIO_Q};
+        const int32_t q1 = (n_steps * kQ[0]) >> 3, q2 = (n_steps * kQ[1]) >> 3, q3 = (n_steps * kQ[2]) >> 3;
 #ifdef R48_NO_PRIO   // ablation build (tools/exp_stepn.py A/B)
         constexpr bool kPrio = false;
 #else
