@@ -82,7 +82,12 @@ int r48_env_reset_with_draws(r48_env *env, const uint8_t *mask, const uint8_t *r
  *   reward   int32[n] (nullable): 0 (GameClient.py:138), or merged values with R48_MERGE_REWARD.
  *   score    int32[n] (nullable): tile-value sum after the step (main.py:48), before auto-reset.
  * flags: R48_AUTO_RESET | R48_RANDOM_POLICY | R48_MERGE_REWARD. Spawn draws come from
- * Philox4x32-10 keyed by (seed, board id) with the step counter, which then advances. */
+ * Philox4x32-10 keyed by (seed, board id) with the step counter, which then advances (the
+ * rank counts the blanks in the line order of the move: uniform over the blanks like
+ * random_fill_grid's row-major pick; oracle/r48_oracle.c orc_spawn_lines).
+ * Ordering: every call on an env reads and writes its boards and advances its host-side step
+ * counter at launch, so calls on one env must be ordered (one stream, or streams the caller
+ * orders); different envs are independent. */
 int r48_env_step(r48_env *env, int8_t *actions, uint32_t flags, uint8_t *done, uint8_t *changed,
                  int32_t *reward, int32_t *score, void *stream);
 
