@@ -210,4 +210,89 @@ __device__ __forceinline__ void cnn_conv2_heads(const uint4 *w, const float *b, 
     }
 }
 
+// ---- inference form of conv2 + heads (r48_policy.hip): the same products, grouped by weight
+// fragment. conv2's 16 fragments W2(g, u) (g = output half, u = 2kk + s) are each read ONCE per tile
+// and feed the 4 positions' chains of half g (4 independent accumulators), instead of one read per
+// chain: 41 fragment reads per 32-board tile instead of 89, and no MFMA waits on the previous one.
+// Half 0's head MFMAs interleave with half 1's conv2 MFMAs (one per fragment); half 1's heads
+// follow its epilogue. Read order of fwd_grouped_frag: conv1 (9), W2(0, u) (8), [W2(1, u), head
+// (p = u >> 1, g = 0, s = u & 1)] (16), head (p, 1, s) (8).
+constexpr int kFwdGroupedReads = 9 + 8 + 16 + 8;
+__host__ __device__ constexpr int fwd_grouped_frag(int i)
+{
+    if (i < 9)
+        return i;
+    i -= 9;
+    if (i < 8)
+        return kFragW1 + i;                                            // W2(0, u = i)
+    i -= 8;
+    if (i < 16)
+        return (i & 1) ? kFragW1 + kFragW2 + 2 * (2 * (i >> 2)) + ((i >> 1) & 1)   // head (i >> 2, 0, (i >> 1) & 1)
+                       : kFragW1 + 8 + (i >> 1);                                   // W2(1, u = i >> 1)
+    i -= 16;
+    if (i < 8)
+        return kFragW1 + kFragW2 + 2 * (2 * (i >> 1) + 1) + (i & 1);  // head (i >> 1, 1, i & 1)
+    return 0;
+}
+
+// out (rows 0..3 logits, row 4 value, without the head bias) from the 9 conv1 fragments h1; the
+// stream holds fwd_grouped_frag(9), (10) on entry. Every accumulator sums its products in the same
+// order in every caller (k_cnn_forward, k_cnn_rollout), so their results are bit-identical.
+__device__ __forceinline__ void cnn_conv2_heads_grouped(const uint4 *w, const float *b, int lane, int h,
+                                                        const bf16x8 (&h1)[9][2], WStream &ws, f32x16 &out)
+{
+    auto next = [&](int i) { return ws.step(w, fwd_grouped_frag(i + 2 < kFwdGroupedReads ? i + 2 : 0), lane); };
+    f32x16 acc[4];
+    int i = 9;
+    {
+        const f32x16 b2 = load_bias(b + 32, h);
+#pragma unroll
+        for (int u = 0; u < 8; u++, i++) {
+            const bf16x8 wa = next(i);
+            wfence();
+#pragma unroll
+            for (int p = 0; p < 4; p++)
+                acc[p] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, h1[kP2[p][u >> 1]][u & 1], u ? acc[p] : b2, 0, 0,
+                                                                 0);
+            wfence();
+        }
+    }
+    bf16x8 h2[4][2];
+#pragma unroll
+    for (int p = 0; p < 4; p++) {
+        h2[p][0] = acc_to_frag_relu(acc[p], 0);
+        h2[p][1] = acc_to_frag_relu(acc[p], 1);
+    }
+    f32x16 o = f32x16{};
+    {
+        const f32x16 b2 = load_bias(b + 64, h);
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const bf16x8 wa = next(i++);
+            wfence();
+#pragma unroll
+            for (int p = 0; p < 4; p++)
+                acc[p] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, h1[kP2[p][u >> 1]][u & 1], u ? acc[p] : b2, 0, 0,
+                                                                 0);
+            wfence();
+            const bf16x8 wh = next(i++);
+            wfence();
+            o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, h2[u >> 1][u & 1], o, 0, 0, 0);
+            wfence();
+        }
+    }
+#pragma unroll
+    for (int p = 0; p < 4; p++) {
+#pragma unroll
+        for (int s = 0; s < 2; s++) {
+            const bf16x8 hh = acc_to_frag_relu(acc[p], s);
+            const bf16x8 wh = next(i++);
+            wfence();
+            o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, hh, o, 0, 0, 0);
+            wfence();
+        }
+    }
+    out = o;
+}
+
 }  // namespace r48cnn

@@ -37,10 +37,37 @@ using namespace r48cnn;
 
 constexpr int kWaves = 4;
 constexpr int kThreads = 64 * kWaves;
+#ifndef R48_POLICY_OCC
+#define R48_POLICY_OCC 2
+#endif
+constexpr int kOcc = R48_POLICY_OCC;   // workgroups (= waves per SIMD) per CU the forward is built for
 constexpr uint32_t kSampleTag = 0xA3Cu;
 
+// conv1 + conv2 + heads of one 32-board tile: the fragment-grouped conv2 (r48_cnn_common.h,
+// 41 LDS fragment reads per tile); R48_POLICY_GROUPED=0 builds the training kernel's chain order
+// (89 reads) for A/B runs. Shared by k_cnn_forward and k_cnn_rollout, so both sum identically.
+#ifndef R48_POLICY_GROUPED
+#define R48_POLICY_GROUPED 1
+#endif
+__device__ __forceinline__ void policy_logits(const uint4 *w_lds, const float *b_lds, int lane, int h, const bf16x8 &x,
+                                              f32x16 &out)
+{
+    bf16x8 h1[9][2];
+    WStream ws;
+#if R48_POLICY_GROUPED
+    ws.start(w_lds, fwd_grouped_frag(0), fwd_grouped_frag(1), lane);
+    cnn_conv1(w_lds, b_lds, lane, h, x, ws, h1, fwd_grouped_frag(9), fwd_grouped_frag(10));
+    cnn_conv2_heads_grouped(w_lds, b_lds, lane, h, h1, ws, out);
+#else
+    bf16x8 h2[4][2][2];
+    ws.start(w_lds, fwd_frag(0), fwd_frag(1), lane);
+    cnn_conv1(w_lds, b_lds, lane, h, x, ws, h1);
+    cnn_conv2_heads(w_lds, b_lds, lane, h, h1, ws, h2, out);
+#endif
+}
+
 template <int MODE>
-__global__ __launch_bounds__(kThreads, 2) void k_cnn_forward(const int8_t *__restrict__ boards, int64_t n,
+__global__ __launch_bounds__(kThreads, kOcc) void k_cnn_forward(const int8_t *__restrict__ boards, int64_t n,
                                                              const uint4 *__restrict__ wfrag,
                                                              const float *__restrict__ bias,
                                                              float *__restrict__ logits, float *__restrict__ value,
@@ -84,12 +111,8 @@ __global__ __launch_bounds__(kThreads, 2) void k_cnn_forward(const int8_t *__res
         // layer 1 (9 row tiles: one per conv1 output position, rows = 32 filters), then layer 2
         // (conv2: weights shared by the 4 output positions) fused with the heads; weight
         // fragments stream from LDS two MFMAs ahead (r48_cnn_common.h)
-        bf16x8 h1[9][2], h2[4][2][2];
         f32x16 out;
-        WStream ws;
-        ws.start(w_lds, fwd_frag(0), fwd_frag(1), lane);
-        cnn_conv1(w_lds, b_lds, lane, h, x, ws, h1);
-        cnn_conv2_heads(w_lds, b_lds, lane, h, h1, ws, h2, out);
+        policy_logits(w_lds, b_lds, lane, h, x, out);
         if (!live)
             continue;  // padding lanes of the last tile computed on a clamped duplicate board
         if (boards_out)  // the rollout's trajectory snapshot of the input board (no separate copy)
@@ -141,12 +164,8 @@ __device__ __forceinline__ uint32_t policy_action(const uint4 *w_lds, const floa
     }
     bf16x8 x;
     __builtin_memcpy(&x, xp, 16);
-    bf16x8 h1[9][2], h2[4][2][2];
     f32x16 out;
-    WStream ws;
-    ws.start(w_lds, fwd_frag(0), fwd_frag(1), lane);
-    cnn_conv1(w_lds, b_lds, lane, h, x, ws, h1);
-    cnn_conv2_heads(w_lds, b_lds, lane, h, h1, ws, h2, out);
+    policy_logits(w_lds, b_lds, lane, h, x, out);
     uint32_t act = 0;
     if (h == 0) {   // the logits rows; softmax + Philox inverse CDF exactly as k_cnn_forward
         const float z0 = out[0] + b_lds[96], z1 = out[1] + b_lds[97], z2 = out[2] + b_lds[98], z3 = out[3] + b_lds[99];
@@ -274,7 +293,7 @@ int r48_cnn_policy_forward(const int8_t *boards, int64_t n, const void *wfrag, c
     if (hipGetDevice(&dev) == hipSuccess)
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     const int64_t tiles = (n + 31) / 32;
-    const int64_t blocks = std::min<int64_t>((tiles + kWaves - 1) / kWaves, (int64_t)cus * 2);
+    const int64_t blocks = std::min<int64_t>((tiles + kWaves - 1) / kWaves, (int64_t)cus * kOcc);
     // one instantiation per input encoding (no per-cell branch)
     auto kern = mode == R48_FEAT_VALUES ? k_cnn_forward<R48_FEAT_VALUES> : k_cnn_forward<R48_FEAT_EXPONENTS>;
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kThreads), 0, (hipStream_t)stream, boards, n,
