@@ -41,6 +41,10 @@ constexpr int kThreads = 64 * kWaves;
 #define R48_POLICY_OCC 2
 #endif
 constexpr int kOcc = R48_POLICY_OCC;   // workgroups (= waves per SIMD) per CU the forward is built for
+#ifndef R48_ROLLOUT_OCC
+#define R48_ROLLOUT_OCC 2
+#endif
+constexpr int kOccRoll = R48_ROLLOUT_OCC;
 constexpr uint32_t kSampleTag = 0xA3Cu;
 
 // conv1 + conv2 + heads of one 32-board tile: the fragment-grouped conv2 (r48_cnn_common.h,
@@ -66,6 +70,28 @@ __device__ __forceinline__ void policy_logits(const uint4 *w_lds, const float *b
 #endif
 }
 
+// The two waves of a SIMD run identical tile loops and start together, so their MFMA-free phases
+// (conv1 epilogues, the dependent head chain, softmax + draw) can coincide. R48_POLICY_DESYNC: 1 =
+// odd wave slots sleep ~2.5k cycles at entry, 2 (default) = odd wave slots issue at higher
+// priority, so one wave runs ahead and the other fills its gaps (forward 0.0748 -> 0.0713 ms per
+// 2^20 boards, 0.518 -> 0.503 ms per 2^23; rollout unchanged: profiles/r02/a3c/policy_grouped.txt).
+#ifndef R48_POLICY_DESYNC
+#define R48_POLICY_DESYNC 2
+#endif
+__device__ __forceinline__ void desync_waves()
+{
+    if (R48_POLICY_DESYNC) {
+        uint32_t hw;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        if (hw & 1) {
+            if (R48_POLICY_DESYNC == 1)
+                __builtin_amdgcn_s_sleep(40);
+            else
+                __builtin_amdgcn_s_setprio(1);
+        }
+    }
+}
+
 template <int MODE>
 __global__ __launch_bounds__(kThreads, kOcc) void k_cnn_forward(const int8_t *__restrict__ boards, int64_t n,
                                                              const uint4 *__restrict__ wfrag,
@@ -82,6 +108,7 @@ __global__ __launch_bounds__(kThreads, kOcc) void k_cnn_forward(const int8_t *__
     for (int i = threadIdx.x; i < 32 + 64 + 8; i += kThreads)
         b_lds[i] = bias[i];
     __syncthreads();
+    desync_waves();
 
     const int lane = threadIdx.x & 63, h = lane >> 5, col = lane & 31;
     const int64_t n_tiles = (n + 31) / 32;
@@ -182,7 +209,7 @@ __device__ __forceinline__ uint32_t policy_action(const uint4 *w_lds, const floa
 }
 
 template <int MODE, bool REWARD>
-__global__ __launch_bounds__(kThreads, 2) void k_cnn_rollout(int8_t *__restrict__ boards, int64_t n, int32_t T,
+__global__ __launch_bounds__(kThreads, kOccRoll) void k_cnn_rollout(int8_t *__restrict__ boards, int64_t n, int32_t T,
                                                              const uint4 *__restrict__ wfrag,
                                                              const float *__restrict__ bias,
                                                              int8_t *__restrict__ traj, int8_t *__restrict__ actions,
@@ -198,6 +225,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_cnn_rollout(int8_t *__restrict_
     for (int i = threadIdx.x; i < 32 + 64 + 8; i += kThreads)
         b_lds[i] = bias[i];
     __syncthreads();
+    desync_waves();
 
     const int lane = threadIdx.x & 63, h = lane >> 5, col = lane & 31;
     const int64_t n_pairs = (n + 63) / 64;
@@ -322,7 +350,7 @@ int r48_cnn_rollout(int8_t *boards, int64_t n, int32_t n_steps, const void *wfra
     if (hipGetDevice(&dev) == hipSuccess)
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     const int64_t pairs = (n + 63) / 64;
-    const int64_t blocks = std::min<int64_t>((pairs + kWaves - 1) / kWaves, (int64_t)cus * 2);
+    const int64_t blocks = std::min<int64_t>((pairs + kWaves - 1) / kWaves, (int64_t)cus * kOccRoll);
     const bool rw = flags & R48_MERGE_REWARD;
     auto kern = mode == R48_FEAT_VALUES ? (rw ? k_cnn_rollout<R48_FEAT_VALUES, true> : k_cnn_rollout<R48_FEAT_VALUES, false>)
                                         : (rw ? k_cnn_rollout<R48_FEAT_EXPONENTS, true>

@@ -32,7 +32,11 @@ for path in libs:
     ws = torch.empty(_lib.load().r48_cnn_train_workspace_floats(), dtype=torch.float32, device=dev)
     run = lambda: cnn_train_grad(net, boards, actions, targets, wn, None, None, beta=0.01, exponents=True,
                                  n_boards=n, packed=packed, workspace=ws)
-    for _ in range(3):
+    out = run()
+    torch.cuda.synchronize()
+    grads = torch.cat([t.detach().float().reshape(-1) for t in out[0]])
+    digest = int((grads.view(torch.int32).long() * 2654435761).sum()) & 0xFFFFFFFF   # bit-level fingerprint
+    for _ in range(2):
         run()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -43,5 +47,5 @@ for path in libs:
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / reps
-    print("%-40s %8.2f ms per %d rows  (%.2f ms per 1e8)" % (os.path.basename(path), ms, rows, ms * 1e8 / rows),
-          flush=True)
+    print("%-40s %8.2f ms per %d rows  (%.2f ms per 1e8)  grad digest %08x" % (os.path.basename(path), ms, rows,
+                                                                               ms * 1e8 / rows, digest), flush=True)

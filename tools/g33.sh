@@ -1,0 +1,7 @@
+set -o pipefail
+O=gpurun_out/g33; mkdir -p $O
+timeout -k 10 200 python tools/exp_train_ablate.py 16777216 build/lib_train_old.so rein48_amd/lib/librein48.so build/lib_train_old.so rein48_amd/lib/librein48.so > $O/train.txt 2>&1 \
+&& timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/pytest_gpu.txt 2>&1 \
+&& timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke(); print('smoke OK')" > $O/smoke.txt 2>&1 \
+&& timeout -k 10 300 python bench.py --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err
+echo rc=$?
