@@ -178,9 +178,9 @@ __global__ __launch_bounds__(kThreads, kOcc) void k_cnn_forward(const int8_t *__
 // whole board, one more returns the halves -- every lane does useful env work. Per board the first
 // step that ends done gives the segment length (a3c.py:201). Results are bit-identical to
 // T x (r48_cnn_policy_forward + r48_env_step) (tests/test_a3c_gpu.py).
+// logits rows of one 32-board tile (lane half 0: registers 0..3, without the head bias)
 template <int MODE>
-__device__ __forceinline__ uint32_t policy_action(const uint4 *w_lds, const float *b_lds, int lane, int h, uint2 raw,
-                                                  uint64_t gid, uint32_t ctr, uint32_t pk0, uint32_t pk1)
+__device__ __forceinline__ f32x16 policy_out(const uint4 *w_lds, const float *b_lds, int lane, int h, uint2 raw)
 {
     uint32_t xp[4];
 #pragma unroll
@@ -193,19 +193,21 @@ __device__ __forceinline__ uint32_t policy_action(const uint4 *w_lds, const floa
     __builtin_memcpy(&x, xp, 16);
     f32x16 out;
     policy_logits(w_lds, b_lds, lane, h, x, out);
-    uint32_t act = 0;
-    if (h == 0) {   // the logits rows; softmax + Philox inverse CDF exactly as k_cnn_forward
-        const float z0 = out[0] + b_lds[96], z1 = out[1] + b_lds[97], z2 = out[2] + b_lds[98], z3 = out[3] + b_lds[99];
-        const float m = fmaxf(fmaxf(z0, z1), fmaxf(z2, z3));
-        const float e0 = __expf(z0 - m), e1 = __expf(z1 - m), e2 = __expf(z2 - m), e3 = __expf(z3 - m);
-        const float inv = 1.0f / (e0 + e1 + e2 + e3);
-        const float p0 = e0 * inv, c1 = p0 + e1 * inv, c2 = c1 + e2 * inv;
-        uint32_t w[4] = {(uint32_t)gid, (uint32_t)(gid >> 32), ctr, kSampleTag};
-        r48::philox4x32_10(w, pk0, pk1);
-        const float u = (float)(w[0] >> 8) * (1.0f / 16777216.0f);
-        act = (p0 > u) ? 0u : (c1 > u) ? 1u : (c2 > u) ? 2u : 3u;
-    }
-    return act;
+    return out;
+}
+
+// softmax + Philox inverse CDF of one board's logits z, exactly as k_cnn_forward's epilogue
+__device__ __forceinline__ uint32_t sample_action(const float (&z)[4], uint64_t gid, uint32_t ctr, uint32_t pk0,
+                                                  uint32_t pk1)
+{
+    const float m = fmaxf(fmaxf(z[0], z[1]), fmaxf(z[2], z[3]));
+    const float e0 = __expf(z[0] - m), e1 = __expf(z[1] - m), e2 = __expf(z[2] - m), e3 = __expf(z[3] - m);
+    const float inv = 1.0f / (e0 + e1 + e2 + e3);
+    const float p0 = e0 * inv, c1 = p0 + e1 * inv, c2 = c1 + e2 * inv;
+    uint32_t w[4] = {(uint32_t)gid, (uint32_t)(gid >> 32), ctr, kSampleTag};
+    r48::philox4x32_10(w, pk0, pk1);
+    const float u = (float)(w[0] >> 8) * (1.0f / 16777216.0f);
+    return (p0 > u) ? 0u : (c1 > u) ? 1u : (c2 > u) ? 2u : 3u;
 }
 
 template <int MODE, bool REWARD>
@@ -248,11 +250,17 @@ __global__ __launch_bounds__(kThreads, kOccRoll) void k_cnn_rollout(int8_t *__re
                 *reinterpret_cast<uint2 *>(traj + 16 * (row0 + bA) + 8 * h) = rawA;
             if (liveB)
                 *reinterpret_cast<uint2 *>(traj + 16 * (row0 + bB) + 8 * h) = rawB;
-            const uint32_t aA = policy_action<MODE>(w_lds, b_lds, lane, h, rawA, gA, ctr0 + (uint32_t)t, pk0, pk1);
-            const uint32_t aB = policy_action<MODE>(w_lds, b_lds, lane, h, rawB, gB, ctr0 + (uint32_t)t, pk0, pk1);
-            // half 0 keeps its A action; half 1 takes B's action from lane col (half 0)
-            const uint32_t aBall = (uint32_t)__shfl((int)aB, col);
-            const uint32_t act = h == 0 ? aA : aBall;
+            const f32x16 oA = policy_out<MODE>(w_lds, b_lds, lane, h, rawA);
+            const f32x16 oB = policy_out<MODE>(w_lds, b_lds, lane, h, rawB);
+            // one draw pass for both tiles: half 0 samples A's board col, half 1 B's (whose logits
+            // sit in half 0 of oB) -- the lane's action is the one its env step below needs
+            float z[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const float zb = __shfl_xor(oB[k], 32);
+                z[k] = (h == 0 ? oA[k] : zb) + b_lds[96 + k];
+            }
+            const uint32_t act = sample_action(z, gE, ctr0 + (uint32_t)t, pk0, pk1);
             // assemble the env board: half 0 gets A's rows 2-3 from its partner, half 1 B's rows 0-1
             const uint2 send = h == 0 ? rawB : rawA;
             const uint2 recv = make_uint2((uint32_t)__shfl_xor((int)send.x, 32), (uint32_t)__shfl_xor((int)send.y, 32));
