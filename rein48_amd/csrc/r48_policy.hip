@@ -172,12 +172,13 @@ __global__ __launch_bounds__(kThreads, kOcc) void k_cnn_forward(const int8_t *__
 // the trajectory rows (pre-step board, action, done, merge reward) -- no per-step launches and no
 // board round trip through HBM. A wave owns a PAIR of 32-board tiles (A, B). Lane (col, h) holds
 // bytes 8h..8h+7 (rows 2h, 2h+1) of board col of both tiles. Per step: the policy of
-// k_cnn_forward on A, then on B (boards on the MFMA columns, action draw in lane half 0), then ONE
-// env step pass (Game.step, GameClient.py:40-51, r48_board.h, the k_step draw contract) in which
+// k_cnn_forward on A, then on B (boards on the MFMA columns), ONE softmax + draw pass for both
+// (lane half 0 samples A's board, half 1 B's), then ONE env step pass (Game.step, GameClient.py:40-51, r48_board.h, the k_step draw contract) in which
 // lane half 0 steps tile A's board and lane half 1 tile B's: one cross-half shuffle assembles the
 // whole board, one more returns the halves -- every lane does useful env work. Per board the first
 // step that ends done gives the segment length (a3c.py:201). Results are bit-identical to
 // T x (r48_cnn_policy_forward + r48_env_step) (tests/test_a3c_gpu.py).
+
 // logits rows of one 32-board tile (lane half 0: registers 0..3, without the head bias)
 template <int MODE>
 __device__ __forceinline__ f32x16 policy_out(const uint4 *w_lds, const float *b_lds, int lane, int h, uint2 raw)
