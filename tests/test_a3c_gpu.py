@@ -152,8 +152,9 @@ def test_trainer_textbook_modes_run(net, bf16):
     assert tr.flat.grad.abs().sum() > 0
 
 
+@pytest.mark.parametrize("n", [100_003, 1, 31, 33, 64, 65])
 @pytest.mark.parametrize("exponents", [False, True])
-def test_fused_cnn_policy_matches_torch(exponents):
+def test_fused_cnn_policy_matches_torch(exponents, n):
     """r48_cnn_policy_forward (bf16 MFMA, register-chained layers) vs the PyTorch CNN.
     Error metric: max |got - ref| / (|ref| + mean|ref|). Against fp32 the kernel's error must be
     within 1.5x of PyTorch's own bf16 forward's error (same rounding points: bf16 inputs, weights,
@@ -168,8 +169,7 @@ def test_fused_cnn_policy_matches_torch(exponents):
     with torch.no_grad():                       # non-trivial biases so every bias path is checked
         for m in (net.conv1, net.conv2, net.heads):
             m.bias.uniform_(-0.5, 0.5)
-    rng = np.random.default_rng(4)
-    n = 100_003                                  # a partial last tile
+    rng = np.random.default_rng(4)               # n: partial last tiles, single board, tile edges
     b = rng.integers(1, 12, size=(n, 16)).astype(np.int8)
     b[rng.random((n, 16)) < 0.4] = 0
     boards = torch.from_numpy(b).to(DEV)
@@ -185,8 +185,10 @@ def test_fused_cnn_policy_matches_torch(exponents):
         net.dtype = torch.bfloat16
         ref16 = net(x)
     e_kernel, e_torch_bf16 = worst((lg, v), ref32), worst(ref16, ref32)
-    # the fused kernel is as accurate as PyTorch's own bf16 path (both vs fp32), and close to it
-    assert e_kernel <= 1.5 * e_torch_bf16 + 1e-3, (e_kernel, e_torch_bf16)
+    # the fused kernel is as accurate as PyTorch's own bf16 path (both vs fp32; a statistic that
+    # needs many boards), and close to it
+    if n >= 10_000:
+        assert e_kernel <= 1.5 * e_torch_bf16 + 1e-3, (e_kernel, e_torch_bf16)
     assert e_kernel <= (4e-2 if exponents else 8e-2), e_kernel
     assert worst((lg, v), ref16) <= 2e-2
     _, _, act = cnn_forward(boards, wfrag, bias, exponents=exponents, logits=False, value=False, actions=True,
@@ -304,8 +306,9 @@ def test_fused_rollout_trajectory_replays_through_the_env():
         assert torch.equal(rew.float(), tr.rewards[t]), t
 
 
+@pytest.mark.parametrize("n_boards", [5003, 1, 65])
 @pytest.mark.parametrize("mode", ["textbook", "reference"])
-def test_rollout_megakernel_equals_per_step_rollout(mode):
+def test_rollout_megakernel_equals_per_step_rollout(mode, n_boards):
     """r48_cnn_rollout (all steps of every board in one launch, boards in registers) == the
     per-step rollout (r48_cnn_policy_forward + r48_env_step per step), bit for bit: trajectory
     boards, actions, done, rewards, final boards and the env / sampling counters; a ragged board
@@ -313,7 +316,7 @@ def test_rollout_megakernel_equals_per_step_rollout(mode):
     from rein48_amd.a3c import A3CConfig, A3CTrainer
     out = []
     for mega in (True, False):
-        cfg = A3CConfig(n_boards=5003, max_steps=37, mode=mode, net="cnn", bf16=True, features="exponents",
+        cfg = A3CConfig(n_boards=n_boards, max_steps=37, mode=mode, net="cnn", bf16=True, features="exponents",
                         seed=77, fused_rollout=mega)                # 5003 = 78 tile pairs + a partial one
         tr = A3CTrainer(cfg, device=DEV)
         tr.rollout()
