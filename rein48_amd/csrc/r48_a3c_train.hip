@@ -73,6 +73,16 @@ constexpr float kEntropyEps = 1e-5f;                          // a3c.py:114
 #define R48_TRAIN_SKIP 0
 #endif
 constexpr int kSkip = R48_TRAIN_SKIP;
+// ablation knob (timing only, wrong gradients): R48_TRAIN_NOBAR drops the per-tile workgroup
+// barriers around the shared-slot contractions
+#ifndef R48_TRAIN_NOBAR
+#define R48_TRAIN_NOBAR 0
+#endif
+__device__ __forceinline__ void tile_barrier()
+{
+    if (!R48_TRAIN_NOBAR)
+        __syncthreads();
+}
 
 // dh1's (conv2 output p, input block kk) pairs grouped by the conv1 position R = kP2[p][kk]
 __device__ constexpr int kDh1P[16] = {0, 0, 1, 1, 0, 2, 0, 1, 2, 3, 1, 3, 2, 2, 3, 3};
@@ -413,7 +423,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
         // ---------------- phase A: dWh[o][f] (f in the wave's 64 features) = sum over the 4 x 32 rows
         // of the workgroup of dout[o] h2[f]; 16x16x32 with A = h2^T (features x rows), B = dout
         if (!(kSkip & 1)) {
-            __syncthreads();
+            tile_barrier();
             // the 4 dout operands up front, the h2^T operands one (slot, ft) step ahead
             const int o = lane & 15;
             bf16x8 bd[kWaves];
@@ -435,7 +445,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
                 wfence();
                 A = An;
             }
-            __syncthreads();
+            tile_barrier();
         }
         // ---------------- phase B: dW2[:, 32 wave ..] = sum_p dh2[p] h1[kP2[p][wave]]^T, in two
         // halves of two patches each (the slot holds one half); dh1 is formed between the halves
@@ -480,7 +490,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
                 }
             }
             if (!(kSkip & 2)) {
-                __syncthreads();
+                tile_barrier();
                 // 16 K-steps (slot sl, patch pl of the half, 16-row block ks), software-pipelined:
                 // the operands of step k + 1 are read before the MFMAs of step k issue
                 // (dw2[0] holds output half g_mine, dw2[1] the other one)
@@ -506,7 +516,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
                     for (int k = 0; k < 3; k++)
                         cur[k] = nxt[k];
                 }
-                __syncthreads();
+                tile_barrier();
             }
         }
         // ---------------- phase C: dW1[co][t] (+ bias t = 4) = sum over the own 32 rows of
