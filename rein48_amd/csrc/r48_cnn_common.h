@@ -95,6 +95,27 @@ __device__ __forceinline__ uint32_t cell_bf16(uint32_t e, int mode)
     return __float_as_uint((float)e) >> 16;                    // small integers are exact
 }
 
+// copy N16 16-byte words global -> LDS with every load of a thread in flight at once (the plain
+// loop load / wait / store pays one global latency per iteration, ~11 for the 41 KB policy image)
+template <int N16, int THREADS>
+__device__ __forceinline__ void stage_lds(uint4 *dst, const uint4 *__restrict__ src)
+{
+    constexpr int kFull = N16 / THREADS, kTail = N16 - kFull * THREADS;
+    const int t = (int)threadIdx.x;
+    uint4 v[kFull];
+#pragma unroll
+    for (int j = 0; j < kFull; j++)
+        v[j] = src[t + j * THREADS];
+    uint4 tail = {};
+    if (kTail && t < kTail)
+        tail = src[t + kFull * THREADS];
+#pragma unroll
+    for (int j = 0; j < kFull; j++)
+        dst[t + j * THREADS] = v[j];
+    if (kTail && t < kTail)
+        dst[t + kFull * THREADS] = tail;
+}
+
 __device__ __forceinline__ bf16x8 frag_at(const uint4 *w, int frag, int lane)
 {
     const uint4 v = w[frag * 64 + lane];

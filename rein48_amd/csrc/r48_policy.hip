@@ -46,6 +46,9 @@ constexpr int kOcc = R48_POLICY_OCC;   // workgroups (= waves per SIMD) per CU t
 #endif
 constexpr int kOccRoll = R48_ROLLOUT_OCC;
 constexpr uint32_t kSampleTag = 0xA3Cu;
+#ifndef R48_STAGE_PLAIN
+#define R48_STAGE_PLAIN 0   // 1: the weight image staged by a plain load / store loop (A/B builds)
+#endif
 
 // conv1 + conv2 + heads of one 32-board tile: the fragment-grouped conv2 (r48_cnn_common.h,
 // 41 LDS fragment reads per tile); R48_POLICY_GROUPED=0 builds the training kernel's chain order
@@ -103,8 +106,12 @@ __global__ __launch_bounds__(kThreads, kOcc) void k_cnn_forward(const int8_t *__
 {
     __shared__ uint4 w_lds[kFrags * 64];
     __shared__ __attribute__((aligned(16))) float b_lds[32 + 64 + 8];   // float4 reads (load_bias)
+#if R48_STAGE_PLAIN
     for (int i = threadIdx.x; i < kFrags * 64; i += kThreads)
         w_lds[i] = wfrag[i];
+#else
+    stage_lds<kFrags * 64, kThreads>(w_lds, wfrag);
+#endif
     for (int i = threadIdx.x; i < 32 + 64 + 8; i += kThreads)
         b_lds[i] = bias[i];
     __syncthreads();
@@ -223,8 +230,12 @@ __global__ __launch_bounds__(kThreads, kOccRoll) void k_cnn_rollout(int8_t *__re
 {
     __shared__ uint4 w_lds[kFrags * 64];
     __shared__ __attribute__((aligned(16))) float b_lds[32 + 64 + 8];
+#if R48_STAGE_PLAIN
     for (int i = threadIdx.x; i < kFrags * 64; i += kThreads)
         w_lds[i] = wfrag[i];
+#else
+    stage_lds<kFrags * 64, kThreads>(w_lds, wfrag);
+#endif
     for (int i = threadIdx.x; i < 32 + 64 + 8; i += kThreads)
         b_lds[i] = bias[i];
     __syncthreads();
