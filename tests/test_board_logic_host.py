@@ -20,3 +20,16 @@ def test_board_logic_matches_oracle(tmp_path):
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "OK (0 failures)" in r.stdout
+
+
+def test_cnn_fragment_schedules_compile_time_checks():
+    """r48_cnn_common.h's weight-fragment read schedules (grouped inference order, chain order)
+    checked by static_asserts in tests/native/cnn_schedule_test.cpp (host-only syntax pass)."""
+    hipcc = "/opt/rocm/bin/hipcc"
+    if not os.path.exists(hipcc):
+        import pytest
+        pytest.skip("hipcc not available")
+    r = subprocess.run([hipcc, "-std=c++17", "--offload-host-only", "-fsyntax-only",
+                        os.path.join(ROOT, "tests", "native", "cnn_schedule_test.cpp")],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
