@@ -203,6 +203,27 @@ def test_fused_cnn_policy_matches_torch(exponents, n):
     assert torch.equal(a_row, want) and torch.equal(snap, boards)
 
 
+def test_fused_cnn_policy_is_independent_of_tiling():
+    """Each board's logits, value and draw depend only on the board and its global id: the same
+    boards forwarded as a whole (many tile pairs per wave) and as offset slices (other tile,
+    wave and workgroup positions, gid0 shifted to match) agree bit for bit."""
+    from rein48_amd.a3c.fused import cnn_forward, pack_cnn
+    from rein48_amd.a3c.nets import ActorCriticCNN
+    torch.manual_seed(5)
+    net = ActorCriticCNN().to(DEV)
+    rng = np.random.default_rng(6)
+    n = 300_007
+    b = rng.integers(0, 12, size=(n, 16)).astype(np.int8)
+    boards = torch.from_numpy(b).to(DEV)
+    wfrag, bias = pack_cnn(net)
+    full = cnn_forward(boards, wfrag, bias, exponents=True, actions=True, seed=11, ctr=3, gid0=100)
+    for lo, hi in ((0, 1), (5, 70), (31, 1000), (4097, 300_007), (123_456, 123_457)):
+        part = cnn_forward(boards[lo:hi].contiguous(), wfrag, bias, exponents=True, actions=True, seed=11, ctr=3,
+                           gid0=100 + lo)
+        for f, q in zip(full, part):
+            assert torch.equal(f[lo:hi], q), (lo, hi)
+
+
 @pytest.mark.parametrize("mode", ["textbook", "reference"])
 def test_fused_cnn_update_gradients_match_torch(mode):
     """r48_cnn_train_grad (forward + loss + backward + weight gradients in one MFMA pass, rows
