@@ -35,12 +35,6 @@ asm: $(SRC) $(DEPS)
 	$(HIPCC) $(HIPFLAGS) --cuda-device-only -c -o /dev/null -Rpass-analysis=kernel-resource-usage rein48_amd/csrc/r48_policy.hip 2> build/resource_usage_policy.txt
 	$(HIPCC) $(HIPFLAGS) --cuda-device-only -c -o /dev/null -Rpass-analysis=kernel-resource-usage rein48_amd/csrc/r48_env.hip 2> build/resource_usage.txt
 
-# k_cnn_train phase ablations for tools/exp_train_ablate.py (timing only; wrong gradients)
-ABLATE := 1 2 4 6 7
-ablate: $(OBJ)
-	@mkdir -p build/ablate_train
-	for m in $(ABLATE); do $(HIPCC) $(HIPFLAGS) $(FLAGS_r48_a3c_train) -DR48_TRAIN_SKIP=$$m -c -o build/ablate_train/train_skip$$m.o rein48_amd/csrc/r48_a3c_train.hip && $(HIPCC) $(HIPFLAGS) -shared -o build/ablate_train/librein48_skip$$m.so $(filter-out $(OBJDIR)/r48_a3c_train.o,$(OBJ)) build/ablate_train/train_skip$$m.o || exit 1; done
-
 oracle:
 	$(MAKE) -s -C oracle
 
@@ -48,4 +42,4 @@ clean:
 	rm -rf $(LIBDIR) build
 	$(MAKE) -s -C oracle clean
 
-.PHONY: all asm ablate oracle clean
+.PHONY: all asm oracle clean

@@ -11,16 +11,23 @@ a call covers the whole K unless --chunk splits it), bit-identical to K single-s
 
 Multi-GPU: one process per GPU (torchrun; `--gpus N` without WORLD_SIZE launches torchrun itself
 as a child process before touching the GPU), rank r owns boards [r*N, (r+1)*N) (Philox keyed by
-global board id); no data-path collective. Timing: barrier + sync on both sides of exactly K
-steps, max over ranks; value = all boards x K / that time.
+global board id); no data-path collective. Timing: synchronize + barrier + synchronize before
+exactly K steps and synchronize after them on every rank; the job's window runs from the earliest
+rank's start to the latest rank's end on the node's shared monotonic clock (both all-reduced), so
+barrier skew cannot shorten it; value = all boards x K / that window.
 
 Extra objects on the JSON line:
   roofline      k_step_n is VALU-issue bound (boards in VGPRs, no memory traffic inside its step
-                loop): achieved = VALU issue cycles per board-step (the shipped loop's instruction
-                mix x measured per-instruction issue costs, committed in profiles/r02/
-                pmc_k_step_n.json with its SQ_INSTS_VALU cross-check) x board-steps / the dispatch
-                time from HIP events in the timed region; peak = one issue cycle per SIMD per clock
-                (1024 SIMDs x 2.4 GHz). `valu_instr_rate` gives the plain instruction-rate fraction.
+                loop): achieved = MODELLED VALU issue cycles per board-step (the shipped loop's
+                static instruction mix x measured per-instruction issue costs, committed in
+                profiles/<round>/pmc_k_step_n.json together with the hash of the kernel sources it
+                was made from) x board-steps / the SAME wall time as `value` -> frac; frac_device
+                uses the HIP-event dispatch time of the same region instead; peak = one issue cycle
+                per SIMD per clock (1024 SIMDs x 2.4 GHz). `hbm_def` prices the same rate at
+                SURVEY.md 8(d)'s 34 B per board-step against 8 TB/s (k_step_n makes no per-step HBM
+                round trip, so that fraction may exceed 1). If the committed profile's source hash
+                differs from the tree's, the profile-derived fields are null and `profile_stale`
+                says so. `valu_instr_rate` gives the plain instruction-rate fraction.
                 `hbm` holds the single-step kernel k_step (boards through HBM every step, 34
                 algorithmic bytes per board-step) at 2^20 boards (Infinity-Cache resident) and at
                 2^26 (past the 256 MiB cache: the HBM point) against the 8 TB/s spec, with PMC
@@ -57,7 +64,19 @@ HBM_MEASURED_GBS = 6290.0  # float4 copy measured on MI355X (same guide)
 SIMDS, CLOCK_GHZ = 1024, 2.4            # 256 CUs x 4 SIMDs; max clock (same guide)
 VALU_PEAK_G = SIMDS * CLOCK_GHZ / 2.0   # G wave-instructions/s: one full-rate wave64 VALU instr per 2 cycles
 VALU_ISSUE_PEAK_G = SIMDS * CLOCK_GHZ   # G VALU issue-cycles/s
-PROFILE_DIR = os.path.join(ROOT, "profiles", "r02")
+PROFILE_ROUND = "r03"
+PROFILE_DIR = os.path.join(ROOT, "profiles", PROFILE_ROUND)
+ENV_SOURCES = ("rein48_amd/csrc/r48_env.hip", "rein48_amd/csrc/r48_board.h")
+
+
+def env_source_sha16():
+    """Hash of the env kernel's sources: a committed profile describes the build it was made from."""
+    import hashlib
+    h = hashlib.sha256()
+    for p in ENV_SOURCES:
+        with open(os.path.join(ROOT, p), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
 
 
 def shard(rank, boards_per_gpu):
@@ -113,12 +132,18 @@ SETTLE_S = 0.3   # minimum untimed stepping before a timed region: GPU clocks ra
 SYNC_POLL = False  # --sync: poll the region's last HIP event before the closing synchronize
 
 
+def _now():
+    """Node-wide monotonic clock (CLOCK_MONOTONIC is shared by every process of one host)."""
+    return time.clock_gettime_ns(time.CLOCK_MONOTONIC) * 1e-9
+
+
 def timed_steps(env, plan, W, chunk, world, dev):
     """W untimed warm-up steps through the same path (in calls of the timed chunk size) --
     continued, still untimed, until at least SETTLE_S of stepping has run -- then exactly sum(plan)
-    steps bracketed by barrier + synchronize (opening: synchronize, barrier, synchronize, t0;
-    closing: synchronize, t1, barrier). -> (slowest rank's wall seconds t1 - t0, max over ranks;
-    device ms of the timed calls from HIP events on the launch stream, one entry per call)."""
+    steps. Opening: synchronize, barrier, synchronize, t0 (per rank); closing: synchronize, t1.
+    -> (window seconds = max over ranks of t1 - min over ranks of t0 on the node's monotonic clock;
+    device ms of the timed calls from HIP events on the launch stream, one entry per call;
+    start skew = max - min over ranks of t0)."""
     t_w = time.perf_counter()
     for c in chunks(W, chunk) if W else []:
         env.step_n(c, auto_reset=True)
@@ -135,7 +160,7 @@ def timed_steps(env, plan, W, chunk, world, dev):
     if world > 1:
         dist.barrier()
         torch.cuda.synchronize(dev)          # the barrier's own device work done before t0
-    t0 = time.perf_counter()
+    t0 = _now()
     for (a, b), c in zip(ev, plan):
         a.record(s)
         env.step_n(c, auto_reset=True)
@@ -147,13 +172,14 @@ def timed_steps(env, plan, W, chunk, world, dev):
         while not last.query():
             pass
     torch.cuda.synchronize(dev)
-    t1 = time.perf_counter()
-    # each rank's K steps end at its own synchronize; the job's time is the slowest rank's
-    # (max over ranks below), so the closing barrier's collective latency (tens of us with RCCL,
-    # against a ~100 us region at --steps 20) is not counted as stepping time
+    t1 = _now()
+    skew = 0.0
     if world > 1:
-        dist.barrier()
-    return max_over_ranks(t1 - t0, dev, world), [a.elapsed_time(b) for a, b in ev]
+        # one window for the node: from the earliest rank's start to the latest rank's end
+        t = torch.tensor([-t0, t1, t0, -t0], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        t0, t1, skew = -float(t[0]), float(t[1]), float(t[2]) + float(t[3])
+    return t1 - t0, [a.elapsed_time(b) for a, b in ev], skew
 
 
 def single_step_hbm(dev, seed, n, launches):
@@ -195,36 +221,57 @@ def single_step_hbm(dev, seed, n, launches):
     return out
 
 
-def roofline_step_n(n, dev_ms, steps):
+def roofline_step_n(n, wall_s, dev_ms, steps):
     """VALU roofline of k_step_n (boards stay in VGPRs for all steps of a call: no memory traffic
-    inside the step loop). Work = VALU issue cycles: the shipped loop's static instruction mix x
-    each instruction's measured issue cost (modelled_cycles_per_board_step, profiles/r02/
-    pmc_k_step_n.json, made by tools/make_r02_profiles.py from build/r48_env.s and
-    profiles/r02/instr_rate.txt); peak = one issue cycle per SIMD per clock (1024 SIMDs x 2.4 GHz).
-    Also reported: SQ_INSTS_VALU per board-step (PMC) against the full-rate instruction peak."""
+    inside the step loop). Work = MODELLED VALU issue cycles: the shipped loop's static instruction
+    mix x each instruction's measured issue cost (modelled_cycles_per_board_step, profiles/<round>/
+    pmc_k_step_n.json, made by tools/make_profiles.py from build/r48_env.s and the instruction-rate
+    table); peak = one issue cycle per SIMD per clock (1024 SIMDs x 2.4 GHz). frac uses the same
+    wall time as `value`, frac_device the HIP-event dispatch time of the region, frac_trace the
+    committed kernel trace of the driver's command. hbm_def: the same board-step rate at 34 B per
+    board-step against 8 TB/s. Profile-derived fields are null when the profile
+    was made from other kernel sources than the tree's (profile_stale)."""
     prof = _load_profile("pmc_k_step_n.json")
-    if prof is None:
-        raise SystemExit("profiles/r02/pmc_k_step_n.json missing (tools/prof_r02.sh + tools/make_r02_profiles.py)")
+    trace = _load_profile("roofline_from_trace.json")
+    sha = env_source_sha16()
+    stale = prof is None or prof.get("source_sha16") != sha
+    bsteps = n * steps
+    rate_wall = bsteps / wall_s
+    rate_dev = bsteps / (dev_ms * 1e-3)
+    hbm = {"bytes_per_board_step": ALGO_BYTES, "achieved": rate_wall * ALGO_BYTES / 1e9, "peak": HBM_PEAK_GBS,
+           "unit": "GB/s", "frac": rate_wall * ALGO_BYTES / 1e9 / HBM_PEAK_GBS,
+           "note": "SURVEY.md 8(d)'s 34 B per board-step priced at the wall rate of `value`; k_step_n reads and "
+                   "writes each board once per call (no per-step HBM round trip), so this may exceed 1"}
+    out = {"bound": "valu", "unit": "G VALU issue-cycles/s", "peak": VALU_ISSUE_PEAK_G,
+           "achieved": None, "frac": None, "frac_device": None, "achieved_is": "modelled",
+           "hbm_def": hbm, "board_steps_timed": bsteps, "wall_ms_timed": wall_s * 1e3, "device_ms_timed": dev_ms,
+           "kernel": "k_step_n<RANDOM=1,AUTO_RESET=1,REWARD=0> (board pair per lane in VGPRs for all steps of the "
+                     "call, line-form orientation tracking)",
+           "source_sha16": sha, "profile": "profiles/%s/pmc_k_step_n.json" % PROFILE_ROUND,
+           "profile_stale": stale, "traffic": None}
+    if stale:
+        return out
     cyc, per = prof["modelled_cycles_per_board_step"], prof["valu_wave_instr_per_board_step"]
-    bsteps_per_s = n * steps / (dev_ms * 1e-3)
-    achieved = cyc * bsteps_per_s / 1e9
-    instr = per * bsteps_per_s / 1e9
-    return {"bound": "valu", "achieved": achieved, "peak": VALU_ISSUE_PEAK_G, "unit": "G VALU issue-cycles/s",
-            "frac": achieved / VALU_ISSUE_PEAK_G, "traffic": prof["hbm_bytes_per_dispatch"] * n / prof["boards"],
-            "traffic_unit": "bytes per launch (HBM/fabric; the boards are read and written once per call)",
-            "traffic_source": "profiles/r02/pmc_k_step_n.json: rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE passes of the "
-                              "same 2^20-board K=20 dispatch (committed profile, not measured in this run)",
-            "kernel": "k_step_n<RANDOM=1,AUTO_RESET=1,REWARD=0> (board pair per lane in VGPRs for all steps of the call, "
-                      "one Philox4x32-10 call per pair-step, line-form orientation tracking)",
-            "issue_cycles_per_board_step": cyc,
-            "issue_cycles_source": "build/r48_env.s hot loop (tools/isa_hist.py) x profiles/r02/instr_rate.txt",
-            "valu_wave_instr_per_board_step": per,
-            "valu_instr_source": "profiles/r02/pmc_k_step_n.json (SQ_INSTS_VALU per dispatch / board-steps)",
-            "valu_instr_rate": {"achieved": instr, "peak": VALU_PEAK_G, "unit": "G VALU wave-instr/s",
-                                "frac": instr / VALU_PEAK_G,
-                                "note": "peak = one wave64 instruction per 2 cycles per SIMD; half-rate instructions "
-                                        "(v_perm, v_mad_u64_u32, v_bcnt, v_mul, v_lshlrev...) take ~4.3 cycles"},
-            "board_steps_timed": n * steps, "device_ms_timed": dev_ms}
+    out.update({
+        "achieved": cyc * rate_wall / 1e9, "frac": cyc * rate_wall / 1e9 / VALU_ISSUE_PEAK_G,
+        "frac_device": cyc * rate_dev / 1e9 / VALU_ISSUE_PEAK_G,
+        "traffic": prof["hbm_bytes_per_dispatch"] * n / prof["boards"],
+        "traffic_unit": "bytes per launch (HBM/fabric; the boards are read and written once per call)",
+        "traffic_source": "profiles/%s/pmc_k_step_n.json: rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE passes of a 2^20-board "
+                          "K=%d dispatch (committed profile; scaled to this run's boards)"
+                          % (PROFILE_ROUND, prof.get("steps_per_dispatch", 20)),
+        "issue_cycles_per_board_step": cyc,
+        "issue_cycles_source": "build/r48_env.s hot loop (tools/isa_hist.py) x profiles/r02/instr_rate.txt",
+        "valu_wave_instr_per_board_step": per,
+        "valu_instr_rate": {"achieved": per * rate_dev / 1e9, "peak": VALU_PEAK_G, "unit": "G VALU wave-instr/s",
+                            "frac": per * rate_dev / 1e9 / VALU_PEAK_G,
+                            "note": "SQ_INSTS_VALU per board-step (PMC) at the device rate; peak = one wave64 "
+                                    "instruction per 2 cycles per SIMD (half-rate instructions take ~4.3)"}})
+    if trace is not None and trace.get("source_sha16") == sha:
+        out["frac_trace"] = trace["frac"]
+        out["frac_trace_source"] = "profiles/%s/roofline_from_trace.json (median k_step_n dispatch of the traced " \
+                                   "driver command)" % PROFILE_ROUND
+    return out
 
 
 def extras(dev, seed, n_small):
@@ -265,15 +312,18 @@ def _allreduce_label(world):
     return "%s all_reduce(SUM)/world" % ("RCCL (torch backend 'nccl')" if b == "nccl" else "torch backend '%s'" % b)
 
 
-def a3c_config3(dev, seed, n_boards, updates=2, world=1):
+def a3c_config3(dev, seed, n_boards, updates=2, world=1, mode="textbook", features="exponents"):
     """BASELINE configs[2] (world 1: 2^20 boards + 2-layer CNN policy on 1 MI355X) and configs[3]
     (world > 1: 2^20 boards per GPU, 8M boards on 8 GPUs, one all-reduce of the flat fp32
     gradient per update): A3C rollout (MAX_STEP_NUM = 100 steps: fused CNN inference + softmax +
     Philox sampling -> env kernel) and the synchronous update (fused MFMA gradient pass,
-    all-reduce, TF1 RMSProp kernel)."""
+    all-reduce, TF1 RMSProp kernel). mode "reference" + features "values" is what a user of the
+    reference gets (raw tile values in, a3c.py:37-39,139; post-step states, reward 0, dropped last
+    reward and the literal [B,B,4]-broadcast actor loss, a3c.py:99-123,187-256); "textbook" +
+    "exponents" is the build's learning-oriented variant."""
     from rein48_amd.a3c import A3CConfig, A3CTrainer
-    cfg = A3CConfig(n_boards=n_boards, max_steps=100, mode="textbook", net="cnn", bf16=True,
-                    features="exponents", seed=seed, update_chunk=10)
+    cfg = A3CConfig(n_boards=n_boards, max_steps=100, mode=mode, net="cnn", bf16=True,
+                    features=features, seed=seed, update_chunk=10)
     tr = A3CTrainer(cfg, device=dev)
     tr.train_step()                                   # warm-up (allocator, kernels, first collective)
     s = torch.cuda.current_stream(dev)
@@ -296,7 +346,7 @@ def a3c_config3(dev, seed, n_boards, updates=2, world=1):
     board_steps = world * n_boards * cfg.max_steps  # every board is stepped every rollout step
     lab = _allreduce_label(world)
     return {"boards": world * n_boards, "boards_per_gpu": n_boards, "n_gpus": world,
-            "net": "cnn (conv2x2x32, conv2x2x64, heads 256->4/1), bf16",
+            "net": "cnn (conv2x2x32, conv2x2x64, heads 256->4/1), bf16", "mode": mode, "features": features,
             "gradient_allreduce": ("%s of %d fp32 per update" % (lab, tr.flat.grad.numel())) if lab else None,
             "rollout_ms": r, "update_ms": u,
             "rollout_env_steps_per_s": board_steps / (r * 1e-3),
@@ -445,7 +495,7 @@ def main():
     env.fill_random(7)                                    # SURVEY.md 8(d) synthetic start boards
     chunk = K if args.chunk <= 0 else max(1, min(args.chunk, K))
     plan = chunks(K, chunk)
-    elapsed, dev_ms = timed_steps(env, plan, W, chunk, world, dev)
+    elapsed, dev_ms, skew = timed_steps(env, plan, W, chunk, world, dev)
     value = world * n * K / elapsed
     line = {
         "metric": METRIC,
@@ -468,8 +518,9 @@ def main():
                    "steps_per_launch": chunk, "launches": len(plan),
                    "world_size": dist.get_world_size() if world > 1 else 1,
                    "dist_backend": dist.get_backend() if world > 1 else None,
+                   "start_skew_us": skew * 1e6,
                    "visible_devices": ndev},
-        "roofline": roofline_step_n(n, sum(dev_ms), K),
+        "roofline": roofline_step_n(n, elapsed, sum(dev_ms), K),
     }
     if cpu_line is not None:
         line["cpu_baseline"] = cpu_line
@@ -488,10 +539,12 @@ def main():
         # the reference reset-distribution start (one tile per board) instead of the synthetic fill
         env2 = VecGame(n, device=dev, seed=args.seed, board_offset=offset)
         env2.reset()
-        el2, _ = timed_steps(env2, plan, W, chunk, world, dev)
+        el2, _, _ = timed_steps(env2, plan, W, chunk, world, dev)
         ex["reset_start"] = {"value": n * K / el2, "note": "boards start from Game.reset (one 2/4 tile)"}
         del env2
         for key, fn in (("a3c_config3", lambda: a3c_config3(dev, args.seed, n)),
+                        ("a3c_config3_reference",
+                         lambda: a3c_config3(dev, args.seed, n, mode="reference", features="values")),
                         ("dqn_config5", lambda: dqn_config5(dev, args.seed, 1 << 21))):
             try:
                 ex[key] = fn()

@@ -224,8 +224,9 @@ def test_fused_cnn_policy_is_independent_of_tiling():
             assert torch.equal(f[lo:hi], q), (lo, hi)
 
 
+@pytest.mark.parametrize("exponents", [True, False])
 @pytest.mark.parametrize("mode", ["textbook", "reference"])
-def test_fused_cnn_update_gradients_match_torch(mode):
+def test_fused_cnn_update_gradients_match_torch(mode, exponents):
     """r48_cnn_train_grad (forward + loss + backward + weight gradients in one MFMA pass, rows
     moved to K through ds_read_b64_tr_b16 LDS images) vs PyTorch autograd of the trainer's own
     loss (losses.chunk_loss) on the same states. Per parameter tensor, error = max|g - g32| /
@@ -249,7 +250,7 @@ def test_fused_cnn_update_gradients_match_torch(mode):
     targets = torch.from_numpy(rng.normal(scale=2.0, size=(T, n)).astype(np.float32)).to(DEV)
     lengths = torch.from_numpy(rng.integers(1, T + 1, size=n)).to(DEV)
     mask = (torch.arange(T, device=DEV)[:, None] < lengths[None, :])
-    x = K.board_features(boards.view(-1, 16), exponents=True)
+    x = K.board_features(boards.view(-1, 16), exponents=exponents)
     with torch.no_grad():
         _, v = net(x)
     stats = segment_stats(v.view(T, n), targets, actions, mask)
@@ -272,7 +273,7 @@ def test_fused_cnn_update_gradients_match_torch(mode):
         cm = ((stats["td_sum"] / (4.0 * stats["B"] ** 2))[None, :] * m / n).contiguous()
         counts = stats["counts"].float().contiguous()
     gf, af, cf = cnn_train_grad(net, boards.view(-1, 16), actions.view(-1).contiguous(), targets.view(-1).contiguous(),
-                                wn.view(-1), None if cm is None else cm.view(-1), counts, exponents=True, n_boards=n)
+                                wn.view(-1), None if cm is None else cm.view(-1), counts, exponents=exponents, n_boards=n)
     names = ["conv1.w", "conv1.b", "conv2.w", "conv2.b", "heads.w", "heads.b"]
     for name, f, r32, r16 in zip(names, gf, g32, g16):
         scale = float(r32.abs().max())

@@ -1,16 +1,15 @@
-"""GPU experiment: where k_cnn_train's time goes. Times r48_cnn_train_grad over `rows` synthetic
-states for the product library and for ablation builds (R48_TRAIN_SKIP, see r48_a3c_train.hip)
-made by `make ablate`; the ablated gradients are wrong by construction, only their time counts.
+"""GPU experiment: times r48_cnn_train_grad (k_cnn_train + its two reduction launches) over `rows`
+synthetic states for the product library, or for variant libraries given on the command line
+(tools/build_variant.sh), with a bit-level digest of the gradient.
 
-    python tools/exp_train_ablate.py [rows] [lib.so ...]   (explicit libraries instead of the ablations)
+    python tools/exp_train.py [rows] [lib.so ...]
 """
-import glob
 import os
 import sys
 
 import torch
 
-sys.path.insert(0, ".")
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
 from rein48_amd import _lib  # noqa: E402
 from rein48_amd.a3c.fused import cnn_train_grad, pack_cnn_train  # noqa: E402
 from rein48_amd.a3c.nets import ActorCriticCNN  # noqa: E402
@@ -18,7 +17,7 @@ from rein48_amd.a3c.nets import ActorCriticCNN  # noqa: E402
 rows = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 24
 dev = torch.device("cuda:0")
 n = 1 << 20
-libs = sys.argv[2:] or [_lib.LIB_PATH] + sorted(glob.glob("build/ablate_train/librein48_skip*.so"))
+libs = sys.argv[2:] or [_lib.LIB_PATH]
 g = torch.Generator(device="cpu").manual_seed(0)
 boards = torch.randint(0, 12, (rows, 16), generator=g, dtype=torch.int8).to(dev)
 actions = torch.randint(0, 4, (rows,), generator=g, dtype=torch.int8).to(dev)

@@ -7,7 +7,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, ".")
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
 from rein48_amd.a3c import A3CConfig, A3CTrainer  # noqa: E402
 
 iters = int(sys.argv[1]) if len(sys.argv) > 1 else 2

@@ -3,7 +3,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, ".")
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
 from rein48_amd.dqn import DQNConfig, DQNTrainer  # noqa: E402
 
 if __name__ == "__main__":

@@ -7,7 +7,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, ".")
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
 from rein48_amd import _lib  # noqa: E402
 from rein48_amd.a3c.fused import cnn_train_grad, pack_cnn_train  # noqa: E402
 from rein48_amd.a3c.nets import ActorCriticCNN  # noqa: E402
