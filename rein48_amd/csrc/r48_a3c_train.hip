@@ -188,9 +188,26 @@ __device__ __forceinline__ void acc32_v(f32x16 &acc, const bf16x8 &a, const bf16
     asm("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
 }
 
-__device__ __forceinline__ void acc32(f32x16 &acc, const bf16x8 &a, const bf16x8 &b)
+// the same with the A operand held in AGPRs (dh2^T: only ever an MFMA operand, so it waits in
+// the accumulator file and leaves the VGPRs to the in-flight accumulators of the position loop)
+__device__ __forceinline__ void acc32_av(f32x16 &acc, const bf16x8 &a, const bf16x8 &b)
 {
-    asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+    asm("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "a"(a), "v"(b));
+}
+
+__device__ __forceinline__ void acc32_a(f32x16 &acc, const bf16x8 &a, const bf16x8 &b)
+{
+    asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "a"(a), "v"(b));
+}
+
+__device__ __forceinline__ void acc16_a(f32x4 &acc, const bf16x8 &a, const bf16x8 &b)
+{
+    asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "a"(a), "v"(b));
+}
+
+__device__ __forceinline__ void acc16_av(f32x4 &acc, const bf16x8 &a, const bf16x8 &b)
+{
+    asm("s_nop 1\n\tv_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "a"(a), "v"(b));
 }
 
 __device__ __forceinline__ void acc16_v(f32x4 &acc, const bf16x8 &a, const bf16x8 &b)
@@ -217,6 +234,30 @@ __device__ __forceinline__ bf16x8 splat_frag(uint32_t w)
     bf16x8 f;
     __builtin_memcpy(&f, &v, 16);
     return f;
+}
+
+// conv1 as cnn_conv1 (same products, same bits), with the MFMA of position R + 1 issued before the
+// epilogue of R (two accumulators in flight) so the pipe runs under the bf16 pack + ReLU
+__device__ __forceinline__ void fwd_conv1(const uint4 *w, const float *b, int lane, int h, const bf16x8 &x,
+                                          WStream &ws, bf16x8 (&h1)[9][2], int after0, int after1)
+{
+    const f32x16 b1 = load_bias(b, h);
+    bf16x8 wa = ws.step(w, 2, lane);
+    wfence();
+    f32x16 acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, x, b1, 0, 0, 0);
+#pragma unroll
+    for (int R = 0; R < 9; R++) {
+        f32x16 nxt = acc;
+        if (R + 1 < 9) {
+            wa = ws.step(w, R + 3 < 9 ? R + 3 : (R + 3 == 9 ? after0 : after1), lane);
+            wfence();
+            nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, x, b1, 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        h1[R][0] = acc_to_frag_relu(acc, 0);
+        h1[R][1] = acc_to_frag_relu(acc, 1);
+        acc = nxt;
+    }
 }
 
 // conv2 (grouped by weight fragment, as cnn_conv2_heads_grouped) + heads, keeping h2[p][g][s]
@@ -331,7 +372,9 @@ __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
     const int64_t n_tiles = (rows + 31) / 32;
     const int64_t stride = (int64_t)gridDim.x * kWaves;
     const int64_t first = (int64_t)blockIdx.x * kWaves + wave;
-    // per-row inputs, loaded one tile ahead (wt = 0 on padding rows; loss inputs only in lane half 0)
+    // per-row inputs of the NEXT tile, loaded after the current tile's loss has consumed its own
+    // (so the loads' latency hides behind the backward and no wait on them lands mid-tile); every
+    // lane loads (no divergent branches around the loads), wt = 0 on padding rows
     struct RowIn {
         uint2 raw;
         float wt, tgt, c;
@@ -344,22 +387,23 @@ __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
         const bool live = r < rows && tile < n_tiles;
         const int64_t rr = r < rows ? r : rows - 1;     // padding lanes compute on a valid row, weight 0
         in.raw = *reinterpret_cast<const uint2 *>(boards + 16 * rr + 8 * h);
-        in.wt = 0.f, in.tgt = 0.f, in.c = 0.f, in.act = 0, in.cnt = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (h == 0) {
-            in.wt = live ? wn[rr] : 0.0f;
-            in.tgt = targets[rr];
-            in.act = actions[rr] & 3;
-            if (cm) {
-                in.c = live ? cm[rr] : 0.0f;
-                in.cnt = *reinterpret_cast<const float4 *>(counts + 4 * (rr % n_boards));
-            }
+        const float wt = wn[rr];
+        in.wt = live ? wt : 0.0f;
+        in.tgt = targets[rr];
+        in.act = actions[rr] & 3;
+        in.c = 0.f, in.cnt = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (cm) {   // wave-uniform
+            const float c = cm[rr];
+            in.c = live ? c : 0.0f;
+            // row rr belongs to board rr % n_boards (rows are [T][n_boards]); 32-bit when it fits
+            const int64_t bidx = rows <= 0xFFFFFFFFll ? (int64_t)((uint32_t)rr % (uint32_t)n_boards) : rr % n_boards;
+            in.cnt = *reinterpret_cast<const float4 *>(counts + 4 * bidx);
         }
         return in;
     };
     RowIn next = fetch(first);
     for (int64_t tile = first; tile < n_tiles; tile += stride) {
         const RowIn in = next;
-        next = fetch(tile + stride);
         // weights and biases are re-read from LDS every tile: an opaque zero offset keeps the
         // compiler from hoisting hundreds of registers of loop-invariant fragments out of the loop
         int wofs = 0;
@@ -386,7 +430,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
             bf16x8 h1[9][2];
             WStream ws;
             ws.start(w, fwd_grouped_frag(0), fwd_grouped_frag(1), lane);
-            cnn_conv1(w, bl, lane, h, x, ws, h1, fwd_grouped_frag(9), fwd_grouped_frag(10));
+            fwd_conv1(w, bl, lane, h, x, ws, h1, fwd_grouped_frag(9), fwd_grouped_frag(10));
             fwd_conv2_heads(w, bl, lane, h, h1, ws, h2, out, my, la);
         }
         // ---------------- loss gradient per row (lane half 0: logits rows 0..3; value in lane + 32)
@@ -446,6 +490,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
             for (int o = 0; o < 5; o++)
                 my[kDt + o * 32 + la.xw] = __builtin_bit_cast(uint16_t, (__bf16)dd[o]);
         }
+        next = fetch(tile + stride);      // the current tile's row inputs are consumed
         // dout as the B operand: k = 8h + j = output o (half 0: dz0..3, dv; half 1: 0)
         bf16x8 dout;
         {
@@ -453,35 +498,37 @@ __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
             uint32_t pk[4] = {h == 0 ? d0 : 0u, h == 0 ? d1 : 0u, h == 0 ? d2 : 0u, 0u};
             __builtin_memcpy(&dout, pk, 16);
         }
-        // ---------------- dh2 = Wh^T dout . [h2 > 0]  (orientation 1; h2 dies here)
+        // ---------------- dh2 = Wh^T dout . [h2 > 0] (orientation 1; h2 dies here), with
+        // dWh[o][f] += sum over rows of h2^T[f] dout[o] (A = h2^T read back transposed from the image,
+        // B = Dt with the column selector; 16x16x32, 8 feature tiles x 2 row steps) interleaved: per
+        // dh2 MFMA two dWh MFMAs, and MFMA m + 1 issues before the epilogue of m, so the pipe runs
+        // under the bf16 pack + ReLU' of every dh2 accumulator
         bf16x8 dh2[4][2][2];
-        {
-            bf16x8 q0 = frag_at(w, kOffWhT, lane), q1 = frag_at(w, kOffWhT + 1, lane);
-#pragma unroll
-            for (int m = 0; m < 8; m++) {               // m = 2p + g
-                const bf16x8 wa = q0;
-                q0 = q1;
-                if (m + 2 < 8)
-                    q1 = frag_at(w, kOffWhT + m + 2, lane);
-                wfence();
-                const f32x16 a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, dout, zero, 0, 0, 0);
-                wfence();
-                dh2[m >> 1][m & 1][0] = mask_pk(acc_to_frag(a, 0), h2[m >> 1][m & 1][0]);
-                dh2[m >> 1][m & 1][1] = mask_pk(acc_to_frag(a, 1), h2[m >> 1][m & 1][1]);
-            }
-        }
-        // ---------------- dWh[o][f] += sum over rows of h2^T[f] dout[o]: A = h2^T (image, transposed),
-        // B = Dt with the column selector (16x16x32; 8 feature tiles x 2 row steps)
         {
             const bf16x8 bd0 = lds_frag(my + la.dr), bd1 = lds_frag(my + la.dr + 16);
             bf16x8 A = trr(my, la, 0, 0);
+            f32x16 acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_at(w, kOffWhT, lane), dout, zero, 0, 0, 0);
+            bf16x8 q = frag_at(w, kOffWhT + 1, lane);
 #pragma unroll
-            for (int k = 0; k < 16; k++) {
-                const bf16x8 An = k + 1 < 16 ? trr(my, la, (k + 1) >> 1, (k + 1) & 1) : A;
-                wfence();
-                acc16_lds(dwh[k >> 1], A, (k & 1) ? bd1 : bd0);
-                wfence();
-                A = An;
+            for (int m = 0; m < 8; m++) {               // m = 2p + g = the dWh feature tile ft
+                f32x16 nxt = acc;
+                if (m + 1 < 8) {
+                    const bf16x8 wa = q;
+                    if (m + 2 < 8)
+                        q = frag_at(w, kOffWhT + m + 2, lane);
+                    wfence();
+                    nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, dout, zero, 0, 0, 0);
+                }
+#pragma unroll
+                for (int k = 2 * m; k < 2 * m + 2; k++) {
+                    const bf16x8 An = k + 1 < 16 ? trr(my, la, (k + 1) >> 1, (k + 1) & 1) : A;
+                    acc16_lds(dwh[m], A, (k & 1) ? bd1 : bd0);
+                    A = An;
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                dh2[m >> 1][m & 1][0] = mask_pk(acc_to_frag(acc, 0), h2[m >> 1][m & 1][0]);
+                dh2[m >> 1][m & 1][1] = mask_pk(acc_to_frag(acc, 1), h2[m >> 1][m & 1][1]);
+                acc = nxt;
             }
         }
         // the dh2 image replaces the h2 image: every read of the h2 image is issued before (one
@@ -514,12 +561,14 @@ __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
 #pragma unroll
                     for (int s = 0; s < 2; s++) {
                         if (p == 0 && s == 0)
-                            acc16_v(db2, dh2t[p][ot][s], ot ? sel1 : sel0);
+                            acc16_av(db2, dh2t[p][ot][s], ot ? sel1 : sel0);
                         else
-                            acc16_lds(db2, dh2t[p][ot][s], ot ? sel1 : sel0);
+                            acc16_a(db2, dh2t[p][ot][s], ot ? sel1 : sel0);
                     }
         }
-        // ---------------- per conv1 position R: h1^T_R, dh1^T_R, dW2, dW1
+        // ---------------- per conv1 position R: h1^T_R, dh1^T_R, dW2, dW1. Software-pipelined: the
+        // h1^T MFMA of R + 1 and the dh1^T epilogue + dW1 MFMAs of R - 1 are issued in the shadow of
+        // R's first dh1 MFMA, so no MFMA waits on an epilogue at a position boundary
         {
             const float b1c = bl[col];
             f32x16 b1s;
@@ -529,41 +578,56 @@ __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
             // W2^T fragments (B operands of dh1^T) stream two MFMAs ahead over the 64 (pair, g, s)
             auto w2t = [](int m) { return kOffW2T + (kDh1K[m >> 2] * 2 + ((m >> 1) & 1)) * 2 + (m & 1); };
             bf16x8 q0 = frag_at(w, w2t(0), lane), q1 = frag_at(w, w2t(1), lane);
+            // h1^T_R: A = x (rows x cells), B = W1_R^T (the W1 fragment's registers), C = b1 per lane
+            f32x16 a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x, frag_at(w, 0, lane), b1s, 0, 0, 0);
+            f32x16 dprev = zero;
+            bf16x8 hprev[2], xprev[2];
 #pragma unroll
             for (int R = 0; R < 9; R++) {
                 const bf16x8 xb0 = lds_frag(my + la.xr + cell_base(R) * 32);
                 const bf16x8 xb1 = lds_frag(my + la.xr + cell_base(R) * 32 + 16);
-                // h1^T_R: A = x (rows x cells), B = W1_R^T (the W1 fragment's registers)
-                const bf16x8 w1 = frag_at(w, R, lane);
-                const f32x16 a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x, w1, b1s, 0, 0, 0);
+                const bf16x8 w1n = frag_at(w, R + 1 < 9 ? R + 1 : 0, lane);
                 bf16x8 h1t[2];
-                f32x16 d = zero;
+                f32x16 d = zero, a1n = a1;
 #pragma unroll
                 for (int m = 4 * kRFirst[R]; m < 4 * kRFirst[R + 1]; m++) {
                     const int n = m >> 2, p = kDh1P[n], kk = kDh1K[n], g = (m >> 1) & 1, s = m & 1;
+                    const bool first = m == 4 * kRFirst[R];
                     const bf16x8 wb = q0;
                     q0 = q1;
                     if (m + 2 < 64)
                         q1 = frag_at(w, w2t(m + 2), lane);
                     wfence();
                     d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(dh2[p][g][s], wb, d, 0, 0, 0);
-                    wfence();
-                    if (m == 4 * kRFirst[R]) {
+                    if (first && R + 1 < 9)
+                        a1n = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x, w1n, b1s, 0, 0, 0);
+                    __builtin_amdgcn_sched_barrier(0);
+                    if (first) {
                         h1t[0] = acc_to_frag_relu(a1, 0);
                         h1t[1] = acc_to_frag_relu(a1, 1);
+                        if (R > 0) {
+                            const bf16x8 t0 = mask_pk(acc_to_frag(dprev, 0), hprev[0]);
+                            const bf16x8 t1 = mask_pk(acc_to_frag(dprev, 1), hprev[1]);
+                            acc16_v(dw1, t0, xprev[0]);
+                            acc16_v(dw1, t1, xprev[1]);
+                        }
                     }
                     // dW2[ot = g][kk] += dh2_p^T (o-tile g, row step s) x h1^T_R (row step s); only
-                    // the first MFMA after the h1^T epilogue needs the VALU -> MFMA wait states
-                    if (m == 4 * kRFirst[R])
-                        acc32_v(dw2[g][kk], dh2t[p][g][s], h1t[s]);
+                    // the first after the h1^T epilogue needs the VALU -> MFMA wait states
+                    if (first)
+                        acc32_av(dw2[g][kk], dh2t[p][g][s], h1t[s]);
                     else
-                        acc32(dw2[g][kk], dh2t[p][g][s], h1t[s]);
+                        acc32_a(dw2[g][kk], dh2t[p][g][s], h1t[s]);
                 }
-                const bf16x8 dh1t0 = mask_pk(acc_to_frag(d, 0), h1t[0]);
-                const bf16x8 dh1t1 = mask_pk(acc_to_frag(d, 1), h1t[1]);
-                acc16_v(dw1, dh1t0, xb0);
-                acc16_v(dw1, dh1t1, xb1);
+                dprev = d;
+                hprev[0] = h1t[0], hprev[1] = h1t[1];
+                xprev[0] = xb0, xprev[1] = xb1;
+                a1 = a1n;
             }
+            const bf16x8 t0 = mask_pk(acc_to_frag(dprev, 0), hprev[0]);
+            const bf16x8 t1 = mask_pk(acc_to_frag(dprev, 1), hprev[1]);
+            acc16_v(dw1, t0, xprev[0]);
+            acc16_v(dw1, t1, xprev[1]);
         }
     }
 
