@@ -39,6 +39,13 @@ extern "C" {
 #define R48_RANDOM_POLICY 2u   /* actions drawn in-kernel (control/rand.py:9-11) and written back */
 #define R48_MERGE_REWARD 4u    /* reward = merged tile values (opt-in; reference reward is 0) */
 
+/* Version of the Philox-mode draw contract (which Philox words decide action, spawn and reset;
+ * DESIGN.md section 7, restated in oracle/r48_oracle.c). A seed replays the same trajectories
+ * only under the same version: version 2 (round 2) counts the spawn rank over the blanks in the
+ * line order of the action, version 1 counted them row-major. The injected-draw path
+ * (r48_env_step_with_draws) is the reference's row-major rule under every version. */
+#define R48_DRAW_CONTRACT 2
+
 typedef struct r48_env r48_env;
 
 /* Game.__init__ (GameClient.py:19-29) for a batch: an env of n_boards boards on `device`.

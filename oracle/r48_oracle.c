@@ -365,12 +365,19 @@ ORC_API int orc_pyrand_episode(orc_mt *s, int max_steps, int8_t *start, int32_t 
 /* ------------------------------------------------------------------------------------
  * Philox4x32-10 (Salmon et al., SC'11) -- the production RNG of the HIP kernel. Only the
  * build defines how its words are used (the reference has no counter-based RNG); this is
- * the specification the kernel must match bit-for-bit (DESIGN.md "Philox mode"):
+ * the specification the kernel must match bit-for-bit (contract version 2
+ * = R48_DRAW_CONTRACT in include/rein48.h):
  *   key = {seed lo, seed hi}
- *   step:  ctr = {gid lo, gid hi, step, 0x2048}  -> w0 action (w0>>30) in random-policy mode,
- *          w1 spawn rank mulhi(w1, n_blank), w2 four iff w2 < 0x1999999A,
- *          w3 auto-reset tile: cell rank w3>>28 of 16, four iff (w3 & 0x0FFFFFFF) < 0x0199999A
- *   reset: ctr = {gid lo, gid hi, reset_ctr, 0x5E7} -> rank w0>>28, four iff w1 < 0x1999999A
+ *   step:  boards with global ids 2q and 2q+1 share ctr = {q lo, q hi, step, 0x2048}; the even
+ *          board takes (x, y) = (w0, w1), the odd one (w2, w3). Per board: action x >> 30 in
+ *          random-policy mode; spawn a 4 iff (x & 0x3FFFFFFF) < 0x06666666; spawn rank
+ *          mulhi(y, n_blank) with the blanks counted in LINE order of the action
+ *          (orc_spawn_lines); auto-reset tile: cell y >> 28 (row-major), a 4 iff
+ *          (y & 0x0FFFFFFF) < 0x0199999A (y is free then: a step that ends done spawned into
+ *          its last blank, mulhi(y, 1) = 0, or spawned nothing).
+ *          Contract version 1 (round 1) counted the spawn rank in row-major order: seeds saved
+ *          under it do not replay under version 2.
+ *   reset: ctr = {gid lo, gid hi, reset_ctr, 0x5E7} -> cell w0 >> 28, four iff w1 < 0x1999999A
  * ---------------------------------------------------------------------------------- */
 ORC_API void orc_philox4x32_10(const uint32_t ctr_in[4], const uint32_t key_in[2], uint32_t out[4])
 {

@@ -179,7 +179,7 @@ class Game:
         return [[0 for _ in range(table_size)] for _ in range(table_size)]
 
     @staticmethod
-    def _check(game_matrix):
+    def _check_kernel(game_matrix):
         rows, cols = len(game_matrix), len(game_matrix[0])
         if rows > 4 or cols > 4:
             return _grid_check(game_matrix)
@@ -191,6 +191,20 @@ class Game:
                                            torch.cuda.current_stream(dev).cuda_stream))
         filled, over = out.cpu().tolist()
         return bool(filled), bool(over)
+
+    @staticmethod
+    def _check(game_matrix):
+        """(has_table_filled, has_game_over). On a non-square matrix the reference's game-over loop
+        (GameClient.py:74-91) runs i and j over range(len(matrix)) = the row count: with fewer rows
+        than columns it only sees the leading rows x rows block, with more rows it indexes past the
+        end of a row (IndexError) -- reproduced here; has_table_filled (:96-100) scans every item."""
+        rows, cols = len(game_matrix), len(game_matrix[0])
+        filled, over = Game._check_kernel(game_matrix)
+        if rows == cols or not filled:
+            return filled, over
+        if rows > cols:
+            raise IndexError("list index out of range")
+        return filled, Game._check_kernel([row[:rows] for row in game_matrix])[1]
 
     @staticmethod
     def has_game_over(game_matrix):

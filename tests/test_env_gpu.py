@@ -238,6 +238,49 @@ def test_static_helpers_on_any_shape():
         assert not Game.has_table_filled(full) and not Game.has_game_over(full)
 
 
+def _ref_game_over(m):
+    """GameClient.py:65-100 restated literally: has_table_filled over every item, then i and j
+    over range(len(m)) (the row count) -- on a non-square matrix a leading square block, or an
+    IndexError when the rows outnumber the columns."""
+    if 0 in [x for row in m for x in row]:
+        return False
+    n = len(m)
+    for i in range(n):
+        for j in range(n):
+            if (i != 0 and m[i][j] == m[i - 1][j]) or (j != 0 and m[i][j] == m[i][j - 1]) or \
+                    (i != n - 1 and m[i][j] == m[i + 1][j]) or (j != n - 1 and m[i][j] == m[i][j + 1]):
+                return False
+    return True
+
+
+@pytest.mark.parametrize("rows,cols", [(2, 4), (3, 5), (1, 4), (4, 2), (6, 3), (5, 9)])
+def test_game_over_on_non_square_matrices_follows_reference_loop(rows, cols):
+    """has_game_over on rectangles (<= 4x4: r48_values_check; larger: r48_values_check_grid)
+    reproduces the reference's square-index loop: columns past the row count are never compared,
+    a zero anywhere means not over, and a filled matrix with more rows than columns raises
+    IndexError like the reference."""
+    from rein48_amd.game import Game
+    rng = np.random.default_rng(rows * 31 + cols)
+    for trial in range(40):
+        m = (2 ** rng.integers(1, 5, size=(rows, cols))).astype(int)
+        if trial % 4 == 0:          # equal neighbours only beyond the leading square block
+            m = (2 ** (1 + (np.add.outer(np.arange(rows), np.arange(cols)) % 2) * 3 +
+                       (np.arange(cols)[None, :] >= rows) * 0)).astype(int)
+            if cols > rows:
+                m[:, rows:] = 2
+        if trial % 5 == 1:
+            m[rng.integers(rows), rng.integers(cols)] = 0
+        m = m.tolist()
+        try:
+            want = _ref_game_over(m)
+        except IndexError:
+            with pytest.raises(IndexError):
+                Game.has_game_over(m)
+            continue
+        assert Game.has_game_over(m) == want, (rows, cols, m)
+        assert Game.has_table_filled(m) == (0 not in [x for r in m for x in r])
+
+
 # ---------------------------------------------------------------- Philox mode vs oracle
 @pytest.mark.parametrize("off", [12345, 1 << 20])   # odd: guarded per-board path; even: pair fast path
 @pytest.mark.parametrize("flags", [O.RANDOM_POLICY, O.RANDOM_POLICY | O.AUTO_RESET,
@@ -355,7 +398,9 @@ def test_fill_random_matches_oracle(max_exp):
         v.fill_random(0)
 
 
-@pytest.mark.parametrize("n,offset", [(30_000, 98), (30_001, 97)])   # pair fast path / guarded per-board path
+# pair fast path (even n, even offset) / byte-stored trajectory rows inside the fast path (odd n,
+# even offset) / guarded per-board path (odd offset)
+@pytest.mark.parametrize("n,offset", [(30_000, 98), (30_001, 98), (30_001, 97)])
 def test_rollout_equals_repeated_steps(n, offset):
     K, seed = 37, 4242
     rng = np.random.default_rng(3)
