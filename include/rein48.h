@@ -294,6 +294,26 @@ int r48_egreedy_actions(const float *q, int64_t n, float eps, uint64_t seed, int
 int r48_td_target(const float *reward, const uint8_t *done, const float *q_next_target,
                   const float *q_next_online, int64_t n, float gamma, float *y, void *stream);
 
+/* ---- The ResNet-10 update's 3x3 convolutions on the 4x4 grid (csrc/r48_conv.hip) ----
+ * Channels-last bf16 activations [boards][16 cells][C], 64 output channels, 32 or 64 input
+ * channels; only the 100 in-grid (cell, tap) pairs are computed. Replace the structured dense
+ * GEMMs of nets.py:ResNet10Q._conv (hipBLASLt) in the update. */
+/* One-hot input planes for the training stem: out bf16 [n][16][32] (plane e = exponent 0..17,
+ * planes 18..31 zero), 16-byte aligned. */
+int r48_board_onehot32(const int8_t *boards, int64_t n, void *out, void *stream);
+/* y[b][p][co] = bias[co] + sum over taps t in the grid, ci of W[co][ci][t] x[b][p + off(t)][ci]
+ * (the forward conv; with the flipped, transposed taps the data gradient). wfrag: 9 x 4 x (cin/32)
+ * MFMA A fragments of 1 KiB (rein48_amd/dqn/conv.py pack_conv); bias fp32 [64] or NULL. All
+ * pointers 16-byte aligned. */
+int r48_conv3x3(const void *x, int64_t boards, int32_t cin, const void *wfrag, const float *bias, void *y,
+                void *stream);
+/* dw fp32 [64][cin][3][3] = sum over boards and in-grid cells of dy[b][p][co] x[b][p + off(t)][ci];
+ * workspace of r48_conv_wgrad_workspace_floats(cin) floats (per-workgroup records, summed in a
+ * fixed order: deterministic). */
+int64_t r48_conv_wgrad_workspace_floats(int32_t cin);
+int r48_conv3x3_wgrad(const void *dy, const void *x, int64_t boards, int32_t cin, float *workspace, float *dw,
+                      void *stream);
+
 /* Fused ResNet-10 Q-network inference on bf16 MFMA (rein48_amd/dqn/nets.py:ResNet10Q with
  * C = 64, 4 basic blocks, eval-mode BN folded): boards int8[n][16] (16-byte aligned) -> q
  * float[n][4] (nullable, 16-byte aligned) and, when actions != NULL, the epsilon-greedy draw of

@@ -78,6 +78,7 @@ constexpr int kPartial = kOffLoss + 2;                        // 9703
 constexpr size_t kLdsWeights = (size_t)(kFragsTrain * 64 + 32) * 16;
 constexpr size_t kLds = kLdsWeights + (size_t)kWaves * kSlot * 2;         // 143,520 B
 constexpr float kEntropyEps = 1e-5f;                          // a3c.py:114
+constexpr float kLn2 = 0.69314718055994531f;
 
 // (conv2 output p, input block kk) pairs grouped by the conv1 position R = kP2[p][kk]
 __device__ constexpr int kDh1P[16] = {0, 0, 1, 1, 0, 2, 0, 1, 2, 3, 1, 3, 2, 2, 3, 3};
@@ -322,6 +323,48 @@ __device__ __forceinline__ void fwd_conv2_heads(const uint4 *w, const float *b, 
     out = o;
 }
 
+// conv2 + heads in chain order (as cnn_conv2_heads: chain c = 2p + g is output position p, half g,
+// its 8 W2 fragments accumulated in one register set; the 2 head MFMAs of chain c issue after chain
+// c + 1), so at most two conv2 accumulators are live and each chain's bf16 pack + ReLU + image store
+// runs under the next chain's MFMAs. 89 fragment reads per tile (the grouped order reads 41 but
+// needs four accumulators and all of h1 at once: no room for the epilogues to overlap).
+__device__ __forceinline__ void fwd_conv2_heads_chain(const uint4 *w, const float *b, int lane, int h,
+                                                      const bf16x8 (&h1)[9][2], WStream &ws, bf16x8 (&h2)[4][2][2],
+                                                      f32x16 &out, uint16_t *img, const LaneAddr &la)
+{
+    const f32x16 b2[2] = {load_bias(b + 32, h), load_bias(b + 64, h)};
+    out = f32x16{};
+    f32x16 acc[2];
+    int i = 9;
+#pragma unroll
+    for (int c = 0; c <= 8; c++) {
+        if (c < 8) {
+            const int p = c >> 1;
+            f32x16 a = b2[c & 1];
+#pragma unroll
+            for (int u = 0; u < 8; u++, i++) {
+                const bf16x8 wa = ws.step(w, fwd_frag(i + 2 < kFwdMfmas ? i + 2 : 0), lane);
+                wfence();
+                a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, h1[kP2[p][u >> 1]][u & 1], a, 0, 0, 0);
+                wfence();
+            }
+            acc[c & 1] = a;
+        }
+        if (c >= 1) {
+            const int cp = c - 1, p = cp >> 1, g = cp & 1;
+#pragma unroll
+            for (int s = 0; s < 2; s++, i++) {
+                h2[p][g][s] = acc_to_frag_relu(acc[cp & 1], s);
+                store_frag(img, la, 64 * p + 32 * g + 16 * s, h2[p][g][s]);
+                const bf16x8 wa = ws.step(w, fwd_frag(i + 2 < kFwdMfmas ? i + 2 : 0), lane);
+                wfence();
+                out = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, h2[p][g][s], out, 0, 0, 0);
+                wfence();
+            }
+        }
+    }
+}
+
 template <int MODE>
 __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
     const int8_t *__restrict__ boards, int64_t rows, int64_t n_boards, const int8_t *__restrict__ actions,
@@ -429,12 +472,21 @@ __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
         {
             bf16x8 h1[9][2];
             WStream ws;
+#ifndef R48_TRAIN_GROUPED_FWD
+            ws.start(w, fwd_frag(0), fwd_frag(1), lane);
+            fwd_conv1(w, bl, lane, h, x, ws, h1, fwd_frag(9), fwd_frag(10));
+            fwd_conv2_heads_chain(w, bl, lane, h, h1, ws, h2, out, my, la);
+#else
             ws.start(w, fwd_grouped_frag(0), fwd_grouped_frag(1), lane);
             fwd_conv1(w, bl, lane, h, x, ws, h1, fwd_grouped_frag(9), fwd_grouped_frag(10));
             fwd_conv2_heads(w, bl, lane, h, h1, ws, h2, out, my, la);
+#endif
         }
         // ---------------- loss gradient per row (lane half 0: logits rows 0..3; value in lane + 32)
-        const float v = __shfl(out[0], col + 32) + bl[100];
+        // the value (row 4 = lane half 1's first register) into lane half 0: v_permlane32_swap, no LDS
+        const float v = __uint_as_float(__builtin_amdgcn_permlane32_swap(__float_as_uint(out[0]),
+                                                                          __float_as_uint(out[0]), false, false)[1]) +
+                        bl[100];
         float dz[4] = {0.f, 0.f, 0.f, 0.f}, dv = 0.f;
         if (h == 0) {
             const float wt = in.wt;
@@ -449,12 +501,13 @@ __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
                 p[k] = __expf(z[k] - m);
                 se += p[k];
             }
-            const float inv = __builtin_amdgcn_rcpf(se), lse = m + __logf(se);
+            // native v_log_f32 (log2): every argument is >= 1 (se) or >= 1e-5 (p + eps), no denormal path
+            const float inv = __builtin_amdgcn_rcpf(se), lse = m + kLn2 * __builtin_amdgcn_logf(se);
             float H = 0.f, gbar = 0.f;
 #pragma unroll
             for (int k = 0; k < 4; k++) {
                 p[k] *= inv;
-                const float lq = __logf(p[k] + kEntropyEps);
+                const float lq = kLn2 * __builtin_amdgcn_logf(p[k] + kEntropyEps);
                 H -= p[k] * lq;
                 gr[k] = -(lq + p[k] * __builtin_amdgcn_rcpf(p[k] + kEntropyEps));     // dH/dp_k
                 gbar += p[k] * gr[k];
@@ -498,19 +551,25 @@ __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
             uint32_t pk[4] = {h == 0 ? d0 : 0u, h == 0 ? d1 : 0u, h == 0 ? d2 : 0u, 0u};
             __builtin_memcpy(&dout, pk, 16);
         }
-        // ---------------- dh2 = Wh^T dout . [h2 > 0] (orientation 1; h2 dies here), with
-        // dWh[o][f] += sum over rows of h2^T[f] dout[o] (A = h2^T read back transposed from the image,
-        // B = Dt with the column selector; 16x16x32, 8 feature tiles x 2 row steps) interleaved: per
-        // dh2 MFMA two dWh MFMAs, and MFMA m + 1 issues before the epilogue of m, so the pipe runs
-        // under the bf16 pack + ReLU' of every dh2 accumulator
+        // ---------------- dh2 = Wh^T dout . [h2 > 0] (orientation 1; h2 dies here), and under it:
+        //   dWh[o][f] += sum over rows of h2^T[f] dout[o]  (A = h2^T read back transposed from the
+        //     image, B = Dt with the column selector; 16x16x32, 8 feature tiles x 2 row steps)
+        //   the dh2 image, block m written over h2 block m once its last dWh read is issued (one
+        //     wave's LDS operations execute in order), then read back transposed: dh2^T (AGPRs)
+        //   db2 += row sums of dh2^T (16x16x32 with a selector B), one block behind
+        // Per step m (= 2p + g = feature block): dh2 MFMA m + 1, two dWh MFMAs, two db2 MFMAs, then
+        // the epilogue of m (bf16 pack + ReLU') -- the pipe runs under every epilogue.
         bf16x8 dh2[4][2][2];
+        bf16x8 dh2t[4][2][2];
         {
+            const bf16x8 sel0 = splat_frag(n16 == (g16 & 1) ? one2 : 0u);
+            const bf16x8 sel1 = splat_frag(n16 == 2 + (g16 & 1) ? one2 : 0u);
             const bf16x8 bd0 = lds_frag(my + la.dr), bd1 = lds_frag(my + la.dr + 16);
             bf16x8 A = trr(my, la, 0, 0);
             f32x16 acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_at(w, kOffWhT, lane), dout, zero, 0, 0, 0);
             bf16x8 q = frag_at(w, kOffWhT + 1, lane);
 #pragma unroll
-            for (int m = 0; m < 8; m++) {               // m = 2p + g = the dWh feature tile ft
+            for (int m = 0; m <= 8; m++) {              // m = 2p + g = the feature block
                 f32x16 nxt = acc;
                 if (m + 1 < 8) {
                     const bf16x8 wa = q;
@@ -519,52 +578,39 @@ __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
                     wfence();
                     nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, dout, zero, 0, 0, 0);
                 }
+                if (m < 8) {
 #pragma unroll
-                for (int k = 2 * m; k < 2 * m + 2; k++) {
-                    const bf16x8 An = k + 1 < 16 ? trr(my, la, (k + 1) >> 1, (k + 1) & 1) : A;
-                    acc16_lds(dwh[m], A, (k & 1) ? bd1 : bd0);
-                    A = An;
+                    for (int k = 2 * m; k < 2 * m + 2; k++) {
+                        const bf16x8 An = k + 1 < 16 ? trr(my, la, (k + 1) >> 1, (k + 1) & 1) : A;
+                        acc16_lds(dwh[m], A, (k & 1) ? bd1 : bd0);
+                        A = An;
+                    }
                 }
-                __builtin_amdgcn_sched_barrier(0);
-                dh2[m >> 1][m & 1][0] = mask_pk(acc_to_frag(acc, 0), h2[m >> 1][m & 1][0]);
-                dh2[m >> 1][m & 1][1] = mask_pk(acc_to_frag(acc, 1), h2[m >> 1][m & 1][1]);
-                acc = nxt;
-            }
-        }
-        // the dh2 image replaces the h2 image: every read of the h2 image is issued before (one
-        // wave's LDS operations execute in order)
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int p = 0; p < 4; p++)
-#pragma unroll
-            for (int g = 0; g < 2; g++)
-#pragma unroll
-                for (int s = 0; s < 2; s++)
-                    store_frag(my, la, 64 * p + 32 * g + 16 * s, dh2[p][g][s]);
-        __builtin_amdgcn_sched_barrier(0);
-        // ---------------- dh2^T (rows in registers) and db2 += its row sums
-        bf16x8 dh2t[4][2][2];
-#pragma unroll
-        for (int p = 0; p < 4; p++)
-#pragma unroll
-            for (int ot = 0; ot < 2; ot++)
-#pragma unroll
-                for (int s = 0; s < 2; s++)
-                    dh2t[p][ot][s] = trr(my, la, 2 * p + ot, s);
-        {
-            const bf16x8 sel0 = splat_frag(n16 == (g16 & 1) ? one2 : 0u);
-            const bf16x8 sel1 = splat_frag(n16 == 2 + (g16 & 1) ? one2 : 0u);
-#pragma unroll
-            for (int p = 0; p < 4; p++)
-#pragma unroll
-                for (int ot = 0; ot < 2; ot++)
+                if (m >= 1) {                           // db2 of block m - 1 (read at step m - 1)
+                    const int b = m - 1;
 #pragma unroll
                     for (int s = 0; s < 2; s++) {
-                        if (p == 0 && s == 0)
-                            acc16_av(db2, dh2t[p][ot][s], ot ? sel1 : sel0);
+                        if (b == 0 && s == 0)
+                            acc16_av(db2, dh2t[b >> 1][b & 1][s], sel0);
+                        else if (b == 1 && s == 0)
+                            acc16_av(db2, dh2t[b >> 1][b & 1][s], sel1);
                         else
-                            acc16_a(db2, dh2t[p][ot][s], ot ? sel1 : sel0);
+                            acc16_a(db2, dh2t[b >> 1][b & 1][s], (b & 1) ? sel1 : sel0);
                     }
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                if (m < 8) {
+                    const int p = m >> 1, g = m & 1;
+                    dh2[p][g][0] = mask_pk(acc_to_frag(acc, 0), h2[p][g][0]);
+                    dh2[p][g][1] = mask_pk(acc_to_frag(acc, 1), h2[p][g][1]);
+                    store_frag(my, la, 64 * p + 32 * g, dh2[p][g][0]);
+                    store_frag(my, la, 64 * p + 32 * g + 16, dh2[p][g][1]);
+                    dh2t[p][g][0] = trr(my, la, m, 0);
+                    dh2t[p][g][1] = trr(my, la, m, 1);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                acc = nxt;
+            }
         }
         // ---------------- per conv1 position R: h1^T_R, dh1^T_R, dW2, dW1. Software-pipelined: the
         // h1^T MFMA of R + 1 and the dh1^T epilogue + dW1 MFMAs of R - 1 are issued in the shadow of
@@ -587,34 +633,42 @@ __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
                 const bf16x8 xb0 = lds_frag(my + la.xr + cell_base(R) * 32);
                 const bf16x8 xb1 = lds_frag(my + la.xr + cell_base(R) * 32 + 16);
                 const bf16x8 w1n = frag_at(w, R + 1 < 9 ? R + 1 : 0, lane);
-                bf16x8 h1t[2];
+                bf16x8 h1t[2], t0, t1;
                 f32x16 d = zero, a1n = a1;
+                // (1) the dh1^T chain of R (independent of h1^T_R); the h1^T epilogue of R and the
+                // dh1^T epilogue of R - 1 run under it, the h1^T MFMA of R + 1 issues after its first
 #pragma unroll
                 for (int m = 4 * kRFirst[R]; m < 4 * kRFirst[R + 1]; m++) {
-                    const int n = m >> 2, p = kDh1P[n], kk = kDh1K[n], g = (m >> 1) & 1, s = m & 1;
-                    const bool first = m == 4 * kRFirst[R];
+                    const int n = m >> 2, p = kDh1P[n], g = (m >> 1) & 1, s = m & 1;
+                    const int first = 4 * kRFirst[R];
                     const bf16x8 wb = q0;
                     q0 = q1;
                     if (m + 2 < 64)
                         q1 = frag_at(w, w2t(m + 2), lane);
                     wfence();
                     d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(dh2[p][g][s], wb, d, 0, 0, 0);
-                    if (first && R + 1 < 9)
+                    if (m == first && R + 1 < 9)
                         a1n = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x, w1n, b1s, 0, 0, 0);
-                    __builtin_amdgcn_sched_barrier(0);
-                    if (first) {
+                    wfence();
+                    if (m == first) {
                         h1t[0] = acc_to_frag_relu(a1, 0);
                         h1t[1] = acc_to_frag_relu(a1, 1);
-                        if (R > 0) {
-                            const bf16x8 t0 = mask_pk(acc_to_frag(dprev, 0), hprev[0]);
-                            const bf16x8 t1 = mask_pk(acc_to_frag(dprev, 1), hprev[1]);
-                            acc16_v(dw1, t0, xprev[0]);
-                            acc16_v(dw1, t1, xprev[1]);
-                        }
                     }
-                    // dW2[ot = g][kk] += dh2_p^T (o-tile g, row step s) x h1^T_R (row step s); only
-                    // the first after the h1^T epilogue needs the VALU -> MFMA wait states
-                    if (first)
+                    if (m == first + 1 && R > 0) {
+                        t0 = mask_pk(acc_to_frag(dprev, 0), hprev[0]);
+                        t1 = mask_pk(acc_to_frag(dprev, 1), hprev[1]);
+                    }
+                }
+                if (R > 0) {
+                    acc16_v(dw1, t0, xprev[0]);
+                    acc16_v(dw1, t1, xprev[1]);
+                }
+                // (2) dW2[ot = g][kk] += dh2_p^T (o-tile g, row step s) x h1^T_R (row step s) for
+                // every (p, kk) of R
+#pragma unroll
+                for (int m = 4 * kRFirst[R]; m < 4 * kRFirst[R + 1]; m++) {
+                    const int n = m >> 2, p = kDh1P[n], kk = kDh1K[n], g = (m >> 1) & 1, s = m & 1;
+                    if (m < 4 * kRFirst[R] + 4)   // the first pair may follow the h1^T epilogue closely
                         acc32_av(dw2[g][kk], dh2t[p][g][s], h1t[s]);
                     else
                         acc32_a(dw2[g][kk], dh2t[p][g][s], h1t[s]);

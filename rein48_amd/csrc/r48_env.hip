@@ -324,9 +324,11 @@ __global__ __launch_bounds__(kBlock) void k_step_n(int8_t *boards, int64_t n, in
     R48_STAMP_BEGIN
     __shared__ __attribute__((aligned(16))) r48::Orient tab[16];
     load_orient_table(tab);
+    // trajectory rows whose pair addresses are not all 2-byte aligned (odd n or odd row pointers)
+    // take byte stores inside the fast path, instead of sending the whole grid down the guarded one
+    const bool traj_bytes = TRAJ && ((n | (int64_t)((uintptr_t)traj_actions | (uintptr_t)traj_done)) & 1) != 0;
     if ((int64_t)(blockIdx.x + 1) * kTile <= n && (gid0 & 1) == 0 &&
-        planes_aligned(actions, done, changed, reward, score) &&
-        (!TRAJ || ((n | (int64_t)((uintptr_t)traj_actions | (uintptr_t)traj_done)) & 1) == 0)) {
+        planes_aligned(actions, done, changed, reward, score)) {
         Board b[2 * NP];
         uint32_t a[2 * NP], ob[2 * NP];
         uint64_t q[NP];
@@ -383,11 +385,23 @@ __global__ __launch_bounds__(kBlock) void k_step_n(int8_t *boards, int64_t n, in
                     step_lane_lines<RANDOM, AUTO_RESET, REWARD>(b[2 * j + 1], ob[2 * j + 1], tab, a[2 * j + 1], dd, sc);
                 if (TRAJ) {
                     const int64_t at = (int64_t)t * n + base + 2 * kBlock * j;
-                    if (traj_actions)
-                        *reinterpret_cast<uint16_t *>(traj_actions + at) = (uint16_t)(r[2 * j].a | (r[2 * j + 1].a << 8));
-                    if (traj_done)
-                        *reinterpret_cast<uint16_t *>(traj_done + at) =
-                            (uint16_t)(r[2 * j].done | (r[2 * j + 1].done << 8));
+                    if (traj_bytes) {   // wave-uniform
+                        if (traj_actions) {
+                            traj_actions[at] = (int8_t)r[2 * j].a;
+                            traj_actions[at + 1] = (int8_t)r[2 * j + 1].a;
+                        }
+                        if (traj_done) {
+                            traj_done[at] = (uint8_t)r[2 * j].done;
+                            traj_done[at + 1] = (uint8_t)r[2 * j + 1].done;
+                        }
+                    } else {
+                        if (traj_actions)
+                            *reinterpret_cast<uint16_t *>(traj_actions + at) =
+                                (uint16_t)(r[2 * j].a | (r[2 * j + 1].a << 8));
+                        if (traj_done)
+                            *reinterpret_cast<uint16_t *>(traj_done + at) =
+                                (uint16_t)(r[2 * j].done | (r[2 * j + 1].done << 8));
+                    }
                 }
             }
         }

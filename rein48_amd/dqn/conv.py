@@ -1,0 +1,127 @@
+"""Host side of the ResNet-10 update's 3x3 convolutions on the 4x4 grid (csrc/r48_conv.hip).
+
+ResNet10Q (nets.py) trains with channels-last bf16 activations [B, 16 cells, C]. On the GPU its
+convolutions run as three hand-written MFMA kernels instead of the structured dense GEMMs
+(hipBLASLt) of the portable path, and only the 100 in-grid (cell, tap) pairs are computed:
+    forward      r48_conv3x3 with pack_conv(w)           (bias added in the kernel)
+    data grad    r48_conv3x3 with pack_conv_dgrad(w)     (taps flipped, in/out channels swapped)
+    weight grad  r48_conv3x3_wgrad                        (fp32, summed in a fixed order)
+The stem's 18 one-hot planes are padded to one 32-channel k-chunk (board_onehot32).
+
+Fragment layout (v_mfma_f32_16x16x32_bf16 A operand), fragment (tap t, row tile O, k-chunk c) of
+1 KiB: lane l, element j = W[16 O + (l & 15)][32 c + 8 (l >> 4) + j][t // 3][t % 3] (zero past the
+real input channels).
+"""
+import torch
+
+from .. import _lib
+from .._lib import check, ptr
+from ..a3c.kernels import _dev, _stream
+
+_IDX = {}
+
+
+def _frag_index(cin_pad, device):
+    """Index into a [64, cin_pad, 9] weight of every fragment element, [9 * 4 * nc, 64, 8]."""
+    key = (cin_pad, str(device))
+    if key not in _IDX:
+        nc = cin_pad // 32
+        lane = torch.arange(64)
+        j = torch.arange(8)
+        idx = torch.empty(9, 4, nc, 64, 8, dtype=torch.long)
+        for t in range(9):
+            for O in range(4):
+                for c in range(nc):
+                    co = 16 * O + (lane & 15)
+                    ci = 32 * c + 8 * (lane >> 4)
+                    idx[t, O, c] = (co[:, None] * cin_pad + ci[:, None] + j[None, :]) * 9 + t
+        _IDX[key] = idx.view(9 * 4 * nc, 64, 8).to(device)
+    return _IDX[key]
+
+
+def _pack(w9, cin_pad):
+    """w9 [64, ci, 9] (any float dtype) -> bf16 fragments [9 * 4 * nc, 64, 8]."""
+    co, ci = w9.shape[:2]
+    if co != 64 or ci > cin_pad:
+        raise ValueError("r48_conv3x3 needs 64 output channels and <= %d input channels" % cin_pad)
+    wp = w9.float()
+    if ci < cin_pad:
+        wp = torch.cat([wp, wp.new_zeros(co, cin_pad - ci, 9)], 1)
+    return wp.reshape(-1)[_frag_index(cin_pad, w9.device)].to(torch.bfloat16).contiguous()
+
+
+def pack_conv(w, cin_pad):
+    """Forward fragments of a Conv2d(ci, 64, 3, padding=1) weight [64, ci, 3, 3]."""
+    return _pack(w.detach().reshape(w.shape[0], w.shape[1], 9), cin_pad)
+
+
+def pack_conv_dgrad(w):
+    """Data-gradient fragments: W'[ci][co][t] = W[co][ci][8 - t] (64 -> 64 channels)."""
+    w9 = w.detach().reshape(w.shape[0], w.shape[1], 9).flip(2).transpose(0, 1)
+    return _pack(w9, 64)
+
+
+def board_onehot32(boards, out=None):
+    """int8 boards [n, 16] -> bf16 one-hot [n, 16, 32] (planes 18..31 zero)."""
+    _dev(boards, "boards", torch.int8)
+    n = boards.numel() // 16
+    if out is None:
+        out = torch.empty((n, 16, 32), dtype=torch.bfloat16, device=boards.device)
+    check(_lib.load().r48_board_onehot32(ptr(boards), n, ptr(out), _stream(boards)))
+    return out
+
+
+def conv3x3(x, frags, bias=None):
+    """x bf16 [B, 16, cin] (cin 32 or 64) -> y bf16 [B, 16, 64]."""
+    if not (x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous() and x.dim() == 3 and x.shape[1] == 16):
+        raise ValueError("x must be a contiguous bf16 CUDA tensor [B, 16, cin]")
+    B, _, cin = x.shape
+    y = torch.empty((B, 16, 64), dtype=torch.bfloat16, device=x.device)
+    b = None if bias is None else bias.detach().float().contiguous()
+    check(_lib.load().r48_conv3x3(ptr(x), B, cin, ptr(frags), ptr(b), ptr(y), _stream(x)))
+    return y
+
+
+_WS = {}
+
+
+def conv3x3_wgrad(dy, x):
+    """dw fp32 [64, cin, 3, 3] = sum over boards and in-grid cells of dy[b, p, co] x[b, p + off(t), ci]."""
+    for t, name in ((dy, "dy"), (x, "x")):
+        if not (t.is_cuda and t.dtype == torch.bfloat16 and t.is_contiguous() and t.dim() == 3):
+            raise ValueError("%s must be a contiguous bf16 CUDA tensor [B, 16, C]" % name)
+    B, _, cin = x.shape
+    L = _lib.load()
+    key = (cin, str(x.device))
+    if key not in _WS:
+        _WS[key] = torch.empty(L.r48_conv_wgrad_workspace_floats(cin), dtype=torch.float32, device=x.device)
+    dw = torch.empty((64, cin, 3, 3), dtype=torch.float32, device=x.device)
+    check(L.r48_conv3x3_wgrad(ptr(dy), ptr(x), B, cin, ptr(_WS[key]), ptr(dw), _stream(x)))
+    return dw
+
+
+class Conv3x3Train(torch.autograd.Function):
+    """y = conv3x3(x, w) + bias on the 4x4 grid for channels-last bf16 x [B, 16, cin_pad]; the
+    weight's real input channels may be fewer than cin_pad (the stem). bias is a constant."""
+
+    @staticmethod
+    def forward(ctx, x, w, bias):
+        cin_pad = x.shape[2]
+        y = conv3x3(x, pack_conv(w, cin_pad), bias)
+        ctx.save_for_backward(x, w)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        gy = gy.to(torch.bfloat16).contiguous()
+        dx = conv3x3(gy, pack_conv_dgrad(w)) if ctx.needs_input_grad[0] else None
+        dw = None
+        if ctx.needs_input_grad[1]:
+            dw = conv3x3_wgrad(gy, x)[:, :w.shape[1]].to(w.dtype)
+        return dx, dw, None
+
+
+def conv3x3_train(x, conv):
+    """Conv2d(ci, 64, 3, padding=1) `conv` on channels-last bf16 x [B, 16, cin_pad] (training)."""
+    return Conv3x3Train.apply(x, conv.weight, conv.bias)

@@ -104,6 +104,7 @@ class ResNet10Q(nn.Module):
         self.dtype = dtype
         self.channels, self.n_blocks, self.use_bn = channels, blocks, bn
         self.fused_bn = True          # training-mode BN + ReLU (+ add) via r48_bn_* on bf16 GPU tensors
+        self.custom_conv = True       # bf16 GPU convs via r48_conv3x3 / _wgrad (conv.py) instead of dense GEMMs
         C = channels
         self.stem = nn.Conv2d(PLANES, C, 3, padding=1)
         self.convs = nn.ModuleList([nn.Conv2d(C, C, 3, padding=1) for _ in range(2 * blocks)])
@@ -130,7 +131,25 @@ class ResNet10Q(nn.Module):
             x = x.to(bn.weight.dtype)                   # CPU batch_norm needs matching dtypes
         return bn(x).view(B, 16 * self.channels)
 
+    def wants_onehot32(self, device, dtype):
+        """True when the input planes should come padded to 32 (board_onehot32): the custom convs."""
+        return (self.custom_conv and self.use_bn and torch.device(device).type == "cuda" and dtype == torch.bfloat16
+                and self.channels == 64)
+
+    def _custom_conv(self, h):
+        return (self.custom_conv and self.use_bn and h.is_cuda and h.dtype == torch.bfloat16
+                and self.channels == 64)
+
     def _conv(self, conv, h):
+        if self._custom_conv(h):
+            # channels-last [B, 16, cin] through the hand-written block-sparse MFMA convs; the
+            # bias is a constant before training-mode BN (see below), added in the kernel
+            from .conv import conv3x3_train
+            B = h.shape[0]
+            x = h.reshape(B, 16, -1)
+            if x.shape[2] not in (32, 64):        # the stem's 18 one-hot planes -> one 32-channel chunk
+                x = F.pad(x, (0, 32 - x.shape[2]))
+            return conv3x3_train(x.contiguous(), conv).view(B, 16 * 64)
         b = conv.bias.repeat(16)
         if self.use_bn:
             # every conv feeds a training-mode BN, which subtracts the batch mean: the conv bias has

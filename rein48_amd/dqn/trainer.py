@@ -206,7 +206,11 @@ class DQNTrainer(DQNLearner):
         c = self.cfg
         dt = torch.bfloat16 if c.bf16 else torch.float32
         b = self.replay.sample(batch or c.batch)
-        x = board_onehot(b["state"], dtype=dt)
+        if self.net.wants_onehot32(b["state"].device, dt):
+            from .conv import board_onehot32
+            x = board_onehot32(b["state"]).view(-1, 16 * 32)     # the training stem's padded planes
+        else:
+            x = board_onehot(b["state"], dtype=dt)
         with torch.no_grad():
             self.target.eval()
             qt = self.q_eval(self.target, b["next_state"]).contiguous()

@@ -373,3 +373,83 @@ def test_fused_resnet_tile_edges_bit_identical():
         assert torch.equal(q.view(torch.int32), full[:n].view(torch.int32)), n
     q0, a0 = resnet_q_forward(b[:0].contiguous(), blob, actions=True)
     assert q0.shape == (0, 4) and a0.shape == (0,)
+
+
+# ---------------------------------------------------------------- the update's 3x3 conv kernels
+def _rel(a, b):
+    return float((a.float() - b.float()).abs().max()) / max(float(b.float().abs().max()), 1e-30)
+
+
+@pytest.mark.parametrize("ci,B", [(64, 4099), (18, 1037), (64, 16)])
+def test_conv3x3_kernels_match_torch_conv2d(ci, B):
+    """r48_conv3x3 (forward and, with the flipped transposed taps, the data gradient) and
+    r48_conv3x3_wgrad vs torch.nn.functional.conv2d (padding 1) in fp32 on the same bf16-rounded
+    inputs: the kernels accumulate in fp32 over bf16 products like the reference computation, so
+    the only differences are summation order and the bf16 rounding of the kernel outputs (forward,
+    data gradient: <= 1e-2 relative to the largest value; weight gradient, fp32 out: <= 2e-3).
+    Ragged board counts (tails of a 16-board tile and of a 4-board staging step) included."""
+    import torch.nn.functional as F
+    from rein48_amd.dqn.conv import board_onehot32, conv3x3, conv3x3_wgrad, pack_conv, pack_conv_dgrad
+    g = torch.Generator(device="cpu").manual_seed(ci * 7 + B)
+    w = (torch.randn(64, ci, 3, 3, generator=g) * 0.1).to(DEV)
+    bias = (torch.randn(64, generator=g) * 0.5).to(DEV)
+    if ci == 18:   # the stem: one-hot planes of exponents, padded to 32 channels
+        boards = torch.randint(0, 18, (B, 16), generator=g, dtype=torch.int8).to(DEV)
+        x = board_onehot32(boards)
+        x_ref = x[:, :, :18].float()
+    else:
+        x = torch.randn(B, 16, ci, generator=g).to(DEV).to(torch.bfloat16)
+        x_ref = x.float()
+    xi = x_ref.permute(0, 2, 1).reshape(B, ci, 4, 4).requires_grad_(True)
+    wb = w.to(torch.bfloat16).float().requires_grad_(True)
+    y_ref = F.conv2d(xi, wb, bias, padding=1)                            # [B, 64, 4, 4]
+    y = conv3x3(x.contiguous(), pack_conv(w, x.shape[2]), bias)          # [B, 16, 64]
+    assert _rel(y, y_ref.permute(0, 2, 3, 1).reshape(B, 16, 64)) < 1e-2
+    gy = torch.randn(B, 16, 64, generator=g).to(DEV).to(torch.bfloat16)
+    y_ref.backward(gy.float().reshape(B, 4, 4, 64).permute(0, 3, 1, 2))
+    dw = conv3x3_wgrad(gy, x.contiguous())[:, :ci]
+    assert _rel(dw, wb.grad) < 2e-3
+    if ci == 64:
+        dx = conv3x3(gy, pack_conv_dgrad(w))
+        assert _rel(dx, xi.grad.reshape(B, ci, 16).permute(0, 2, 1)) < 1e-2
+    # deterministic: fixed-order reductions
+    assert torch.equal(conv3x3_wgrad(gy, x.contiguous())[:, :ci], dw)
+
+
+def test_onehot32_exact():
+    from rein48_amd.dqn.conv import board_onehot32
+    b = np.random.default_rng(5).integers(0, 18, size=(3001, 16)).astype(np.int8)
+    got = board_onehot32(torch.from_numpy(b).to(DEV)).float().cpu().numpy()
+    want = np.zeros((3001, 16, 32), np.float32)
+    want[:, :, :18] = R.onehot(b).reshape(3001, 16, 18)
+    np.testing.assert_array_equal(got, want)
+
+
+def test_resnet_update_custom_conv_matches_structured_gemm():
+    """One training forward/backward of the bf16 ResNet10Q through the hand-written convolutions
+    (r48_conv3x3 / _wgrad) vs through the structured dense GEMMs (hipBLASLt): both are bf16
+    computations of the same fp32 function, so the losses agree to bf16 precision and every
+    weight gradient is close in relative norm."""
+    from rein48_amd.dqn.kernels import board_onehot
+    from rein48_amd.dqn.nets import ResNet10Q
+    torch.manual_seed(10)
+    net = ResNet10Q(dtype=torch.bfloat16).to(DEV).train()
+    with torch.no_grad():
+        net.head.weight.normal_(std=0.05)
+    b = torch.from_numpy(np.random.default_rng(10).integers(0, 12, size=(8200, 16)).astype(np.int8)).to(DEV)
+    x = board_onehot(b, dtype=torch.bfloat16)
+    tgt = torch.randn(8200, 4, device=DEV)
+    grads, losses = [], []
+    for custom in (True, False):
+        net.custom_conv = custom
+        net.zero_grad()
+        for m in net.bns:
+            m.reset_running_stats()
+        loss = torch.nn.functional.smooth_l1_loss(net(x), tgt)
+        loss.backward()
+        losses.append(float(loss.detach()))
+        grads.append([p.grad.detach().float().clone() for k, p in net.named_parameters()
+                      if not (k.endswith(".bias") and (k.startswith("stem") or k.startswith("convs")))])
+    assert abs(losses[0] - losses[1]) <= 1e-2 * abs(losses[1])
+    for ga, gb in zip(*grads):
+        assert float((ga - gb).norm()) <= 5e-2 * float(gb.norm()) + 1e-6
