@@ -160,9 +160,14 @@ def timed_steps(env, plan, W, chunk, world, dev):
     if world > 1:
         dist.barrier()
         torch.cuda.synchronize(dev)          # the barrier's own device work done before t0
+    # the first opening event is recorded before t0: on an idle stream it completes at once, so the
+    # device time it brackets is the launch's own plus the launch latency (conservative), and its
+    # host-side cost does not delay the launch (tools/exp_sync.py: ~1-3 us of a ~95 us region)
+    ev[0][0].record(s)
     t0 = _now()
-    for (a, b), c in zip(ev, plan):
-        a.record(s)
+    for k, ((a, b), c) in enumerate(zip(ev, plan)):
+        if k:
+            a.record(s)
         env.step_n(c, auto_reset=True)
         b.record(s)
     if SYNC_POLL:
@@ -171,8 +176,9 @@ def timed_steps(env, plan, W, chunk, world, dev):
         last = ev[-1][1]
         while not last.query():
             pass
-    torch.cuda.synchronize(dev)
+    ev[-1][1].synchronize()          # the region's last event: every step of every call is done
     t1 = _now()
+    torch.cuda.synchronize(dev)
     skew = 0.0
     if world > 1:
         # one window for the node: from the earliest rank's start to the latest rank's end
@@ -205,13 +211,15 @@ def single_step_hbm(dev, seed, n, launches):
     gbs = n * ALGO_BYTES / (ms * 1e-3) / 1e9
     name = "pmc_k_step_2p%d.json" % (n.bit_length() - 1)
     prof = _load_profile(name)
+    if prof is not None and prof.get("source_sha16") != env_source_sha16():
+        prof = None   # made from other kernel sources than the tree's
     out = {"kernel": "k_step<RANDOM=1,AUTO_RESET=1,REWARD=0>", "boards": n, "launch_ms": ms,
            "env_steps_per_s": n / (ms * 1e-3), "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": gbs / HBM_PEAK_GBS, "frac_of_measured_copy_ceiling": gbs / HBM_MEASURED_GBS,
            "algorithmic_bytes_per_launch": n * ALGO_BYTES,
            "traffic": prof.get("hbm_bytes_per_launch") if prof else None,
-           "traffic_source": ("profiles/r02/%s (committed rocprofv3 FETCH_SIZE + WRITE_SIZE passes, not "
-                              "measured in this run)" % name) if prof else None}
+           "traffic_source": ("profiles/%s/%s (committed rocprofv3 FETCH_SIZE + WRITE_SIZE passes, not "
+                              "measured in this run)" % (PROFILE_ROUND, name)) if prof else None}
     if n * ALGO_BYTES < 256 * 2 ** 20:
         out["bound"] = "mall"
         out["note"] = ("%d MB per step stays in the 256 MiB Infinity Cache: a cache-resident rate, not HBM; the "

@@ -1,9 +1,11 @@
-# Round-2 profiles of the shipped env path: kernel trace + stats of the driver's bench command,
-# then PMC passes (one counter group per run, --pmc only) for k_step_n (K = 20, 2^20 boards, the
-# bench's dispatch) and for k_step (single-step HBM kernel) at 2^20 and 2^26 boards.
+# Profiles of the shipped env path (tools/make_profiles.py turns them into profiles/<round>/):
+# kernel trace + stats of the driver's bench command, then PMC passes (one counter group per
+# run, --pmc only) for k_step_n (K = 20, 2^20 boards, the bench's dispatch) and for k_step
+# (single-step HBM kernel) at 2^20 and 2^26 boards.  usage: bash tools/gpurun/prof_env.sh r03
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/prof; mkdir -p $O
+R=${1:-r03}
+O=gpurun_out/prof_$R; mkdir -p $O
 KS="python3 tools/prof_stepn.py 20 300"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o kt -- python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/kt_bench.json 2> $O/kt.log \
 && timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_LEVEL_WAVES SQ_CYCLES GRBM_GUI_ACTIVE --output-format csv -d $O/sqa -o pmc -- $KS > $O/sqa.log 2>&1 \

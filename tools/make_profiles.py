@@ -1,7 +1,9 @@
-"""Assemble the committed round-2 profile summaries that bench.py reads, from a tools/prof_r02.sh
-run (gpurun_out/prof) and the shipped build's assembly (make asm -> build/r48_env.s).
+"""Assemble the committed profile summaries that bench.py reads, from a tools/gpurun/prof_env.sh
+run (gpurun_out/prof_<round>) and the shipped build's assembly (make asm -> build/r48_env.s).
+Every summary carries source_sha16 (bench.env_source_sha16(): the env kernel sources it was made
+from); bench.py ignores a summary whose hash differs from the tree's.
 
-Writes under profiles/r02/:
+Writes under profiles/<round>/:
   pmc_k_step_n.json      k_step_n (2^20 boards, K = 20 steps per dispatch, the bench's dispatch):
                          SQ counters per dispatch, VALU wave-instructions per board-step
                          (SQ_INSTS_VALU), HBM bytes per dispatch (FETCH_SIZE x 2 + WRITE_SIZE, the
@@ -13,7 +15,7 @@ Writes under profiles/r02/:
   kernel_stats_bench.csv rocprofv3 --kernel-trace --stats of `python3 bench.py --gpus 1 --steps 20
                          --warmup 5` (the driver's command)
   roofline_from_trace.json  the bench roofline recomputed from that trace (median k_step_n dispatch)
-usage: python tools/make_r02_profiles.py [gpurun_out/prof]"""
+usage: python tools/make_profiles.py <round> [gpurun_out/prof_<round>]"""
 import csv
 import json
 import os
@@ -26,7 +28,9 @@ import isa_hist  # noqa: E402
 from pmc_summary import summarize  # noqa: E402
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-OUT = os.path.join(ROOT, "profiles", "r02")
+sys.path.insert(0, ROOT)
+from bench import env_source_sha16  # noqa: E402
+
 SIMDS, CLOCK_GHZ = 1024, 2.4
 BOARDS, K = 1 << 20, 20
 KSTEPN = "k_step_nILb1ELb1ELb0ELi1"
@@ -37,7 +41,10 @@ def hbm_bytes(pm):
 
 
 def main():
-    d = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "gpurun_out", "prof")
+    rnd = sys.argv[1]
+    d = sys.argv[2] if len(sys.argv) > 2 else os.path.join(ROOT, "gpurun_out", "prof_" + rnd)
+    OUT = os.path.join(ROOT, "profiles", rnd)
+    sha = env_source_sha16()
     os.makedirs(OUT, exist_ok=True)
     # ---- k_step_n
     s = summarize("k_step_n", BOARDS // 2, [os.path.join(d, x) for x in ("sqa", "sqb", "stepn_fetch", "stepn_write")])
@@ -49,7 +56,8 @@ def main():
     s.update({
         "kernel": "k_step_n<RANDOM=1,AUTO_RESET=1,REWARD=0,NP=1>",
         "boards": BOARDS, "steps_per_dispatch": K, "board_steps_per_dispatch": bsteps,
-        "source": "rocprofv3 --pmc passes (one counter group each) of tools/prof_stepn.py 20 300, tools/prof_r02.sh",
+        "source": "rocprofv3 --pmc passes (one counter group each) of tools/prof_stepn.py 20 300, tools/gpurun/prof_env.sh",
+        "source_sha16": sha,
         "valu_wave_instr_per_board_step": pm["SQ_INSTS_VALU"] / bsteps,
         "hbm_bytes_per_dispatch": hbm_bytes(pm),
         "algorithmic_bytes_per_dispatch": 34 * BOARDS,
@@ -66,7 +74,8 @@ def main():
         k = summarize("k_step<", n // 2, [os.path.join(d, "k%s_fetch" % tag[2:]), os.path.join(d, "k%s_write" % tag[2:])])
         pk = k["per_dispatch_mean"]
         k.update({"kernel": "k_step<RANDOM=1,AUTO_RESET=1,REWARD=0>", "boards": n,
-                  "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of tools/prof_kstep.py, tools/prof_r02.sh",
+                  "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of tools/prof_kstep.py, tools/gpurun/prof_env.sh",
+                  "source_sha16": sha,
                   "hbm_bytes_per_launch": hbm_bytes(pk), "algorithmic_bytes_per_launch": 34 * n,
                   "traffic_over_algorithmic": hbm_bytes(pk) / (34.0 * n),
                   "correction": "bytes = (2 x FETCH_SIZE + WRITE_SIZE) x 1024 (KiB; gfx950 FETCH_SIZE halving)"})
@@ -82,7 +91,7 @@ def main():
     med = statistics.median(durs)
     cyc_bs = cyc / 128.0
     ach = cyc_bs * bsteps / (med * 1e-9) / 1e9
-    rt = {"kernel": "k_step_n<RANDOM=1,AUTO_RESET=1,REWARD=0,NP=1>", "dispatches": len(durs),
+    rt = {"kernel": "k_step_n<RANDOM=1,AUTO_RESET=1,REWARD=0,NP=1>", "source_sha16": sha, "dispatches": len(durs),
           "median_dispatch_ns": med, "mean_dispatch_ns": sum(durs) / len(durs),
           "board_steps_per_dispatch": bsteps,
           "modelled_issue_cycles_per_board_step": cyc_bs,
@@ -93,8 +102,8 @@ def main():
           "formula": "frac = modelled issue cycles per board-step x 2^20 x 20 / median dispatch time / "
                      "(1024 SIMDs x 2.4 GHz); instr_rate_frac = SQ_INSTS_VALU per dispatch / median dispatch time / "
                      "(1024 SIMDs x 2.4 GHz / 2 cycles per full-rate wave64 instruction)",
-          "trace": "profiles/r02/kernel_stats_bench.csv (rocprofv3 --kernel-trace --stats of python3 bench.py --gpus 1 "
-                   "--steps 20 --warmup 5)"}
+          "trace": "profiles/%s/kernel_stats_bench.csv (rocprofv3 --kernel-trace --stats of python3 bench.py --gpus 1 "
+                   "--steps 20 --warmup 5)" % rnd}
     json.dump(rt, open(os.path.join(OUT, "roofline_from_trace.json"), "w"), indent=1)
     print(json.dumps(rt, indent=1))
 
