@@ -313,6 +313,16 @@ int r48_conv3x3(const void *x, int64_t boards, int32_t cin, const void *wfrag, c
 int64_t r48_conv_wgrad_workspace_floats(int32_t cin);
 int r48_conv3x3_wgrad(const void *dy, const void *x, int64_t boards, int32_t cin, float *workspace, float *dw,
                       void *stream);
+/* The Q head Linear(1024 -> 4) of the update (nets.py: linear(h, head.weight, head.bias, bf16)
+ * .float(), replacing its three hipBLASLt GEMMs): h bf16 [boards][1024] (channels-last cells x
+ * channels), w bf16 [4][1024], bias fp32 [4] (used bf16-rounded); q fp32 [boards][4] holds the
+ * bf16-rounded outputs. Backward: dq fp32 [boards][4] (used bf16-rounded, as the gradient of the bf16
+ * output) -> dh bf16 [boards][1024] and dw fp32 [4 * 1024 + 4] (weight rows, then the bias
+ * gradient; bf16-rounded, fixed-order sums). All pointers 16-byte aligned. */
+int r48_q_head_forward(const void *h, int64_t boards, const void *w, const float *bias, float *q, void *stream);
+int64_t r48_q_head_workspace_floats(void);
+int r48_q_head_backward(const float *dq, const void *h, int64_t boards, const void *w, void *dh, float *workspace,
+                        float *dw, void *stream);
 
 /* Fused ResNet-10 Q-network inference on bf16 MFMA (rein48_amd/dqn/nets.py:ResNet10Q with
  * C = 64, 4 basic blocks, eval-mode BN folded): boards int8[n][16] (16-byte aligned) -> q

@@ -42,6 +42,9 @@ SIGNATURES = {
     "r48_conv3x3": (C.c_int, [_P, _I64, _I32, _P, _P, _P, _P]),
     "r48_conv_wgrad_workspace_floats": (_I64, [_I32]),
     "r48_conv3x3_wgrad": (C.c_int, [_P, _P, _I64, _I32, _P, _P, _P]),
+    "r48_q_head_forward": (C.c_int, [_P, _I64, _P, _P, _P, _P]),
+    "r48_q_head_workspace_floats": (_I64, []),
+    "r48_q_head_backward": (C.c_int, [_P, _P, _I64, _P, _P, _P, _P, _P]),
     "r48_egreedy_actions": (C.c_int, [_P, _I64, C.c_float, _U64, _I64, _U32, _P, _P]),
     "r48_td_target": (C.c_int, [_P, _P, _P, _P, _I64, C.c_float, _P, _P]),
     "r48_replay_create": (C.c_int, [C.POINTER(_P), C.c_int, _I64, _U32, _U64]),

@@ -261,68 +261,6 @@ __device__ __forceinline__ void fwd_conv1(const uint4 *w, const float *b, int la
     }
 }
 
-// conv2 (grouped by weight fragment, as cnn_conv2_heads_grouped) + heads, keeping h2[p][g][s]
-// for the backward and storing each fragment into the h2 image as it is formed; the stream holds
-// fwd_grouped_frag(9), (10) on entry. out: rows 0..3 logits, row 4 value, without the head bias.
-__device__ __forceinline__ void fwd_conv2_heads(const uint4 *w, const float *b, int lane, int h,
-                                                const bf16x8 (&h1)[9][2], WStream &ws, bf16x8 (&h2)[4][2][2],
-                                                f32x16 &out, uint16_t *img, const LaneAddr &la)
-{
-    auto next = [&](int i) { return ws.step(w, fwd_grouped_frag(i + 2 < kFwdGroupedReads ? i + 2 : 0), lane); };
-    f32x16 acc[4];
-    int i = 9;
-    {
-        const f32x16 b2 = load_bias(b + 32, h);
-#pragma unroll
-        for (int u = 0; u < 8; u++, i++) {
-            const bf16x8 wa = next(i);
-            wfence();
-#pragma unroll
-            for (int p = 0; p < 4; p++)
-                acc[p] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, h1[kP2[p][u >> 1]][u & 1], u ? acc[p] : b2, 0, 0,
-                                                                 0);
-            wfence();
-        }
-    }
-#pragma unroll
-    for (int p = 0; p < 4; p++)
-#pragma unroll
-        for (int s = 0; s < 2; s++) {
-            h2[p][0][s] = acc_to_frag_relu(acc[p], s);
-            store_frag(img, la, 64 * p + 16 * s, h2[p][0][s]);
-        }
-    f32x16 o = f32x16{};
-    {
-        const f32x16 b2 = load_bias(b + 64, h);
-#pragma unroll
-        for (int u = 0; u < 8; u++) {
-            const bf16x8 wa = next(i++);
-            wfence();
-#pragma unroll
-            for (int p = 0; p < 4; p++)
-                acc[p] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, h1[kP2[p][u >> 1]][u & 1], u ? acc[p] : b2, 0, 0,
-                                                                 0);
-            wfence();
-            const bf16x8 wh = next(i++);
-            wfence();
-            o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, h2[u >> 1][0][u & 1], o, 0, 0, 0);
-            wfence();
-        }
-    }
-#pragma unroll
-    for (int p = 0; p < 4; p++)
-#pragma unroll
-        for (int s = 0; s < 2; s++) {
-            h2[p][1][s] = acc_to_frag_relu(acc[p], s);
-            store_frag(img, la, 64 * p + 32 + 16 * s, h2[p][1][s]);
-            const bf16x8 wh = next(i++);
-            wfence();
-            o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, h2[p][1][s], o, 0, 0, 0);
-            wfence();
-        }
-    out = o;
-}
-
 // conv2 + heads in chain order (as cnn_conv2_heads: chain c = 2p + g is output position p, half g,
 // its 8 W2 fragments accumulated in one register set; the 2 head MFMAs of chain c issue after chain
 // c + 1), so at most two conv2 accumulators are live and each chain's bf16 pack + ReLU + image store
@@ -453,7 +391,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
         asm volatile("" : "+s"(wofs));
         const uint4 *w = w_lds_base + wofs;
         const float *bl = b_lds_base + wofs;
-        // ---------------- forward (r48_policy.hip k_cnn_forward, fragment-grouped conv2)
+        // ---------------- forward (the math of r48_policy.hip k_cnn_forward; conv2 in chain order)
         uint32_t xp[4];
 #pragma unroll
         for (int q = 0; q < 4; q++) {
@@ -472,15 +410,9 @@ __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
         {
             bf16x8 h1[9][2];
             WStream ws;
-#ifndef R48_TRAIN_GROUPED_FWD
             ws.start(w, fwd_frag(0), fwd_frag(1), lane);
             fwd_conv1(w, bl, lane, h, x, ws, h1, fwd_frag(9), fwd_frag(10));
             fwd_conv2_heads_chain(w, bl, lane, h, h1, ws, h2, out, my, la);
-#else
-            ws.start(w, fwd_grouped_frag(0), fwd_grouped_frag(1), lane);
-            fwd_conv1(w, bl, lane, h, x, ws, h1, fwd_grouped_frag(9), fwd_grouped_frag(10));
-            fwd_conv2_heads(w, bl, lane, h, h1, ws, h2, out, my, la);
-#endif
         }
         // ---------------- loss gradient per row (lane half 0: logits rows 0..3; value in lane + 32)
         // the value (row 4 = lane half 1's first register) into lane half 0: v_permlane32_swap, no LDS

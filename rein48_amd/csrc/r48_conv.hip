@@ -43,8 +43,6 @@ typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 #define R48_LDS __attribute__((address_space(3)))
 
-constexpr int kWaves = 4;
-constexpr int kThreads = 64 * kWaves;
 constexpr int kCout = 64;
 
 // tap t = 3 (dr + 1) + (dc + 1); centre first (all 16 cells: it starts every accumulator)
@@ -92,16 +90,25 @@ int cu_count()
 // x bf16 [boards][16][32 NC], wfrag (tap, O, c) fragments: lane l element j = W[16 O + (l & 15)]
 // [32 c + 8 (l >> 4) + j][tap] (rein48_amd/dqn/conv.py pack_conv), bias fp32 [64] or null,
 // y bf16 [boards][16][64].
+//
+// One workgroup of 8 waves per CU shares one LDS copy of the weights; each wave walks its tiles of
+// 16 boards one grid row at a time. Output row r needs input rows r - 1 .. r + 1, so the row
+// registers of a tile are refilled while it is still being computed: input rows 2 and 3 load under
+// output rows 0 and 1, and the NEXT tile's rows 0 and 1 load under output rows 2 and 3 (their
+// registers are free by then). A wave keeps 1-2 rows (8-16 KB) in flight behind its MFMAs.
+constexpr int kConvWaves = 8;
+
 template <int NC>
-__global__ __launch_bounds__(kThreads, 2) void k_conv3x3(const uint16_t *__restrict__ x, int64_t boards,
-                                                        const uint4 *__restrict__ wfrag,
-                                                        const float *__restrict__ bias, uint16_t *__restrict__ y)
+__global__ __launch_bounds__(64 * kConvWaves, 1) void k_conv3x3(const uint16_t *__restrict__ x, int64_t boards,
+                                                               const uint4 *__restrict__ wfrag,
+                                                               const float *__restrict__ bias,
+                                                               uint16_t *__restrict__ y)
 {
     constexpr int kFrags = 9 * 4 * NC;
     constexpr int kCin = 32 * NC;
     __shared__ uint4 w_lds[kFrags * 64];
     __shared__ __attribute__((aligned(16))) float b_lds[kCout];
-    for (int i = threadIdx.x; i < kFrags * 64; i += kThreads)
+    for (int i = threadIdx.x; i < kFrags * 64; i += 64 * kConvWaves)
         w_lds[i] = wfrag[i];
     if (threadIdx.x < kCout)
         b_lds[threadIdx.x] = bias ? bias[threadIdx.x] : 0.0f;
@@ -109,41 +116,70 @@ __global__ __launch_bounds__(kThreads, 2) void k_conv3x3(const uint16_t *__restr
     const int lane = threadIdx.x & 63, n = lane & 15, g = lane >> 4;
     const int wave = threadIdx.x >> 6;
     const int64_t n_tiles = (boards + 15) / 16;
-    const int64_t stride = (int64_t)gridDim.x * kWaves;
-    for (int64_t tile = (int64_t)blockIdx.x * kWaves + wave; tile < n_tiles; tile += stride) {
-        const int64_t b = tile * 16 + n;
-        const bool live = b < boards;
-        const int64_t bb = live ? b : boards - 1;
-        // all 16 cells of this lane's board, input channels 32 c + 8 g .. + 7 per chunk c
-        uint4 xv[16][NC];
-        const uint16_t *xr = x + bb * 16 * kCin + 8 * g;
+    const int64_t stride = (int64_t)gridDim.x * kConvWaves;
+    int64_t tile = (int64_t)blockIdx.x * kConvWaves + wave;
+    if (tile >= n_tiles)
+        return;
+    // xr[R][col][c]: input cell 4 R + col of this lane's board, channels 32 c + 8 g .. + 7
+    uint4 xr[4][4][NC];
+    auto load_row = [&](int64_t t, int R) {
+        const int64_t b = t * 16 + n;
+        const uint16_t *src = x + ((b < boards ? b : boards - 1) * 16 + 4 * R) * kCin + 8 * g;
 #pragma unroll
-        for (int q = 0; q < 16; q++)
+        for (int col = 0; col < 4; col++)
 #pragma unroll
             for (int c = 0; c < NC; c++)
-                xv[q][c] = *reinterpret_cast<const uint4 *>(xr + q * kCin + 32 * c);
-        uint16_t *yr = y + bb * 16 * kCout + 4 * g;
+                xr[R][col][c] = *reinterpret_cast<const uint4 *>(src + col * kCin + 32 * c);
+    };
+    load_row(tile, 0);
+    load_row(tile, 1);
+    for (; tile < n_tiles; tile += stride) {
+        const int64_t next = tile + stride;
+        const int64_t b = tile * 16 + n;
+        const bool live = b < boards;
+        uint16_t *yr = y + (live ? b : 0) * 16 * kCout + 4 * g;
 #pragma unroll
-        for (int O = 0; O < 4; O++) {
-            const f32x4 b4 = *reinterpret_cast<const f32x4 *>(b_lds + 16 * O + 4 * g);
-            f32x4 acc[16];
+        for (int r = 0; r < 4; r++) {
+            // rows r - 2 of this tile were last read by output row r - 1. Unconditional (the last
+            // tile reloads itself): a load under a branch makes hipcc's counted waits at the join
+            // drain everything in flight
+            load_row(r < 2 ? tile : (next < n_tiles ? next : tile), r < 2 ? r + 2 : r - 2);
+            __builtin_amdgcn_sched_barrier(0);   // issue the row loads here, ahead of this row's MFMAs
 #pragma unroll
-            for (int k = 0; k < 9 * NC; k++) {
-                const int t = kTapOrder[k / NC], c = k % NC;
-                const bf16x8 A = as_frag(w_lds[((t * 4 + O) * NC + c) * 64 + lane]);
+            for (int oh = 0; oh < 2; oh++) {   // two passes of two row tiles: 32 accumulator registers
+                f32x4 acc[4][2];               // [output column][row tile 2 oh + o]
 #pragma unroll
-                for (int p = 0; p < 16; p++) {
-                    if (!in_grid(p, t))
+                for (int k = 0; k < 9 * NC; k++) {
+                    const int t = kTapOrder[k / NC], c = k % NC;
+                    const int dr = t / 3 - 1, dc = t % 3 - 1;
+                    if (r + dr < 0 || r + dr > 3)
                         continue;
-                    acc[p] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, as_frag(xv[p + tap_off(t)][c]),
-                                                                     k == 0 ? b4 : acc[p], 0, 0, 0);
-                }
-            }
-            if (live) {
+                    bf16x8 A[2];
 #pragma unroll
-                for (int p = 0; p < 16; p++)
-                    *reinterpret_cast<uint2 *>(yr + p * kCout + 16 * O) =
-                        make_uint2(pack2(acc[p][0], acc[p][1]), pack2(acc[p][2], acc[p][3]));
+                    for (int o = 0; o < 2; o++)
+                        A[o] = as_frag(w_lds[((t * 4 + 2 * oh + o) * NC + c) * 64 + lane]);
+#pragma unroll
+                    for (int col = 0; col < 4; col++) {
+                        if (col + dc < 0 || col + dc > 3)
+                            continue;
+#pragma unroll
+                        for (int o = 0; o < 2; o++)
+                            acc[col][o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                                A[o], as_frag(xr[r + dr][col + dc][c]),
+                                k == 0 ? *reinterpret_cast<const f32x4 *>(b_lds + 16 * (2 * oh + o) + 4 * g)
+                                       : acc[col][o],
+                                0, 0, 0);
+                    }
+                }
+                if (live) {
+#pragma unroll
+                    for (int col = 0; col < 4; col++)
+#pragma unroll
+                        for (int o = 0; o < 2; o++)
+                            *reinterpret_cast<uint2 *>(yr + (4 * r + col) * kCout + 16 * (2 * oh + o)) =
+                                make_uint2(pack2(acc[col][o][0], acc[col][o][1]),
+                                           pack2(acc[col][o][2], acc[col][o][3]));
+                }
             }
         }
     }
@@ -151,17 +187,30 @@ __global__ __launch_bounds__(kThreads, 2) void k_conv3x3(const uint16_t *__restr
 
 // --------------------------------------------------------------------------------- wgrad
 // Per step a workgroup stages kStepRows rows (kStepRows / 16 boards) of dy [rows][64] and x
-// [rows][CIN] into LDS images (row-major, the 16-byte chunk index XOR-ed with the row so the
-// staging stores are conflict free), plus one zero row per image. The global loads of step s + 2
-// are issued while step s computes (a two-step register ring), so a workgroup keeps ~32 KB in flight.
+// [rows][CIN] into LDS images by LDS-DMA (global_load_lds_dwordx4: no staging registers): row-major,
+// the 16-byte chunk index XOR-ed with swz(row) (applied to the per-lane SOURCE address, the LDS side
+// of one DMA is lane-linear). A ring of kRing buffers keeps steps s + 1 .. s + 5 in flight while
+// step s computes (~64-80 KB per CU), waited for with a counted vmcnt and a raw barrier. The x image
+// has a zero band: rows kStepRows + 32 ks, one per k-step, so that every transposed-read address of
+// k-step ks is the k-step-0 address plus the constant 32 ks rows (an immediate offset) -- also for
+// the out-of-grid taps, which read the zero row.
 constexpr int kStepRows = 64;
 constexpr int kKSteps = kStepRows / 32;
+constexpr int kZeroRow = kStepRows;                              // zero band: kZeroRow + 32 ks
+constexpr int kXRows = kStepRows + 32 * (kKSteps - 1) + 1;
+constexpr int kRing = 6;                                          // LDS buffers: 5 steps ahead
+constexpr int kRedGroup = 16;                                     // records per first-pass group
+
+// chunk swizzle of image row `row`: XOR with row & 7 spreads a transposed read's 4 consecutive rows
+// over the bank row; XOR with 4 when row & 8 keeps the rows 8 apart (the lane groups g = 0, 1 of
+// one 32-lane half) off each other's banks
+__host__ __device__ constexpr int swz(int row) { return (row & 7) ^ ((row & 8) >> 1); }
 
 template <int COLS>
 __device__ __forceinline__ int wimg(int row, int col)
 {
     constexpr int kChunks = COLS / 8;
-    return row * COLS + ((((col >> 3) ^ row) & (kChunks - 1)) << 3) + (col & 7);
+    return row * COLS + ((((col >> 3) ^ swz(row)) & (kChunks - 1)) << 3) + (col & 7);
 }
 
 __device__ __forceinline__ bf16x8 tr_pair(const uint16_t *p0, const uint16_t *p1)
@@ -180,119 +229,153 @@ __device__ __forceinline__ void acc16(f32x4 &acc, const bf16x8 &a, const bf16x8 
     asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
 }
 
-// partial record per workgroup: [9 taps][64 co][CIN ci] fp32
+// One DMA of 64 x 16 bytes: rows [row0, row0 + 512 / COLS) of a [rows][COLS] bf16 tensor into the
+// LDS image rows starting at img_row (wave-uniform), swizzled; source rows clamped to `last`.
+template <int COLS>
+__device__ __forceinline__ void dma_rows(const uint16_t *src, int64_t row0, int64_t last, uint16_t *img,
+                                         int img_row, int lane)
+{
+    constexpr int kChunks = COLS / 8, kRows = 64 / kChunks;
+    const int r = lane / kChunks, phys = lane % kChunks;
+    const int chunk = (phys ^ swz(img_row + r)) & (kChunks - 1);
+    const int64_t gr = row0 + r < last ? row0 + r : last;
+    // inline asm: the builtin makes hipcc wait vmcnt(0) before every later ds_read of the array
+    // (it cannot tell the ring buffers apart), which would drain the ring each step
+    const uint32_t dst = __builtin_amdgcn_readfirstlane(
+        (uint32_t)reinterpret_cast<uintptr_t>((R48_LDS void *)(img + img_row * COLS)));   // wave-uniform
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
+                 "s_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(src + gr * COLS + 8 * chunk), "s"(dst)
+                 : "memory");
+    static_assert(kRows * kChunks == 64, "one DMA = 64 chunks");
+}
+
+// partial record per workgroup: [9 taps][64 co][CIN ci] fp32. Eight waves (two per SIMD, so one
+// wave's DMA issue and barrier waits run under the other's MFMAs): wave w owns input-channel tile
+// w % (CIN / 16) and output tiles of its share, for every tap.
+constexpr int kWgWaves = 8;
+
 template <int CIN>
-__global__ __launch_bounds__(kThreads, 1) void k_conv_wgrad(const uint16_t *__restrict__ dy,
+__global__ __launch_bounds__(64 * kWgWaves, 1) void k_conv_wgrad(const uint16_t *__restrict__ dy,
                                                            const uint16_t *__restrict__ x, int64_t boards,
                                                            float *__restrict__ partials)
 {
+    constexpr int kThr = 64 * kWgWaves;
     constexpr int NCT = CIN / 16;                                // input-channel tiles of 16
-    constexpr int kCoT = NCT >= kWaves ? 4 : 4 * NCT / kWaves;   // output tiles per wave (4 or 2)
-    constexpr int kDyImg = (kStepRows + 1) * kCout, kXImg = (kStepRows + 1) * CIN;
+    constexpr int kCoT = 4 * NCT / kWgWaves;                     // output tiles per wave (2 or 1)
+    static_assert(kCoT >= 1 && kCoT * kWgWaves == 4 * NCT, "wave split");
+    constexpr int kDyImg = kStepRows * kCout, kXImg = kXRows * CIN;
     constexpr int kBuf = kDyImg + kXImg;
-    constexpr int kDyChunks = kStepRows * kCout / 8, kXChunks = kStepRows * CIN / 8;
-    constexpr int kPerThread = (kDyChunks + kXChunks) / kThreads;   // 16-byte chunks per thread per step
-    static_assert((kDyChunks + kXChunks) % kThreads == 0 && kDyChunks % kThreads == 0, "staging split");
-    __shared__ __attribute__((aligned(16))) uint16_t lds[2 * kBuf];
+    constexpr int kDyRowsPerDma = 512 / kCout, kXRowsPerDma = 512 / CIN;
+    constexpr int kDyDmas = kStepRows / kDyRowsPerDma, kXDmas = kStepRows / kXRowsPerDma;   // per step
+    constexpr int kDmas = kDyDmas + kXDmas;
+    static_assert(kDyDmas * kDyRowsPerDma == kStepRows && kXDmas * kXRowsPerDma == kStepRows, "staging split");
+    __shared__ __attribute__((aligned(16))) uint16_t lds[kRing * kBuf];   // the only LDS object
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int i16 = lane & 15, g = lane >> 4;
-    const int ct = NCT >= kWaves ? wave : wave % NCT;            // input-channel tile of this wave
-    const int cot0 = NCT >= kWaves ? 0 : (wave / NCT) * kCoT;    // first output tile of this wave
-    for (int i = threadIdx.x; i < kCout; i += kThreads) {        // zero rows (never overwritten)
-        lds[kStepRows * kCout + i] = 0;
-        lds[kBuf + kStepRows * kCout + i] = 0;
+    const int ct = wave % NCT;                                   // input-channel tile of this wave
+    const int cot0 = (wave / NCT) * kCoT;                        // first output tile of this wave
+    // DMA d = wave, wave + 8, ... of a step (dy pieces first): this wave's count per step
+    const int my_dmas = (kDmas - wave + kWgWaves - 1) / kWgWaves;
+    for (int i = threadIdx.x; i < kRing * kKSteps * CIN; i += kThr) {   // zero bands (never overwritten)
+        const int buf = i / (kKSteps * CIN), k = i % (kKSteps * CIN);
+        lds[buf * kBuf + kDyImg + (kZeroRow + 32 * (k / CIN)) * CIN + k % CIN] = 0;
     }
-    for (int i = threadIdx.x; i < CIN; i += kThreads) {
-        lds[kDyImg + kStepRows * CIN + i] = 0;
-        lds[kBuf + kDyImg + kStepRows * CIN + i] = 0;
-    }
-    // transposed-read addresses. A (dy^T, lanes = co) of k-step ks: rows 32 ks + 8g + 4u + q,
-    // columns 16 cot + 4p (lane 4q + p of a 16-lane group addresses row q of the group's 4-row
-    // block). B (x^T shifted by tap t, lanes = ci): row + off(t) when that cell is in the grid,
-    // else the zero row.
+    // transposed-read addresses of k-step 0 (k-step ks adds 32 ks rows). A (dy^T, lanes = co):
+    // rows 8g + 4u + q, columns 16 cot + 4p (lane 4q + p of a 16-lane group addresses row q of the
+    // group's 4-row block). B (x^T shifted by tap t, lanes = ci): row + off(t) when that cell is in
+    // the grid, else the zero row.
     const int q = i16 >> 2, p4 = i16 & 3;
-    int a_off[kKSteps][kCoT][2], b_off[kKSteps][9][2];
+    int a_off[kCoT][2], b_off[9][2];
 #pragma unroll
-    for (int ks = 0; ks < kKSteps; ks++)
+    for (int u = 0; u < 2; u++) {
+        const int row = 8 * g + 4 * u + q;
 #pragma unroll
-        for (int u = 0; u < 2; u++) {
-            const int row = 32 * ks + 8 * g + 4 * u + q;
+        for (int j = 0; j < kCoT; j++)
+            a_off[j][u] = wimg<kCout>(row, 16 * (cot0 + j) + 4 * p4);
 #pragma unroll
-            for (int j = 0; j < kCoT; j++)
-                a_off[ks][j][u] = wimg<kCout>(row, 16 * (cot0 + j) + 4 * p4);
-#pragma unroll
-            for (int t = 0; t < 9; t++) {
-                const int src = in_grid(row & 15, t) ? row + tap_off(t) : kStepRows;
-                b_off[ks][t][u] = kDyImg + wimg<CIN>(src, 16 * ct + 4 * p4);
-            }
+        for (int t = 0; t < 9; t++) {
+            const int src = in_grid(row & 15, t) ? row + tap_off(t) : kZeroRow;
+            b_off[t][u] = kDyImg + wimg<CIN>(src, 16 * ct + 4 * p4);
         }
+    }
     f32x4 acc[9][kCoT];
 #pragma unroll
     for (int t = 0; t < 9; t++)
 #pragma unroll
         for (int j = 0; j < kCoT; j++)
             acc[t][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // this workgroup's steps: a contiguous range
-    const int64_t rows_total = boards * 16;
+    // this workgroup's steps: blockIdx.x + i * gridDim.x (the grid sweeps the tensors in order)
+    const int64_t rows_total = boards * 16, last = rows_total - 1;
     const int64_t steps_total = (rows_total + kStepRows - 1) / kStepRows;
-    const int64_t per = (steps_total + gridDim.x - 1) / gridDim.x;
-    const int64_t s0 = (int64_t)blockIdx.x * per, s1 = s0 + per < steps_total ? s0 + per : steps_total;
-    // chunk c of a step: c < kDyChunks -> dy row c / 8, 16-byte column c % 8; else x
-    auto load = [&](int64_t step, uint4 (&v)[kPerThread]) {
-#pragma unroll
-        for (int k = 0; k < kPerThread; k++) {
-            const int c = threadIdx.x + k * kThreads;
-            const bool is_dy = c < kDyChunks;
-            const int cc = is_dy ? c : c - kDyChunks, cols = is_dy ? kCout : CIN;
-            const int r = cc / (cols / 8), ch = cc % (cols / 8);
-            const int64_t row = step * kStepRows + r;
-            v[k] = make_uint4(0, 0, 0, 0);
-            if (step < s1 && row < rows_total)
-                v[k] = *reinterpret_cast<const uint4 *>((is_dy ? dy : x) + row * cols + 8 * ch);
-        }
-    };
-    auto store = [&](const uint4 (&v)[kPerThread], int buf) {
+    const int64_t n_my = blockIdx.x < steps_total ? (steps_total - blockIdx.x + gridDim.x - 1) / gridDim.x : 0;
+    // stage this workgroup's step i into ring buffer `buf`: this wave issues its my_dmas DMAs.
+    // Steps past the end are staged too (clamped rows, a buffer nobody reads), so every step
+    // issues the same count and the counted wait below stays exact.
+    auto stage = [&](int64_t i, int buf) {
         uint16_t *dimg = lds + buf * kBuf, *ximg = dimg + kDyImg;
+        const int64_t row0 = ((int64_t)blockIdx.x + i * gridDim.x) * kStepRows;
 #pragma unroll
-        for (int k = 0; k < kPerThread; k++) {
-            const int c = threadIdx.x + k * kThreads;
-            if (c < kDyChunks)
-                *reinterpret_cast<uint4 *>(dimg + wimg<kCout>(c / (kCout / 8), 8 * (c % (kCout / 8)))) = v[k];
-            else
-                *reinterpret_cast<uint4 *>(ximg + wimg<CIN>((c - kDyChunks) / (CIN / 8),
-                                                            8 * ((c - kDyChunks) % (CIN / 8)))) = v[k];
+        for (int k = 0; k < (kDmas + kWgWaves - 1) / kWgWaves; k++) {
+            const int d = wave + k * kWgWaves;
+            if (d < kDyDmas)
+                dma_rows<kCout>(dy, row0 + d * kDyRowsPerDma, last, dimg, d * kDyRowsPerDma, lane);
+            else if (d < kDmas)
+                dma_rows<CIN>(x, row0 + (d - kDyDmas) * kXRowsPerDma, last, ximg, (d - kDyDmas) * kXRowsPerDma,
+                              lane);
         }
     };
-    uint4 ra[kPerThread], rb[kPerThread];
-    load(s0, ra);
-    load(s0 + 1, rb);
-    store(ra, 0);
-    __syncthreads();
-    for (int64_t s = s0; s < s1; s++) {
-        const int buf = (int)((s - s0) & 1);
-        // ring: rb holds step s + 1; ra is free -> step s + 2
-        load(s + 2, ra);
+    auto compute = [&](int buf) {
         const uint16_t *img = lds + buf * kBuf;
 #pragma unroll
         for (int ks = 0; ks < kKSteps; ks++) {
             bf16x8 A[kCoT];
 #pragma unroll
             for (int j = 0; j < kCoT; j++)
-                A[j] = tr_pair(img + a_off[ks][j][0], img + a_off[ks][j][1]);
+                A[j] = tr_pair(img + a_off[j][0] + 32 * ks * kCout, img + a_off[j][1] + 32 * ks * kCout);
 #pragma unroll
             for (int t = 0; t < 9; t++) {
-                const bf16x8 B = tr_pair(img + b_off[ks][t][0], img + b_off[ks][t][1]);
+                const bf16x8 B = tr_pair(img + b_off[t][0] + 32 * ks * CIN, img + b_off[t][1] + 32 * ks * CIN);
 #pragma unroll
                 for (int j = 0; j < kCoT; j++)
                     acc16(acc[t][j], A[j], B);
             }
         }
-        store(rb, buf ^ 1);      // step s + 1 into the other buffer (its readers passed the last barrier)
-        __syncthreads();
+    };
+    __syncthreads();                                              // zero bands written
 #pragma unroll
-        for (int k = 0; k < kPerThread; k++)
-            rb[k] = ra[k];
+    for (int i = 0; i < kRing - 1; i++)
+        stage(i, i);
+    for (int64_t i = 0; i < n_my; i++) {
+        const int64_t s = (int64_t)blockIdx.x + i * gridDim.x;
+        const int buf = (int)(i % kRing);
+        // this wave's DMAs of step s done (steps s + 1, s + 2 may stay in flight), then the barrier
+        // that orders them for every reader -- and that every wave passes only after its reads of
+        // step s - 1, whose buffer is restaged below
+        if (my_dmas == 2)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"((kRing - 2) * 2) : "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kRing - 2) : "memory");
+        static_assert(kDmas <= 2 * kWgWaves && kDmas > kWgWaves, "one or two DMAs per wave and step");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (s == steps_total - 1 && rows_total - s * kStepRows < kStepRows) {
+            // the ragged last step: its rows past the end were staged from the clamped last row
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const int real = (int)(rows_total - s * kStepRows);
+            uint16_t *dimg = lds + buf * kBuf, *ximg = dimg + kDyImg;
+            for (int i = threadIdx.x; i < (kStepRows - real) * kCout; i += kThr)
+                dimg[real * kCout + i] = 0;
+            for (int i = threadIdx.x; i < (kStepRows - real) * CIN; i += kThr)
+                ximg[real * CIN + i] = 0;
+            __syncthreads();
+        }
+        stage(i + kRing - 1, (buf + kRing - 1) % kRing);          // buffer of step i - 1
+        compute(buf);
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");              // no DMA outlives the kernel
     // record: D[m = co 16][n = ci 16], lane l: column i16 (ci), rows 4g + i (co). 24 wait states
     // between the last accumulating MFMA and the AGPR reads
     asm volatile("s_nop 15\n\ts_nop 7" ::: "memory");
@@ -306,19 +389,274 @@ __global__ __launch_bounds__(kThreads, 1) void k_conv_wgrad(const uint16_t *__re
                 rec[(t * kCout + 16 * (cot0 + j) + 4 * g + i) * CIN + 16 * ct + i16] = acc[t][j][i];
 }
 
-// out[co][ci][t] (torch's [co, ci, 3, 3] layout) = fixed-order sum over the records [t][co][ci]
+// Fixed-order sum of the n_rec records [t][co][ci] in two passes (deterministic): pass 1 sums
+// groups of kRedGroup consecutive records (one lane per group and 4 record entries), pass 2 sums
+// the groups in order and writes torch's [co][ci][3][3] layout.
 template <int CIN>
-__global__ __launch_bounds__(256) void k_conv_wgrad_reduce(const float *__restrict__ partials, int n_rec,
-                                                          float *__restrict__ out)
+__global__ __launch_bounds__(256) void k_conv_wgrad_reduce1(const float4 *__restrict__ partials, int n_rec,
+                                                           float4 *__restrict__ groups)
 {
-    const int k = blockIdx.x * 256 + threadIdx.x;      // record index: (t * 64 + co) * CIN + ci
-    if (k >= 9 * kCout * CIN)
+    constexpr int kQ = 9 * kCout * CIN / 4;                       // float4 entries per record
+    const int n_grp = (n_rec + kRedGroup - 1) / kRedGroup;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= kQ * n_grp)
         return;
-    float s = 0.f;
-    for (int r = 0; r < n_rec; r++)
-        s += partials[(int64_t)r * 9 * kCout * CIN + k];
-    const int t = k / (kCout * CIN), co = (k / CIN) % kCout, ci = k % CIN;
-    out[(co * CIN + ci) * 9 + t] = s;
+    const int grp = i / kQ, k = i % kQ;
+    const int r0 = grp * kRedGroup, r1 = r0 + kRedGroup < n_rec ? r0 + kRedGroup : n_rec;
+    float4 v[kRedGroup];
+#pragma unroll
+    for (int r = 0; r < kRedGroup; r++)
+        v[r] = r0 + r < r1 ? partials[(int64_t)(r0 + r) * kQ + k] : make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 s = v[0];
+#pragma unroll
+    for (int r = 1; r < kRedGroup; r++) {
+        s.x += v[r].x;
+        s.y += v[r].y;
+        s.z += v[r].z;
+        s.w += v[r].w;
+    }
+    groups[(int64_t)grp * kQ + k] = s;
+}
+
+template <int CIN>
+__global__ __launch_bounds__(256) void k_conv_wgrad_reduce2(const float4 *__restrict__ groups, int n_grp,
+                                                           float *__restrict__ out)
+{
+    constexpr int kQ = 9 * kCout * CIN / 4;
+    const int k = blockIdx.x * 256 + threadIdx.x;                // float4 entry: (t * 64 + co) * CIN + 4 k'
+    if (k >= kQ)
+        return;
+    float4 s = groups[k];
+    for (int r = 1; r < n_grp; r++) {
+        const float4 v = groups[(int64_t)r * kQ + k];
+        s.x += v.x;
+        s.y += v.y;
+        s.z += v.z;
+        s.w += v.w;
+    }
+    const int e = 4 * k, t = e / (kCout * CIN), co = (e / CIN) % kCout, ci = e % CIN;
+    float *o = out + (co * CIN + ci) * 9 + t;
+    o[0] = s.x;
+    o[9] = s.y;
+    o[18] = s.z;
+    o[27] = s.w;
+}
+
+// --------------------------------------------------------------------------------- Q head
+// q[b][a] = bf16(sum_k h[b][k] W[a][k] + bias[a]) for the 4 actions, k < 1024 = 16 cells x 64
+// channels (nets.py: linear(h, head.weight, head.bias, bf16).float()). A wave takes one board at a
+// time, lane l its k = 16 l .. 16 l + 15 (one 32-byte piece of the 2 KiB row: the wave reads the
+// row in full lines); W stays in 32 registers; the 4 dot products are summed across the wave.
+// kHeadUnroll boards per iteration keep 8 KiB per wave in flight. HBM-bound: 2 KiB per board.
+constexpr int kHeadK = 1024, kHeadWaves = 8, kHeadUnroll = 4;
+
+__device__ __forceinline__ void unpack16(const uint4 (&v)[2], float (&f)[16])
+{
+    const uint32_t w[8] = {v[0].x, v[0].y, v[0].z, v[0].w, v[1].x, v[1].y, v[1].z, v[1].w};
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        f[2 * i] = __uint_as_float(w[i] << 16);
+        f[2 * i + 1] = __uint_as_float(w[i] & 0xFFFF0000u);
+    }
+}
+
+__device__ __forceinline__ float bf16_round(float v)   // round to nearest even, as a float
+{
+    return (float)(__bf16)v;
+}
+
+__device__ __forceinline__ float wave_sum(float v)
+{
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1)
+        v += __shfl_xor(v, m);
+    return v;
+}
+
+__global__ __launch_bounds__(64 * kHeadWaves) void k_q_head_fwd(const uint16_t *__restrict__ h, int64_t boards,
+                                                             const uint16_t *__restrict__ w,
+                                                             const float *__restrict__ bias, float *__restrict__ q)
+{
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = (int64_t)blockIdx.x * kHeadWaves + (threadIdx.x >> 6);
+    const int64_t n_waves = (int64_t)gridDim.x * kHeadWaves;
+    float wf[4][16];
+#pragma unroll
+    for (int a = 0; a < 4; a++) {
+        uint4 v[2];
+        v[0] = *reinterpret_cast<const uint4 *>(w + a * kHeadK + 16 * lane);
+        v[1] = *reinterpret_cast<const uint4 *>(w + a * kHeadK + 16 * lane + 8);
+        unpack16(v, wf[a]);
+    }
+    float b4[4];
+#pragma unroll
+    for (int a = 0; a < 4; a++)
+        b4[a] = bf16_round(bias[a]);
+    for (int64_t b0 = wave * kHeadUnroll; b0 < boards; b0 += n_waves * kHeadUnroll) {
+        uint4 v[kHeadUnroll][2];
+#pragma unroll
+        for (int u = 0; u < kHeadUnroll; u++) {
+            const int64_t b = b0 + u < boards ? b0 + u : boards - 1;
+            v[u][0] = *reinterpret_cast<const uint4 *>(h + b * kHeadK + 16 * lane);
+            v[u][1] = *reinterpret_cast<const uint4 *>(h + b * kHeadK + 16 * lane + 8);
+        }
+#pragma unroll
+        for (int u = 0; u < kHeadUnroll; u++) {
+            float f[16];
+            unpack16(v[u], f);
+            float s[4];
+#pragma unroll
+            for (int a = 0; a < 4; a++) {
+                s[a] = 0.f;
+#pragma unroll
+                for (int i = 0; i < 16; i++)
+                    s[a] = __builtin_fmaf(f[i], wf[a][i], s[a]);
+                s[a] = wave_sum(s[a]);
+            }
+            if (lane == 0 && b0 + u < boards)
+                *reinterpret_cast<float4 *>(q + 4 * (b0 + u)) =
+                    make_float4(bf16_round(s[0] + b4[0]), bf16_round(s[1] + b4[1]), bf16_round(s[2] + b4[2]),
+                                bf16_round(s[3] + b4[3]));
+        }
+    }
+}
+
+// Backward of the head for one board per wave step: g = bf16(dq[b]) (the bf16 output's gradient);
+// dh[b][k] = bf16(sum_a g[a] W[a][k]); the weight gradient sum_b g[a] h[b][k] and the bias gradient
+// sum_b g[a] accumulate per lane in fp32 (lane l owns k = 16 l .. + 15 of all 4 rows), the waves of a
+// workgroup are summed through LDS in a fixed order, and each workgroup writes one record of
+// kHeadK * 4 + 4 floats (summed by k_records_reduce*: deterministic).
+constexpr int kHeadRec = 4 * kHeadK + 4;
+
+__global__ __launch_bounds__(64 * kHeadWaves) void k_q_head_bwd(const float *__restrict__ dq,
+                                                             const uint16_t *__restrict__ h, int64_t boards,
+                                                             const uint16_t *__restrict__ w,
+                                                             uint16_t *__restrict__ dh, float *__restrict__ records)
+{
+    __shared__ float red[kHeadWaves][kHeadRec];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t wave = (int64_t)blockIdx.x * kHeadWaves + wv;
+    const int64_t n_waves = (int64_t)gridDim.x * kHeadWaves;
+    float wf[4][16];
+#pragma unroll
+    for (int a = 0; a < 4; a++) {
+        uint4 v[2];
+        v[0] = *reinterpret_cast<const uint4 *>(w + a * kHeadK + 16 * lane);
+        v[1] = *reinterpret_cast<const uint4 *>(w + a * kHeadK + 16 * lane + 8);
+        unpack16(v, wf[a]);
+    }
+    float gw[4][16], gb[4];
+#pragma unroll
+    for (int a = 0; a < 4; a++) {
+        gb[a] = 0.f;
+#pragma unroll
+        for (int i = 0; i < 16; i++)
+            gw[a][i] = 0.f;
+    }
+    for (int64_t b0 = wave * kHeadUnroll; b0 < boards; b0 += n_waves * kHeadUnroll) {
+        uint4 v[kHeadUnroll][2];
+        float4 g4[kHeadUnroll];
+#pragma unroll
+        for (int u = 0; u < kHeadUnroll; u++) {
+            const int64_t b = b0 + u < boards ? b0 + u : boards - 1;
+            v[u][0] = *reinterpret_cast<const uint4 *>(h + b * kHeadK + 16 * lane);
+            v[u][1] = *reinterpret_cast<const uint4 *>(h + b * kHeadK + 16 * lane + 8);
+            g4[u] = *reinterpret_cast<const float4 *>(dq + 4 * b);
+        }
+#pragma unroll
+        for (int u = 0; u < kHeadUnroll; u++) {
+            const bool live = b0 + u < boards;
+            const float g[4] = {live ? bf16_round(g4[u].x) : 0.f, live ? bf16_round(g4[u].y) : 0.f,
+                                live ? bf16_round(g4[u].z) : 0.f, live ? bf16_round(g4[u].w) : 0.f};
+            float f[16];
+            unpack16(v[u], f);
+            uint32_t o[8];
+#pragma unroll
+            for (int i = 0; i < 16; i += 2) {
+                float d0 = 0.f, d1 = 0.f;
+#pragma unroll
+                for (int a = 0; a < 4; a++) {
+                    d0 = __builtin_fmaf(g[a], wf[a][i], d0);
+                    d1 = __builtin_fmaf(g[a], wf[a][i + 1], d1);
+                }
+                o[i / 2] = pack2(d0, d1);
+            }
+#pragma unroll
+            for (int a = 0; a < 4; a++) {
+                gb[a] += g[a];
+#pragma unroll
+                for (int i = 0; i < 16; i++)
+                    gw[a][i] = __builtin_fmaf(g[a], f[i], gw[a][i]);
+            }
+            if (live) {
+                uint16_t *dst = dh + (b0 + u) * kHeadK + 16 * lane;
+                *reinterpret_cast<uint4 *>(dst) = make_uint4(o[0], o[1], o[2], o[3]);
+                *reinterpret_cast<uint4 *>(dst + 8) = make_uint4(o[4], o[5], o[6], o[7]);
+            }
+        }
+    }
+#pragma unroll
+    for (int a = 0; a < 4; a++)
+#pragma unroll
+        for (int i = 0; i < 16; i++)
+            red[wv][a * kHeadK + 16 * lane + i] = gw[a][i];
+    if (lane < 4)
+        red[wv][4 * kHeadK + lane] = gb[lane];
+    __syncthreads();
+    float *rec = records + (int64_t)blockIdx.x * kHeadRec;
+    for (int i = threadIdx.x; i < kHeadRec; i += 64 * kHeadWaves) {
+        float t = red[0][i];
+#pragma unroll
+        for (int k = 1; k < kHeadWaves; k++)
+            t += red[k][i];
+        rec[i] = t;
+    }
+}
+
+// fixed-order sums of n_rec records of `len` floats (len % 4 == 0): pass 1 sums groups of
+// kRedGroup consecutive records, pass 2 the groups in order, the result rounded through bf16 when
+// round_bf16 (the bf16 parameter-gradient contract of nets.py's linear)
+__global__ __launch_bounds__(256) void k_records_reduce1(const float4 *__restrict__ recs, int n_rec, int len4,
+                                                        float4 *__restrict__ groups)
+{
+    const int n_grp = (n_rec + kRedGroup - 1) / kRedGroup;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= len4 * n_grp)
+        return;
+    const int grp = i / len4, k = i % len4;
+    const int r0 = grp * kRedGroup, r1 = r0 + kRedGroup < n_rec ? r0 + kRedGroup : n_rec;
+    float4 v[kRedGroup];
+#pragma unroll
+    for (int r = 0; r < kRedGroup; r++)
+        v[r] = r0 + r < r1 ? recs[(int64_t)(r0 + r) * len4 + k] : make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 s = v[0];
+#pragma unroll
+    for (int r = 1; r < kRedGroup; r++) {
+        s.x += v[r].x;
+        s.y += v[r].y;
+        s.z += v[r].z;
+        s.w += v[r].w;
+    }
+    groups[(int64_t)grp * len4 + k] = s;
+}
+
+__global__ __launch_bounds__(256) void k_records_reduce2(const float4 *__restrict__ groups, int n_grp, int len4,
+                                                        int round_bf16, float4 *__restrict__ out)
+{
+    const int k = blockIdx.x * 256 + threadIdx.x;
+    if (k >= len4)
+        return;
+    float4 s = groups[k];
+    for (int r = 1; r < n_grp; r++) {
+        const float4 v = groups[(int64_t)r * len4 + k];
+        s.x += v.x;
+        s.y += v.y;
+        s.z += v.z;
+        s.w += v.w;
+    }
+    if (round_bf16)
+        s = make_float4(bf16_round(s.x), bf16_round(s.y), bf16_round(s.z), bf16_round(s.w));
+    out[k] = s;
 }
 
 // one lane per (board, cell): the one-hot of the exponent over 32 bf16 planes (e = 0..17, planes
@@ -364,20 +702,21 @@ int r48_conv3x3(const void *x, int64_t boards, int32_t cin, const void *wfrag, c
          reinterpret_cast<uintptr_t>(bias)) & 15u)
         return fail(R48_EINVAL, "r48_conv3x3: x, wfrag, bias and y must be 16-byte aligned");
     const int64_t tiles = (boards + 15) / 16;
-    const int64_t want = (tiles + kWaves - 1) / kWaves;
-    const int grid = (int)(want < 2 * cu_count() ? want : 2 * cu_count());
+    const int64_t want = (tiles + kConvWaves - 1) / kConvWaves;
+    const int grid = (int)(want < cu_count() ? want : cu_count());
     if (cin == 64)
-        hipLaunchKernelGGL(k_conv3x3<2>, dim3(grid), dim3(kThreads), 0, (hipStream_t)stream, (const uint16_t *)x,
-                           boards, (const uint4 *)wfrag, bias, (uint16_t *)y);
+        hipLaunchKernelGGL(k_conv3x3<2>, dim3(grid), dim3(64 * kConvWaves), 0, (hipStream_t)stream,
+                           (const uint16_t *)x, boards, (const uint4 *)wfrag, bias, (uint16_t *)y);
     else
-        hipLaunchKernelGGL(k_conv3x3<1>, dim3(grid), dim3(kThreads), 0, (hipStream_t)stream, (const uint16_t *)x,
-                           boards, (const uint4 *)wfrag, bias, (uint16_t *)y);
+        hipLaunchKernelGGL(k_conv3x3<1>, dim3(grid), dim3(64 * kConvWaves), 0, (hipStream_t)stream,
+                           (const uint16_t *)x, boards, (const uint4 *)wfrag, bias, (uint16_t *)y);
     return launched("k_conv3x3");
 }
 
 int64_t r48_conv_wgrad_workspace_floats(int32_t cin)
 {
-    return (int64_t)cu_count() * 9 * kCout * (cin == 32 ? 32 : 64);
+    const int64_t recs = cu_count();
+    return (recs + (recs + kRedGroup - 1) / kRedGroup) * 9 * kCout * (cin == 32 ? 32 : 64);
 }
 
 int r48_conv3x3_wgrad(const void *dy, const void *x, int64_t boards, int32_t cin, float *workspace, float *dw,
@@ -385,22 +724,71 @@ int r48_conv3x3_wgrad(const void *dy, const void *x, int64_t boards, int32_t cin
 {
     if (!dy || !x || !workspace || !dw || boards < 1 || (cin != 32 && cin != 64))
         return fail(R48_EINVAL, "r48_conv3x3_wgrad: NULL argument, boards < 1 or cin not 32/64");
-    if ((reinterpret_cast<uintptr_t>(dy) | reinterpret_cast<uintptr_t>(x)) & 15u)
-        return fail(R48_EINVAL, "r48_conv3x3_wgrad: dy and x must be 16-byte aligned");
+    if ((reinterpret_cast<uintptr_t>(dy) | reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(workspace)) &
+        15u)
+        return fail(R48_EINVAL, "r48_conv3x3_wgrad: dy, x and workspace must be 16-byte aligned");
     const int grid = cu_count();
-    const int n_out = 9 * kCout * cin;
+    const int n_grp = (grid + kRedGroup - 1) / kRedGroup;
+    const int64_t rec = (int64_t)9 * kCout * cin;
+    const int q = (int)(rec / 4);
+    hipStream_t s = (hipStream_t)stream;
+    float4 *groups = reinterpret_cast<float4 *>(workspace + grid * rec);
     if (cin == 64) {
-        hipLaunchKernelGGL(k_conv_wgrad<64>, dim3(grid), dim3(kThreads), 0, (hipStream_t)stream,
-                           (const uint16_t *)dy, (const uint16_t *)x, boards, workspace);
-        hipLaunchKernelGGL(k_conv_wgrad_reduce<64>, dim3((n_out + 255) / 256), dim3(256), 0, (hipStream_t)stream,
-                           workspace, grid, dw);
+        hipLaunchKernelGGL(k_conv_wgrad<64>, dim3(grid), dim3(64 * kWgWaves), 0, s, (const uint16_t *)dy,
+                           (const uint16_t *)x, boards, workspace);
+        hipLaunchKernelGGL(k_conv_wgrad_reduce1<64>, dim3((q * n_grp + 255) / 256), dim3(256), 0, s,
+                           (const float4 *)workspace, grid, groups);
+        hipLaunchKernelGGL(k_conv_wgrad_reduce2<64>, dim3((q + 255) / 256), dim3(256), 0, s, groups, n_grp, dw);
     } else {
-        hipLaunchKernelGGL(k_conv_wgrad<32>, dim3(grid), dim3(kThreads), 0, (hipStream_t)stream,
-                           (const uint16_t *)dy, (const uint16_t *)x, boards, workspace);
-        hipLaunchKernelGGL(k_conv_wgrad_reduce<32>, dim3((n_out + 255) / 256), dim3(256), 0, (hipStream_t)stream,
-                           workspace, grid, dw);
+        hipLaunchKernelGGL(k_conv_wgrad<32>, dim3(grid), dim3(64 * kWgWaves), 0, s, (const uint16_t *)dy,
+                           (const uint16_t *)x, boards, workspace);
+        hipLaunchKernelGGL(k_conv_wgrad_reduce1<32>, dim3((q * n_grp + 255) / 256), dim3(256), 0, s,
+                           (const float4 *)workspace, grid, groups);
+        hipLaunchKernelGGL(k_conv_wgrad_reduce2<32>, dim3((q + 255) / 256), dim3(256), 0, s, groups, n_grp, dw);
     }
     return launched("k_conv_wgrad");
+}
+
+int64_t r48_q_head_workspace_floats(void)
+{
+    const int64_t recs = cu_count();
+    return (recs + (recs + kRedGroup - 1) / kRedGroup) * kHeadRec;
+}
+
+int r48_q_head_forward(const void *h, int64_t boards, const void *w, const float *bias, float *q, void *stream)
+{
+    if (!h || !w || !bias || !q || boards < 1)
+        return fail(R48_EINVAL, "r48_q_head_forward: NULL argument or boards < 1");
+    if ((reinterpret_cast<uintptr_t>(h) | reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(q)) & 15u)
+        return fail(R48_EINVAL, "r48_q_head_forward: h, w and q must be 16-byte aligned");
+    const int64_t want = (boards + kHeadWaves * kHeadUnroll - 1) / (kHeadWaves * kHeadUnroll);
+    const int grid = (int)(want < 2 * cu_count() ? want : 2 * cu_count());
+    hipLaunchKernelGGL(k_q_head_fwd, dim3(grid), dim3(64 * kHeadWaves), 0, (hipStream_t)stream, (const uint16_t *)h,
+                       boards, (const uint16_t *)w, bias, q);
+    return launched("k_q_head_fwd");
+}
+
+int r48_q_head_backward(const float *dq, const void *h, int64_t boards, const void *w, void *dh, float *workspace,
+                        float *dw, void *stream)
+{
+    if (!dq || !h || !w || !dh || !workspace || !dw || boards < 1)
+        return fail(R48_EINVAL, "r48_q_head_backward: NULL argument or boards < 1");
+    if ((reinterpret_cast<uintptr_t>(dq) | reinterpret_cast<uintptr_t>(h) | reinterpret_cast<uintptr_t>(w) |
+         reinterpret_cast<uintptr_t>(dh) | reinterpret_cast<uintptr_t>(workspace) |
+         reinterpret_cast<uintptr_t>(dw)) & 15u)
+        return fail(R48_EINVAL, "r48_q_head_backward: all pointers must be 16-byte aligned");
+    const int grid = cu_count();
+    const int n_grp = (grid + kRedGroup - 1) / kRedGroup;
+    const int len4 = kHeadRec / 4;
+    hipStream_t s = (hipStream_t)stream;
+    float4 *groups = reinterpret_cast<float4 *>(workspace + (int64_t)grid * kHeadRec);
+    hipLaunchKernelGGL(k_q_head_bwd, dim3(grid), dim3(64 * kHeadWaves), 0, s, dq, (const uint16_t *)h, boards,
+                       (const uint16_t *)w, (uint16_t *)dh, workspace);
+    hipLaunchKernelGGL(k_records_reduce1, dim3((len4 * n_grp + 255) / 256), dim3(256), 0, s,
+                       (const float4 *)workspace, grid, len4, groups);
+    hipLaunchKernelGGL(k_records_reduce2, dim3((len4 + 255) / 256), dim3(256), 0, s, groups, n_grp, len4, 1,
+                       (float4 *)dw);
+    return launched("k_q_head_bwd");
 }
 
 }  // extern "C"

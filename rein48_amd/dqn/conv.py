@@ -6,7 +6,8 @@ convolutions run as three hand-written MFMA kernels instead of the structured de
     forward      r48_conv3x3 with pack_conv(w)           (bias added in the kernel)
     data grad    r48_conv3x3 with pack_conv_dgrad(w)     (taps flipped, in/out channels swapped)
     weight grad  r48_conv3x3_wgrad                        (fp32, summed in a fixed order)
-The stem's 18 one-hot planes are padded to one 32-channel k-chunk (board_onehot32).
+The stem's 18 one-hot planes are padded to one 32-channel k-chunk (board_onehot32). The Q head
+Linear(1024 -> 4) runs as r48_q_head_forward / _backward (QHead) instead of three hipBLASLt GEMMs.
 
 Fragment layout (v_mfma_f32_16x16x32_bf16 A operand), fragment (tap t, row tile O, k-chunk c) of
 1 KiB: lane l, element j = W[16 O + (l & 15)][32 c + 8 (l >> 4) + j][t // 3][t % 3] (zero past the
@@ -125,3 +126,54 @@ class Conv3x3Train(torch.autograd.Function):
 def conv3x3_train(x, conv):
     """Conv2d(ci, 64, 3, padding=1) `conv` on channels-last bf16 x [B, 16, cin_pad] (training)."""
     return Conv3x3Train.apply(x, conv.weight, conv.bias)
+
+
+_HEAD_WS = {}
+
+
+def q_head_forward(h, w, b):
+    """h bf16 [B, 1024], w [4, 1024], b [4] -> q fp32 [B, 4] (bf16-rounded values)."""
+    if not (h.is_cuda and h.dtype == torch.bfloat16 and h.is_contiguous() and h.dim() == 2 and h.shape[1] == 1024):
+        raise ValueError("h must be a contiguous bf16 CUDA tensor [B, 1024]")
+    wb = w.detach().to(torch.bfloat16).contiguous()
+    bf = b.detach().float().contiguous()
+    q = torch.empty((h.shape[0], 4), dtype=torch.float32, device=h.device)
+    check(_lib.load().r48_q_head_forward(ptr(h), h.shape[0], ptr(wb), ptr(bf), ptr(q), _stream(h)))
+    return q
+
+
+def q_head_backward(dq, h, w):
+    """-> (dh bf16 [B, 1024], dw fp32 [4, 1024], db fp32 [4]); parameter gradients bf16-rounded."""
+    L = _lib.load()
+    key = str(h.device)
+    if key not in _HEAD_WS:
+        _HEAD_WS[key] = torch.empty(L.r48_q_head_workspace_floats(), dtype=torch.float32, device=h.device)
+    dq = dq.float().contiguous()
+    wb = w.detach().to(torch.bfloat16).contiguous()
+    dh = torch.empty_like(h)
+    g = torch.empty(4 * 1024 + 4, dtype=torch.float32, device=h.device)
+    check(L.r48_q_head_backward(ptr(dq), ptr(h), h.shape[0], ptr(wb), ptr(dh), ptr(_HEAD_WS[key]), ptr(g),
+                                _stream(h)))
+    return dh, g[:4096].view(4, 1024), g[4096:]
+
+
+class QHead(torch.autograd.Function):
+    """q = float(bf16(h @ bf16(w)^T + bf16(b))) -- nets.py's linear(h, w, b, bf16).float() -- with
+    the gradients of that path (bf16 output gradient, bf16-rounded parameter gradients)."""
+
+    @staticmethod
+    def forward(ctx, h, w, b):
+        ctx.save_for_backward(h, w)
+        ctx.w_dtype, ctx.b_dtype = w.dtype, b.dtype
+        return q_head_forward(h, w, b)
+
+    @staticmethod
+    def backward(ctx, dq):
+        h, w = ctx.saved_tensors
+        dh, dw, db = q_head_backward(dq, h, w)
+        return dh, dw.to(ctx.w_dtype), db.to(ctx.b_dtype)
+
+
+def q_head(h, head):
+    """The head Linear(16 C -> 4) `head` on bf16 activations h [B, 1024] (training)."""
+    return QHead.apply(h.contiguous(), head.weight, head.bias)

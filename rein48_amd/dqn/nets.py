@@ -183,6 +183,9 @@ class ResNet10Q(nn.Module):
             c1, c2 = self.convs[2 * b], self.convs[2 * b + 1]
             y = self._bn_relu(1 + 2 * b, self._conv(c1, h))
             h = self._bn_relu(2 + 2 * b, self._conv(c2, y), residual=h)
+        if self._custom_conv(h):
+            from .conv import q_head
+            return q_head(h, self.head)
         return linear(h, self.head.weight, self.head.bias, d).float()
 
     @torch.no_grad()

@@ -416,6 +416,37 @@ def test_conv3x3_kernels_match_torch_conv2d(ci, B):
     assert torch.equal(conv3x3_wgrad(gy, x.contiguous())[:, :ci], dw)
 
 
+@pytest.mark.parametrize("B", [4099, 5, 1])
+def test_q_head_matches_linear(B):
+    """QHead (r48_q_head_forward / _backward) vs the path it replaces, nets.py's
+    linear(h, w, b, bf16).float() through hipBLASLt: the same bf16 products summed in fp32 in another
+    order, outputs and parameter gradients rounded to bf16 -- q and dh agree within 1 bf16 ulp of
+    the largest value (<= 1e-2 relative), dw and db within 1e-2 relative. Ragged B (not a multiple
+    of the 4-board unroll) included; the fixed-order reductions make the backward deterministic."""
+    from rein48_amd.a3c.nets import linear
+    from rein48_amd.dqn.conv import QHead
+    g = torch.Generator(device="cpu").manual_seed(B)
+    h = torch.randn(B, 1024, generator=g).to(DEV).to(torch.bfloat16)
+    w = (torch.randn(4, 1024, generator=g) * 0.05).to(DEV).requires_grad_(True)
+    b = torch.randn(4, generator=g).to(DEV).requires_grad_(True)
+    dq = torch.randn(B, 4, generator=g).to(DEV)
+    outs = []
+    for fn in (lambda hh: QHead.apply(hh, w, b), lambda hh: linear(hh, w, b, torch.bfloat16).float()):
+        hh = h.clone().requires_grad_(True)
+        w.grad = b.grad = None
+        q = fn(hh)
+        q.backward(dq)
+        outs.append((q.detach(), hh.grad.detach(), w.grad.detach().clone(), b.grad.detach().clone()))
+    (q, dh, dw, db), (q_r, dh_r, dw_r, db_r) = outs
+    assert q.dtype == torch.float32 and torch.equal(q, q.to(torch.bfloat16).float())
+    assert _rel(q, q_r) < 1e-2 and _rel(dh, dh_r) < 1e-2
+    assert _rel(dw, dw_r) < 1e-2 and _rel(db, db_r) < 1e-2
+    hh = h.clone().requires_grad_(True)
+    w.grad = b.grad = None
+    QHead.apply(hh, w, b).backward(dq)
+    assert torch.equal(hh.grad, dh) and torch.equal(w.grad, dw) and torch.equal(b.grad, db)
+
+
 def test_onehot32_exact():
     from rein48_amd.dqn.conv import board_onehot32
     b = np.random.default_rng(5).integers(0, 18, size=(3001, 16)).astype(np.int8)

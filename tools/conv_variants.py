@@ -1,0 +1,43 @@
+"""Ablation variants of rein48_amd/csrc/r48_conv.hip for timing experiments (tools/exp_conv.py):
+each variant is the product source with one textual edit, written to build/var/ and linked into
+build/lib_conv_<name>.so by tools/build_variant.sh. The product source carries no ablation switches.
+usage: python tools/conv_variants.py [name ...]"""
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(ROOT, "rein48_amd", "csrc", "r48_conv.hip")
+
+VARIANTS = {
+    # conv3x3: outputs never stored (a runtime condition that is never true keeps the math alive)
+    "fwd_nostore": [("            if (live) {\n#pragma unroll\n                    for (int col",
+                     "            if (live && boards == -7) {\n#pragma unroll\n                    for (int col")],
+    # conv3x3: rows loaded once (prologue), no loads inside the tile loop
+    "fwd_noload": [("            load_row(r < 2 ? tile : (next < n_tiles ? next : tile), r < 2 ? r + 2 : r - 2);\n", "")],
+    # wgrad: the DMA ring runs, no MFMA work
+    "wgrad_nocompute": [("        stage(i + kRing - 1, (buf + kRing - 1) % kRing);          // buffer of step i - 1\n"
+                         "        compute(buf);\n",
+                         "        stage(i + kRing - 1, (buf + kRing - 1) % kRing);          // buffer of step i - 1\n")],
+    # wgrad: MFMA work and barriers over the prologue's buffers, no DMA inside the loop
+    "wgrad_nodma": [("        stage(i + kRing - 1, (buf + kRing - 1) % kRing);          // buffer of step i - 1\n", "")],
+}
+
+
+def build(name):
+    s = open(SRC).read()
+    for old, new in VARIANTS[name]:
+        if old not in s:
+            raise SystemExit("variant %s: pattern not found" % name)
+        s = s.replace(old, new)
+    os.makedirs(os.path.join(ROOT, "build", "var"), exist_ok=True)
+    path = os.path.join(ROOT, "build", "var", "conv_%s.hip" % name)
+    open(path, "w").write(s)
+    subprocess.check_call(["bash", os.path.join(ROOT, "tools", "build_variant.sh"), path, "r48_conv",
+                           os.path.join(ROOT, "build", "lib_conv_%s.so" % name)], cwd=ROOT)
+
+
+if __name__ == "__main__":
+    for n in sys.argv[1:] or list(VARIANTS):
+        build(n)
+        print("built", n)
