@@ -302,17 +302,23 @@ int r48_td_target(const float *reward, const uint8_t *done, const float *q_next_
  * planes 18..31 zero), 16-byte aligned. */
 int r48_board_onehot32(const int8_t *boards, int64_t n, void *out, void *stream);
 /* y[b][p][co] = bias[co] + sum over taps t in the grid, ci of W[co][ci][t] x[b][p + off(t)][ci]
- * (the forward conv; with the flipped, transposed taps the data gradient). wfrag: 9 x 4 x (cin/32)
- * MFMA A fragments of 1 KiB (rein48_amd/dqn/conv.py pack_conv); bias fp32 [64] or NULL. All
- * pointers 16-byte aligned. */
-int r48_conv3x3(const void *x, int64_t boards, int32_t cin, const void *wfrag, const float *bias, void *y,
-                void *stream);
+ * (+ add[b][p][co]) (the forward conv; with the flipped, transposed taps the data gradient).
+ * wfrag: 9 x 4 x (cin/32) MFMA A fragments of 1 KiB (rein48_amd/dqn/conv.py pack_conv); bias fp32
+ * [64] or NULL; add bf16 [boards][16][64] or NULL (cin 64 only: a basic block's input gradient
+ * summed in the epilogue). All pointers 16-byte aligned. */
+int r48_conv3x3(const void *x, int64_t boards, int32_t cin, const void *wfrag, const float *bias, const void *add,
+                void *y, void *stream);
 /* dw fp32 [64][cin][3][3] = sum over boards and in-grid cells of dy[b][p][co] x[b][p + off(t)][ci];
  * workspace of r48_conv_wgrad_workspace_floats(cin) floats (per-workgroup records, summed in a
  * fixed order: deterministic). */
 int64_t r48_conv_wgrad_workspace_floats(int32_t cin);
 int r48_conv3x3_wgrad(const void *dy, const void *x, int64_t boards, int32_t cin, float *workspace, float *dw,
                       void *stream);
+/* Every fragment set of the update's convs in one launch: weights = DEVICE array of 9 fp32
+ * pointers (stem [64][18][3][3], conv1..8 [64][64][3][3]); fwd (bf16, 16-byte aligned) gets the
+ * stem's 36 fragments then conv1..8's 72 each (the r48_conv3x3 wfrag of each layer, pack_conv
+ * layout), dgrad gets conv1..8's data-gradient fragments (72 each, pack_conv_dgrad layout). */
+int r48_conv_pack_resnet(const float *const *weights, void *fwd, void *dgrad, void *stream);
 /* The Q head Linear(1024 -> 4) of the update (nets.py: linear(h, head.weight, head.bias, bf16)
  * .float(), replacing its three hipBLASLt GEMMs): h bf16 [boards][1024] (channels-last cells x
  * channels), w bf16 [4][1024], bias fp32 [4] (used bf16-rounded); q fp32 [boards][4] holds the
@@ -360,14 +366,16 @@ int r48_struct_conv_weight_grad(const void *gdense, int32_t co, int32_t ci, int3
  * unbiased variance, save = float[2 C] {mean, invstd} for the backward. Backward: given dy
  * (gradient of y) and the saved y (ReLU mask, when relu) -> dx, dgamma, dbeta (nullable) and
  * dresidual (nullable: the gradient reaching the residual input). workspace: float[
- * r48_bn_workspace_floats(rows, C)], not shared between calls in flight. Deterministic. */
+ * r48_bn_workspace_floats(rows, C)], not shared between calls in flight. Deterministic.
+ * mask (nullable): uint8[rows][C / 8], bit k of byte (r, j) = (y[r][8 j + k] > 0); the forward
+ * writes it, and the backward reads it instead of y when given (y may then be NULL). */
 int64_t r48_bn_workspace_floats(int64_t rows, int32_t C);
 int r48_bn_forward(const void *x, const void *residual, int64_t rows, int32_t C, const float *gamma,
                    const float *beta, float *running_mean, float *running_var, float momentum, float eps,
-                   int32_t relu, float *save, float *workspace, void *y, void *stream);
-int r48_bn_backward(const void *dy, const void *y, const void *x, int64_t rows, int32_t C, const float *gamma,
-                    const float *save, int32_t relu, float *workspace, void *dx, void *dresidual, float *dgamma,
-                    float *dbeta, void *stream);
+                   int32_t relu, float *save, float *workspace, void *y, uint8_t *mask, void *stream);
+int r48_bn_backward(const void *dy, const void *y, const uint8_t *mask, const void *x, int64_t rows, int32_t C,
+                    const float *gamma, const float *save, int32_t relu, float *workspace, void *dx, void *dresidual,
+                    float *dgamma, float *dbeta, void *stream);
 
 /* Thread-local message of the last failed call on this thread ("" if none). */
 const char *r48_last_error(void);

@@ -229,10 +229,13 @@ __global__ __launch_bounds__(kBlock) void k_bn_finish(const uint16_t *__restrict
     }
 }
 
-template <int C, bool RELU, bool RES>
+// mask (optional, MASK): one byte per thread and row, bit k = (y[row][8 cg + k] > 0) -- the ReLU
+// derivative the backward needs, 1/16 of the bytes of y
+template <int C, bool RELU, bool RES, bool MASK>
 __global__ __launch_bounds__(kBlock) void k_bn_apply(const uint16_t *__restrict__ x,
                                                      const uint16_t *__restrict__ res, int64_t rows,
-                                                     const float *__restrict__ coef, uint16_t *__restrict__ y)
+                                                     const float *__restrict__ coef, uint16_t *__restrict__ y,
+                                                     uint8_t *__restrict__ mask)
 {
     using G = Geo<C>;
     const int cg = G::cg();
@@ -257,17 +260,34 @@ __global__ __launch_bounds__(kBlock) void k_bn_apply(const uint16_t *__restrict_
                 v += q[k];
             f[k] = RELU ? fmaxf(v, 0.f) : v;
         }
-        *reinterpret_cast<uint4 *>(y + o) = pack8(f);
+        const uint4 out = pack8(f);
+        *reinterpret_cast<uint4 *>(y + o) = out;
+        if (MASK) {
+            const uint32_t w[4] = {out.x, out.y, out.z, out.w};
+            uint32_t m = 0;
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                m |= ((w[k] & 0x7FFFu) != 0 && !(w[k] & 0x8000u) ? 1u : 0u) << (2 * k) |
+                     ((w[k] & 0x7FFF0000u) != 0 && !(w[k] & 0x80000000u) ? 1u : 0u) << (2 * k + 1);
+            mask[o >> 3] = (uint8_t)m;
+        }
     }
 }
 
 // ---------------------------------------------------------------- backward
-// g = dy * [y > 0] (ReLU'), or dy
-template <bool RELU>
-__device__ __forceinline__ void grad_in(const uint16_t *dy, const uint16_t *y, int64_t o, float g[8])
+// g = dy * [y > 0] (ReLU'), or dy; with MASK the ReLU derivative comes from the forward's mask
+// bits instead of y
+template <bool RELU, bool MASK>
+__device__ __forceinline__ void grad_in(const uint16_t *dy, const uint16_t *y, const uint8_t *mask, int64_t o,
+                                        float g[8])
 {
     unpack8(ld16(dy, o), g);
-    if (RELU) {
+    if (RELU && MASK) {
+        const uint32_t m = mask[o >> 3];
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+            g[k] = (m >> k) & 1u ? g[k] : 0.f;
+    } else if (RELU) {
         float yy[8];
         unpack8(ld16(y, o), yy);
 #pragma unroll
@@ -276,9 +296,10 @@ __device__ __forceinline__ void grad_in(const uint16_t *dy, const uint16_t *y, i
     }
 }
 
-template <int C, bool RELU>
+template <int C, bool RELU, bool MASK>
 __global__ __launch_bounds__(kBlock) void k_bn_bwd_reduce(const uint16_t *__restrict__ dy,
                                                           const uint16_t *__restrict__ y,
+                                                          const uint8_t *__restrict__ mask,
                                                           const uint16_t *__restrict__ x, int64_t rows,
                                                           const float *__restrict__ save, float *__restrict__ part)
 {
@@ -294,11 +315,14 @@ __global__ __launch_bounds__(kBlock) void k_bn_bwd_reduce(const uint16_t *__rest
     int64_t r = G::row0();
     for (; r + (kUnroll - 1) * st < rows; r += kUnroll * st) {
         uint4 vd[kUnroll], vy[kUnroll], vx[kUnroll];
+        uint32_t vm[kUnroll];
 #pragma unroll
         for (int u = 0; u < kUnroll; u++) {
             const int64_t o = (r + u * st) * C + 8 * cg;
             vd[u] = ld16(dy, o);
-            if (RELU)
+            if (RELU && MASK)
+                vm[u] = mask[o >> 3];
+            else if (RELU)
                 vy[u] = ld16(y, o);
             vx[u] = ld16(x, o);
         }
@@ -307,11 +331,13 @@ __global__ __launch_bounds__(kBlock) void k_bn_bwd_reduce(const uint16_t *__rest
             float g[8], f[8], yy[8];
             unpack8(vd[u], g);
             unpack8(vx[u], f);
-            if (RELU)
+            if (RELU && !MASK)
                 unpack8(vy[u], yy);
 #pragma unroll
             for (int k = 0; k < 8; k++) {
-                if (RELU)
+                if (RELU && MASK)
+                    g[k] = (vm[u] >> k) & 1u ? g[k] : 0.f;
+                else if (RELU)
                     g[k] = yy[k] > 0.f ? g[k] : 0.f;
                 acc[0][k] += g[k];
                 acc[1][k] = fmaf(g[k], f[k] - mean[k], acc[1][k]);
@@ -321,7 +347,7 @@ __global__ __launch_bounds__(kBlock) void k_bn_bwd_reduce(const uint16_t *__rest
     for (; r < rows; r += st) {
         const int64_t o = r * C + 8 * cg;
         float g[8], f[8];
-        grad_in<RELU>(dy, y, o, g);
+        grad_in<RELU, MASK>(dy, y, mask, o, g);
         unpack8(ld16(x, o), f);
 #pragma unroll
         for (int k = 0; k < 8; k++) {
@@ -362,9 +388,10 @@ __global__ __launch_bounds__(kBlock) void k_bn_bwd_finish(const float *__restric
     coef[2 * C + c] = (float)(-a * sg / n - cc * mean);
 }
 
-template <int C, bool RELU, bool DRES>
+template <int C, bool RELU, bool DRES, bool MASK>
 __global__ __launch_bounds__(kBlock) void k_bn_bwd_apply(const uint16_t *__restrict__ dy,
                                                          const uint16_t *__restrict__ y,
+                                                         const uint8_t *__restrict__ mask,
                                                          const uint16_t *__restrict__ x, int64_t rows,
                                                          const float *__restrict__ coef,
                                                          uint16_t *__restrict__ dx, uint16_t *__restrict__ dres)
@@ -382,7 +409,7 @@ __global__ __launch_bounds__(kBlock) void k_bn_bwd_apply(const uint16_t *__restr
     for (int64_t r = G::row0(); r < rows; r += st) {
         const int64_t o = r * C + 8 * cg;
         float g[8], f[8], out[8];
-        grad_in<RELU>(dy, y, o, g);
+        grad_in<RELU, MASK>(dy, y, mask, o, g);
         unpack8(ld16(x, o), f);
 #pragma unroll
         for (int k = 0; k < 8; k++)
@@ -422,10 +449,20 @@ int check_args(const void *x, int64_t rows, int32_t C)
     return R48_OK;
 }
 
+template <int C, bool RELU, bool RES>
+void launch_apply(dim3 g, hipStream_t s, const uint16_t *x, const uint16_t *res, int64_t rows, const float *coef,
+                  uint16_t *y, uint8_t *mask)
+{
+    if (mask)
+        hipLaunchKernelGGL((k_bn_apply<C, RELU, RES, true>), g, dim3(kBlock), 0, s, x, res, rows, coef, y, mask);
+    else
+        hipLaunchKernelGGL((k_bn_apply<C, RELU, RES, false>), g, dim3(kBlock), 0, s, x, res, rows, coef, y, mask);
+}
+
 template <int C>
 int forward_c(const uint16_t *x, const uint16_t *res, int64_t rows, const float *gamma, const float *beta,
               float *rm, float *rv, float momentum, float eps, int relu, float *save, float *ws, uint16_t *y,
-              hipStream_t s)
+              uint8_t *mask, hipStream_t s)
 {
     const int nb = reduce_blocks(rows, C);
     float *coef = ws + (int64_t)nb * 2 * C;
@@ -434,38 +471,45 @@ int forward_c(const uint16_t *x, const uint16_t *res, int64_t rows, const float 
                        save, coef);
     const dim3 g(apply_blocks(rows, C));
     if (relu && res)
-        hipLaunchKernelGGL((k_bn_apply<C, true, true>), g, dim3(kBlock), 0, s, x, res, rows, coef, y);
+        launch_apply<C, true, true>(g, s, x, res, rows, coef, y, mask);
     else if (relu)
-        hipLaunchKernelGGL((k_bn_apply<C, true, false>), g, dim3(kBlock), 0, s, x, res, rows, coef, y);
+        launch_apply<C, true, false>(g, s, x, res, rows, coef, y, mask);
     else if (res)
-        hipLaunchKernelGGL((k_bn_apply<C, false, true>), g, dim3(kBlock), 0, s, x, res, rows, coef, y);
+        launch_apply<C, false, true>(g, s, x, res, rows, coef, y, mask);
     else
-        hipLaunchKernelGGL((k_bn_apply<C, false, false>), g, dim3(kBlock), 0, s, x, res, rows, coef, y);
+        launch_apply<C, false, false>(g, s, x, res, rows, coef, y, mask);
     return launched("k_bn_apply");
 }
 
+template <int C, bool RELU, bool MASK>
+void launch_bwd(int nb, dim3 g, hipStream_t s, const uint16_t *dy, const uint16_t *y, const uint8_t *mask,
+                const uint16_t *x, int64_t rows, const float *gamma, const float *save, float *ws, float *coef,
+                uint16_t *dx, uint16_t *dres, float *dgamma, float *dbeta)
+{
+    hipLaunchKernelGGL((k_bn_bwd_reduce<C, RELU, MASK>), dim3(nb), dim3(kBlock), 0, s, dy, y, mask, x, rows, save, ws);
+    hipLaunchKernelGGL(k_bn_bwd_finish, dim3(C), dim3(kBlock), 0, s, ws, nb, C, rows, gamma, save, dgamma, dbeta, coef);
+    if (dres)
+        hipLaunchKernelGGL((k_bn_bwd_apply<C, RELU, true, MASK>), g, dim3(kBlock), 0, s, dy, y, mask, x, rows, coef, dx,
+                           dres);
+    else
+        hipLaunchKernelGGL((k_bn_bwd_apply<C, RELU, false, MASK>), g, dim3(kBlock), 0, s, dy, y, mask, x, rows, coef,
+                           dx, dres);
+}
+
 template <int C>
-int backward_c(const uint16_t *dy, const uint16_t *y, const uint16_t *x, int64_t rows, const float *gamma,
-               const float *save, int relu, float *ws, uint16_t *dx, uint16_t *dres, float *dgamma, float *dbeta,
-               hipStream_t s)
+int backward_c(const uint16_t *dy, const uint16_t *y, const uint8_t *mask, const uint16_t *x, int64_t rows,
+               const float *gamma, const float *save, int relu, float *ws, uint16_t *dx, uint16_t *dres,
+               float *dgamma, float *dbeta, hipStream_t s)
 {
     const int nb = reduce_blocks(rows, C);
     float *coef = ws + (int64_t)nb * 2 * C;
-    if (relu)
-        hipLaunchKernelGGL((k_bn_bwd_reduce<C, true>), dim3(nb), dim3(kBlock), 0, s, dy, y, x, rows, save, ws);
-    else
-        hipLaunchKernelGGL((k_bn_bwd_reduce<C, false>), dim3(nb), dim3(kBlock), 0, s, dy, y, x, rows, save, ws);
-    hipLaunchKernelGGL(k_bn_bwd_finish, dim3(C), dim3(kBlock), 0, s, ws, nb, C, rows, gamma, save, dgamma, dbeta, coef);
     const dim3 g(apply_blocks(rows, C));
-    if (relu && dres)
-        hipLaunchKernelGGL((k_bn_bwd_apply<C, true, true>), g, dim3(kBlock), 0, s, dy, y, x, rows, coef, dx, dres);
+    if (relu && mask)
+        launch_bwd<C, true, true>(nb, g, s, dy, y, mask, x, rows, gamma, save, ws, coef, dx, dres, dgamma, dbeta);
     else if (relu)
-        hipLaunchKernelGGL((k_bn_bwd_apply<C, true, false>), g, dim3(kBlock), 0, s, dy, y, x, rows, coef, dx, dres);
-    else if (dres)
-        hipLaunchKernelGGL((k_bn_bwd_apply<C, false, true>), g, dim3(kBlock), 0, s, dy, y, x, rows, coef, dx, dres);
+        launch_bwd<C, true, false>(nb, g, s, dy, y, mask, x, rows, gamma, save, ws, coef, dx, dres, dgamma, dbeta);
     else
-        hipLaunchKernelGGL((k_bn_bwd_apply<C, false, false>), g, dim3(kBlock), 0, s, dy, y, x, rows, coef, dx,
-                           dres);
+        launch_bwd<C, false, false>(nb, g, s, dy, y, mask, x, rows, gamma, save, ws, coef, dx, dres, dgamma, dbeta);
     return launched("k_bn_bwd_apply");
 }
 
@@ -482,7 +526,7 @@ int64_t r48_bn_workspace_floats(int64_t rows, int32_t C)
 
 int r48_bn_forward(const void *x, const void *residual, int64_t rows, int32_t C, const float *gamma,
                    const float *beta, float *running_mean, float *running_var, float momentum, float eps,
-                   int32_t relu, float *save, float *workspace, void *y, void *stream)
+                   int32_t relu, float *save, float *workspace, void *y, uint8_t *mask, void *stream)
 {
     int rc = check_args(x, rows, C);
     if (rc)
@@ -496,37 +540,37 @@ int r48_bn_forward(const void *x, const void *residual, int64_t rows, int32_t C,
     switch (C) {
     case 32:
         return forward_c<32>(xs, rs, rows, gamma, beta, running_mean, running_var, momentum, eps, relu, save,
-                             workspace, (uint16_t *)y, s);
+                             workspace, (uint16_t *)y, mask, s);
     case 64:
         return forward_c<64>(xs, rs, rows, gamma, beta, running_mean, running_var, momentum, eps, relu, save,
-                             workspace, (uint16_t *)y, s);
+                             workspace, (uint16_t *)y, mask, s);
     default:
         return forward_c<128>(xs, rs, rows, gamma, beta, running_mean, running_var, momentum, eps, relu, save,
-                              workspace, (uint16_t *)y, s);
+                              workspace, (uint16_t *)y, mask, s);
     }
 }
 
-int r48_bn_backward(const void *dy, const void *y, const void *x, int64_t rows, int32_t C, const float *gamma,
-                    const float *save, int32_t relu, float *workspace, void *dx, void *dresidual, float *dgamma,
-                    float *dbeta, void *stream)
+int r48_bn_backward(const void *dy, const void *y, const uint8_t *mask, const void *x, int64_t rows, int32_t C,
+                    const float *gamma, const float *save, int32_t relu, float *workspace, void *dx, void *dresidual,
+                    float *dgamma, float *dbeta, void *stream)
 {
     int rc = check_args(x, rows, C);
     if (rc)
         return rc;
     if (!dy || !aligned16(dy) || !gamma || !save || !workspace || !dx || !aligned16(dx) ||
-        (relu && (!y || !aligned16(y))) || (dresidual && !aligned16(dresidual)))
+        (relu && !mask && (!y || !aligned16(y))) || (dresidual && !aligned16(dresidual)))
         return fail(R48_EINVAL, "r48_bn_backward: null or misaligned argument");
     const uint16_t *d = (const uint16_t *)dy, *ys = (const uint16_t *)y, *xs = (const uint16_t *)x;
     hipStream_t s = (hipStream_t)stream;
     switch (C) {
     case 32:
-        return backward_c<32>(d, ys, xs, rows, gamma, save, relu, workspace, (uint16_t *)dx, (uint16_t *)dresidual,
-                              dgamma, dbeta, s);
+        return backward_c<32>(d, ys, mask, xs, rows, gamma, save, relu, workspace, (uint16_t *)dx,
+                              (uint16_t *)dresidual, dgamma, dbeta, s);
     case 64:
-        return backward_c<64>(d, ys, xs, rows, gamma, save, relu, workspace, (uint16_t *)dx, (uint16_t *)dresidual,
-                              dgamma, dbeta, s);
+        return backward_c<64>(d, ys, mask, xs, rows, gamma, save, relu, workspace, (uint16_t *)dx,
+                              (uint16_t *)dresidual, dgamma, dbeta, s);
     default:
-        return backward_c<128>(d, ys, xs, rows, gamma, save, relu, workspace, (uint16_t *)dx,
+        return backward_c<128>(d, ys, mask, xs, rows, gamma, save, relu, workspace, (uint16_t *)dx,
                                (uint16_t *)dresidual, dgamma, dbeta, s);
     }
 }

@@ -98,10 +98,13 @@ int cu_count()
 // registers are free by then). A wave keeps 1-2 rows (8-16 KB) in flight behind its MFMAs.
 constexpr int kConvWaves = 8;
 
-template <int NC>
+// ADD: y += add[b][p][co] (bf16, the same layout as y) before the bf16 rounding -- the data
+// gradient of a basic block's first conv plus the gradient of the identity path
+template <int NC, bool ADD>
 __global__ __launch_bounds__(64 * kConvWaves, 1) void k_conv3x3(const uint16_t *__restrict__ x, int64_t boards,
                                                                const uint4 *__restrict__ wfrag,
                                                                const float *__restrict__ bias,
+                                                               const uint16_t *__restrict__ add,
                                                                uint16_t *__restrict__ y)
 {
     constexpr int kFrags = 9 * 4 * NC;
@@ -148,6 +151,15 @@ __global__ __launch_bounds__(64 * kConvWaves, 1) void k_conv3x3(const uint16_t *
 #pragma unroll
             for (int oh = 0; oh < 2; oh++) {   // two passes of two row tiles: 32 accumulator registers
                 f32x4 acc[4][2];               // [output column][row tile 2 oh + o]
+                uint2 ad[4][2];
+                if (ADD) {
+                    const uint16_t *ar = add + (live ? b : 0) * 16 * kCout + 4 * g;
+#pragma unroll
+                    for (int col = 0; col < 4; col++)
+#pragma unroll
+                        for (int o = 0; o < 2; o++)
+                            ad[col][o] = *reinterpret_cast<const uint2 *>(ar + (4 * r + col) * kCout + 16 * (2 * oh + o));
+                }
 #pragma unroll
                 for (int k = 0; k < 9 * NC; k++) {
                     const int t = kTapOrder[k / NC], c = k % NC;
@@ -170,6 +182,17 @@ __global__ __launch_bounds__(64 * kConvWaves, 1) void k_conv3x3(const uint16_t *
                                        : acc[col][o],
                                 0, 0, 0);
                     }
+                }
+                if (ADD) {
+#pragma unroll
+                    for (int col = 0; col < 4; col++)
+#pragma unroll
+                        for (int o = 0; o < 2; o++) {
+                            acc[col][o][0] += __uint_as_float(ad[col][o].x << 16);
+                            acc[col][o][1] += __uint_as_float(ad[col][o].x & 0xFFFF0000u);
+                            acc[col][o][2] += __uint_as_float(ad[col][o].y << 16);
+                            acc[col][o][3] += __uint_as_float(ad[col][o].y & 0xFFFF0000u);
+                        }
                 }
                 if (live) {
 #pragma unroll
@@ -659,6 +682,42 @@ __global__ __launch_bounds__(256) void k_records_reduce2(const float4 *__restric
     out[k] = s;
 }
 
+// ------------------------------------------------------------------- weight fragments
+// The A fragments of every conv of the ResNet-10 update in one launch: part 0 = stem forward
+// (18 input channels padded to one 32-channel k-chunk: 36 fragments), parts 1..8 = conv1..8
+// forward (72 each), parts 9..16 = conv1..8 data gradient (W'[ci][co][t] = W[co][ci][8 - t]). One
+// thread per bf16 element: fragment (t, O, c), lane l, element j holds
+// W[16 O + (l & 15)][32 c + 8 (l >> 4) + j][t] of the (possibly flipped) weight -- the layout of
+// rein48_amd/dqn/conv.py pack_conv / pack_conv_dgrad.
+constexpr int kPackParts = 17;
+
+__global__ __launch_bounds__(256) void k_conv_pack(const float *const *__restrict__ w, uint16_t *__restrict__ fwd,
+                                                  uint16_t *__restrict__ dgrad)
+{
+    const int part = blockIdx.y;
+    const int nc = part == 0 ? 1 : 2;
+    const int n = 9 * 4 * nc * 512;                              // elements of this part
+    const int e = blockIdx.x * 256 + threadIdx.x;
+    if (e >= n)
+        return;
+    const int frag = e >> 9, lane = (e >> 3) & 63, j = e & 7;
+    const int c = frag % nc, O = (frag / nc) % 4, t = frag / (4 * nc);
+    const int m = 16 * O + (lane & 15), k = 32 * c + 8 * (lane >> 4) + j;   // A row (output), k (input)
+    float v;
+    uint16_t *out;
+    if (part == 0) {                                             // stem [64][18][9]
+        v = k < 18 ? w[0][(m * 18 + k) * 9 + t] : 0.f;
+        out = fwd;
+    } else if (part <= 8) {                                      // conv `part` forward [64][64][9]
+        v = w[part][(m * 64 + k) * 9 + t];
+        out = fwd + 36 * 512 + (part - 1) * 72 * 512;
+    } else {                                                     // conv part - 8, data gradient
+        v = w[part - 8][(k * 64 + m) * 9 + (8 - t)];
+        out = dgrad + (part - 9) * 72 * 512;
+    }
+    out[e] = (uint16_t)(__builtin_bit_cast(uint32_t, (float)(__bf16)v) >> 16);
+}
+
 // one lane per (board, cell): the one-hot of the exponent over 32 bf16 planes (e = 0..17, planes
 // 18..31 zero: the stem's input channels padded to one 32-channel k-chunk), four 16-byte stores
 __global__ __launch_bounds__(256) void k_onehot32(const int8_t *__restrict__ boards, int64_t n_cells,
@@ -693,23 +752,29 @@ int r48_board_onehot32(const int8_t *boards, int64_t n, void *out, void *stream)
     return launched("k_onehot32");
 }
 
-int r48_conv3x3(const void *x, int64_t boards, int32_t cin, const void *wfrag, const float *bias, void *y,
-                void *stream)
+int r48_conv3x3(const void *x, int64_t boards, int32_t cin, const void *wfrag, const float *bias, const void *add,
+                void *y, void *stream)
 {
     if (!x || !wfrag || !y || boards < 1 || (cin != 32 && cin != 64))
         return fail(R48_EINVAL, "r48_conv3x3: NULL argument, boards < 1 or cin not 32/64");
     if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(wfrag) | reinterpret_cast<uintptr_t>(y) |
-         reinterpret_cast<uintptr_t>(bias)) & 15u)
-        return fail(R48_EINVAL, "r48_conv3x3: x, wfrag, bias and y must be 16-byte aligned");
+         reinterpret_cast<uintptr_t>(bias) | reinterpret_cast<uintptr_t>(add)) & 15u)
+        return fail(R48_EINVAL, "r48_conv3x3: x, wfrag, bias, add and y must be 16-byte aligned");
+    if (add && cin != 64)
+        return fail(R48_EINVAL, "r48_conv3x3: add needs 64 input channels");
     const int64_t tiles = (boards + 15) / 16;
     const int64_t want = (tiles + kConvWaves - 1) / kConvWaves;
     const int grid = (int)(want < cu_count() ? want : cu_count());
-    if (cin == 64)
-        hipLaunchKernelGGL(k_conv3x3<2>, dim3(grid), dim3(64 * kConvWaves), 0, (hipStream_t)stream,
-                           (const uint16_t *)x, boards, (const uint4 *)wfrag, bias, (uint16_t *)y);
+    const uint16_t *a = (const uint16_t *)add;
+    if (cin == 64 && add)
+        hipLaunchKernelGGL((k_conv3x3<2, true>), dim3(grid), dim3(64 * kConvWaves), 0, (hipStream_t)stream,
+                           (const uint16_t *)x, boards, (const uint4 *)wfrag, bias, a, (uint16_t *)y);
+    else if (cin == 64)
+        hipLaunchKernelGGL((k_conv3x3<2, false>), dim3(grid), dim3(64 * kConvWaves), 0, (hipStream_t)stream,
+                           (const uint16_t *)x, boards, (const uint4 *)wfrag, bias, a, (uint16_t *)y);
     else
-        hipLaunchKernelGGL(k_conv3x3<1>, dim3(grid), dim3(64 * kConvWaves), 0, (hipStream_t)stream,
-                           (const uint16_t *)x, boards, (const uint4 *)wfrag, bias, (uint16_t *)y);
+        hipLaunchKernelGGL((k_conv3x3<1, false>), dim3(grid), dim3(64 * kConvWaves), 0, (hipStream_t)stream,
+                           (const uint16_t *)x, boards, (const uint4 *)wfrag, bias, a, (uint16_t *)y);
     return launched("k_conv3x3");
 }
 
@@ -789,6 +854,15 @@ int r48_q_head_backward(const float *dq, const void *h, int64_t boards, const vo
     hipLaunchKernelGGL(k_records_reduce2, dim3((len4 + 255) / 256), dim3(256), 0, s, groups, n_grp, len4, 1,
                        (float4 *)dw);
     return launched("k_q_head_bwd");
+}
+
+int r48_conv_pack_resnet(const float *const *weights, void *fwd, void *dgrad, void *stream)
+{
+    if (!weights || !fwd || !dgrad || ((reinterpret_cast<uintptr_t>(fwd) | reinterpret_cast<uintptr_t>(dgrad)) & 15u))
+        return fail(R48_EINVAL, "r48_conv_pack_resnet: NULL or misaligned argument");
+    hipLaunchKernelGGL(k_conv_pack, dim3(9 * 4 * 2 * 512 / 256, kPackParts), dim3(256), 0, (hipStream_t)stream, weights,
+                       (uint16_t *)fwd, (uint16_t *)dgrad);
+    return launched("k_conv_pack");
 }
 
 }  // extern "C"

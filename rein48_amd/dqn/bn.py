@@ -44,7 +44,7 @@ class _BNAct(torch.autograd.Function):
         g, b = gamma.detach().float().contiguous(), beta.detach().float().contiguous()
         check(_lib.load().r48_bn_forward(ptr(x), ptr(residual), rows, C, ptr(g), ptr(b), ptr(running_mean),
                                          ptr(running_var), float(momentum), float(eps), int(bool(relu)),
-                                         ptr(save), ptr(ws), ptr(y), _stream(x)))
+                                         ptr(save), ptr(ws), ptr(y), None, _stream(x)))
         ctx.save_for_backward(x, y, g, save)
         ctx.relu, ctx.has_res = bool(relu), residual is not None
         ctx.param_dtype = gamma.dtype
@@ -62,7 +62,7 @@ class _BNAct(torch.autograd.Function):
         dgamma = torch.empty(C, dtype=torch.float32, device=x.device)
         dbeta = torch.empty(C, dtype=torch.float32, device=x.device)
         ws = _workspace(rows, C, x.device)
-        check(_lib.load().r48_bn_backward(ptr(dy), ptr(y), ptr(x), rows, C, ptr(g), ptr(save), int(ctx.relu),
+        check(_lib.load().r48_bn_backward(ptr(dy), ptr(y), None, ptr(x), rows, C, ptr(g), ptr(save), int(ctx.relu),
                                           ptr(ws), ptr(dx), ptr(dres), ptr(dgamma), ptr(dbeta), _stream(x)))
         return (dx, dgamma.to(ctx.param_dtype), dbeta.to(ctx.param_dtype), dres, None, None, None, None, None)
 

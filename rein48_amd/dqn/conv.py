@@ -72,22 +72,25 @@ def board_onehot32(boards, out=None):
     return out
 
 
-def conv3x3(x, frags, bias=None):
-    """x bf16 [B, 16, cin] (cin 32 or 64) -> y bf16 [B, 16, 64]."""
+def conv3x3(x, frags, bias=None, add=None, out=None):
+    """x bf16 [B, 16, cin] (cin 32 or 64) -> y bf16 [B, 16, 64] (+ add, bf16 [B, 16, 64])."""
     if not (x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous() and x.dim() == 3 and x.shape[1] == 16):
         raise ValueError("x must be a contiguous bf16 CUDA tensor [B, 16, cin]")
     B, _, cin = x.shape
-    y = torch.empty((B, 16, 64), dtype=torch.bfloat16, device=x.device)
+    if add is not None and not (add.dtype == torch.bfloat16 and add.is_contiguous() and add.numel() == B * 1024):
+        raise ValueError("add must be a contiguous bf16 tensor of B x 16 x 64")
+    y = torch.empty((B, 16, 64), dtype=torch.bfloat16, device=x.device) if out is None else out
     b = None if bias is None else bias.detach().float().contiguous()
-    check(_lib.load().r48_conv3x3(ptr(x), B, cin, ptr(frags), ptr(b), ptr(y), _stream(x)))
+    check(_lib.load().r48_conv3x3(ptr(x), B, cin, ptr(frags), ptr(b), ptr(add), ptr(y), _stream(x)))
     return y
 
 
 _WS = {}
 
 
-def conv3x3_wgrad(dy, x):
-    """dw fp32 [64, cin, 3, 3] = sum over boards and in-grid cells of dy[b, p, co] x[b, p + off(t), ci]."""
+def conv3x3_wgrad(dy, x, out=None):
+    """dw fp32 [64, cin, 3, 3] = sum over boards and in-grid cells of dy[b, p, co] x[b, p + off(t), ci]
+    (into `out` when given: a contiguous fp32 tensor of that shape, e.g. a parameter's .grad)."""
     for t, name in ((dy, "dy"), (x, "x")):
         if not (t.is_cuda and t.dtype == torch.bfloat16 and t.is_contiguous() and t.dim() == 3):
             raise ValueError("%s must be a contiguous bf16 CUDA tensor [B, 16, C]" % name)
@@ -96,7 +99,9 @@ def conv3x3_wgrad(dy, x):
     key = (cin, str(x.device))
     if key not in _WS:
         _WS[key] = torch.empty(L.r48_conv_wgrad_workspace_floats(cin), dtype=torch.float32, device=x.device)
-    dw = torch.empty((64, cin, 3, 3), dtype=torch.float32, device=x.device)
+    dw = torch.empty((64, cin, 3, 3), dtype=torch.float32, device=x.device) if out is None else out
+    if not (dw.dtype == torch.float32 and dw.is_contiguous() and dw.numel() == 64 * cin * 9):
+        raise ValueError("out must be a contiguous fp32 tensor of 64 x cin x 9")
     check(L.r48_conv3x3_wgrad(ptr(dy), ptr(x), B, cin, ptr(_WS[key]), ptr(dw), _stream(x)))
     return dw
 
@@ -142,8 +147,10 @@ def q_head_forward(h, w, b):
     return q
 
 
-def q_head_backward(dq, h, w):
-    """-> (dh bf16 [B, 1024], dw fp32 [4, 1024], db fp32 [4]); parameter gradients bf16-rounded."""
+def q_head_backward(dq, h, w, out=None):
+    """-> (dh bf16 [B, 1024], dw fp32 [4, 1024], db fp32 [4]); parameter gradients bf16-rounded,
+    written to `out` when given (fp32 storage of 4 * 1024 + 4 floats from its first element: the
+    weight rows, then the bias)."""
     L = _lib.load()
     key = str(h.device)
     if key not in _HEAD_WS:
@@ -151,7 +158,12 @@ def q_head_backward(dq, h, w):
     dq = dq.float().contiguous()
     wb = w.detach().to(torch.bfloat16).contiguous()
     dh = torch.empty_like(h)
-    g = torch.empty(4 * 1024 + 4, dtype=torch.float32, device=h.device)
+    if out is None:
+        g = torch.empty(4 * 1024 + 4, dtype=torch.float32, device=h.device)
+    else:
+        if not (out.dtype == torch.float32 and out.is_contiguous() and out.data_ptr() % 16 == 0):
+            raise ValueError("out must be contiguous 16-byte aligned fp32 storage")
+        g = torch.as_strided(out, (4 * 1024 + 4,), (1,))
     check(L.r48_q_head_backward(ptr(dq), ptr(h), h.shape[0], ptr(wb), ptr(dh), ptr(_HEAD_WS[key]), ptr(g),
                                 _stream(h)))
     return dh, g[:4096].view(4, 1024), g[4096:]
@@ -177,3 +189,30 @@ class QHead(torch.autograd.Function):
 def q_head(h, head):
     """The head Linear(16 C -> 4) `head` on bf16 activations h [B, 1024] (training)."""
     return QHead.apply(h.contiguous(), head.weight, head.bias)
+
+
+_PACK = {}
+
+
+def pack_resnet_train(convs):
+    """Forward fragments of the 9 convs (stem, conv1..8) and data-gradient fragments of conv1..8 in
+    one launch (r48_conv_pack_resnet) -> (fwd list of 9, dgrad list of 9 with None for the stem),
+    views of two blobs reused across calls (same layouts as pack_conv / pack_conv_dgrad)."""
+    ws = [c.weight for c in convs]
+    dev = ws[0].device
+    if len(ws) != 9 or ws[0].shape != (64, 18, 3, 3) or any(w.shape != (64, 64, 3, 3) for w in ws[1:]) or \
+            any(w.dtype != torch.float32 or not w.is_contiguous() for w in ws):
+        raise ValueError("pack_resnet_train needs the 9 contiguous fp32 conv weights of ResNet10Q (C = 64)")
+    key = (str(dev), tuple(w.data_ptr() for w in ws))
+    if key not in _PACK:
+        _PACK.clear()
+        fwd = torch.empty((36 + 8 * 72) * 512, dtype=torch.bfloat16, device=dev)
+        dg = torch.empty(8 * 72 * 512, dtype=torch.bfloat16, device=dev)
+        tab = torch.tensor([w.data_ptr() for w in ws], dtype=torch.int64, device=dev)
+        fv = [fwd[:36 * 512].view(36, 64, 8)] + [fwd[(36 + 72 * i) * 512:(36 + 72 * (i + 1)) * 512].view(72, 64, 8)
+                                                 for i in range(8)]
+        dv = [None] + [dg[72 * i * 512:72 * (i + 1) * 512].view(72, 64, 8) for i in range(8)]
+        _PACK[key] = (tab, fwd, dg, fv, dv)
+    tab, fwd, dg, fv, dv = _PACK[key]
+    check(_lib.load().r48_conv_pack_resnet(ptr(tab), ptr(fwd), ptr(dg), _stream(fwd)))
+    return fv, dv

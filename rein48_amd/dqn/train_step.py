@@ -1,0 +1,131 @@
+"""One training step of ResNet10Q (BASELINE config 5) with an explicit forward and backward on the
+GPU -- the same arithmetic as `loss.backward()` through nets.py's custom-conv path, without
+autograd's bookkeeping, and with the fusions it cannot express:
+
+  * every BN+ReLU forward writes a ReLU mask (1 bit per activation, r48_bn_forward `mask`), and
+    its backward reads the mask instead of the 16x larger BN output;
+  * a basic block's input gradient (first conv's data gradient + the identity path's gradient)
+    is summed in the data-gradient conv's epilogue (r48_conv3x3 `add`), not by a separate add;
+  * parameter gradients are written straight into their .grad views of the flat gradient buffer
+    (FlatParams): the convs' weight-gradient reduction, BN's dgamma/dbeta, the head's weight and
+    bias gradient (one record);
+  * activations live in buffers allocated once per batch size (9 conv outputs, 9 BN outputs).
+
+Semantics = DQNLearner.learn's autograd path: Huber (smooth L1, beta 1) loss of Q(x)[action]
+against the TD target, mean over the batch; BatchNorm in training mode (batch statistics, running
+statistics updated with momentum, num_batches_tracked + 1); conv biases are constants (every conv
+feeds a training-mode BN: their gradient is exactly zero). Differences from the autograd path are
+bf16 rounding order only (the fused residual sum rounds once instead of twice): tests/
+test_dqn_gpu.py::test_resnet_train_step_matches_autograd.
+"""
+import torch
+import torch.nn.functional as F
+
+from .. import _lib
+from .._lib import check, ptr
+from ..a3c.kernels import _stream
+from .bn import _workspace
+from .conv import conv3x3, conv3x3_wgrad, pack_resnet_train, q_head_backward, q_head_forward
+
+
+def supported(net):
+    """The fused step covers ResNet10Q with 64 channels, 4 blocks, BN, bf16 on the GPU."""
+    return (getattr(net, "channels", None) == 64 and getattr(net, "n_blocks", None) == 4 and net.use_bn
+            and net.dtype == torch.bfloat16 and next(net.parameters()).is_cuda)
+
+
+class ResNetTrainStep:
+    def __init__(self, net):
+        if not supported(net):
+            raise ValueError("ResNetTrainStep needs a bf16 CUDA ResNet10Q with 64 channels, 4 blocks and BN")
+        self.net = net
+        self._bufs = {}
+
+    def _buffers(self, B, dev):
+        key = (B, str(dev))
+        if key not in self._bufs:
+            act = lambda: torch.empty((B, 16, 64), dtype=torch.bfloat16, device=dev)   # noqa: E731
+            self._bufs.clear()            # one batch size at a time: the activations are large
+            self._bufs[key] = {
+                "y": [act() for _ in range(9)],                 # conv outputs (BN inputs)
+                "z": [act() for _ in range(9)],                 # BN+ReLU outputs (next conv inputs)
+                "m": [torch.empty((B * 16, 8), dtype=torch.uint8, device=dev) for _ in range(9)],
+                "save": [torch.empty(128, dtype=torch.float32, device=dev) for _ in range(9)],
+                "g": [act() for _ in range(6)],                 # gradient scratch
+                "stem_dw": torch.empty((64, 32, 3, 3), dtype=torch.float32, device=dev),
+            }
+        return self._bufs[key]
+
+    def _bn_forward(self, k, y, z, mask, save, residual=None):
+        bn = self.net.bns[k]
+        bn.num_batches_tracked.add_(1)
+        rows = y.numel() // 64
+        mom = bn.momentum if bn.momentum is not None else 0.1
+        check(_lib.load().r48_bn_forward(ptr(y), ptr(residual), rows, 64, ptr(bn.weight), ptr(bn.bias),
+                                         ptr(bn.running_mean), ptr(bn.running_var), float(mom), float(bn.eps), 1,
+                                         ptr(save), ptr(_workspace(rows, 64, y.device)), ptr(z), ptr(mask),
+                                         _stream(y)))
+
+    def _bn_backward(self, k, dz, mask, y, save, dy, dres=None):
+        bn = self.net.bns[k]
+        rows = y.numel() // 64
+        check(_lib.load().r48_bn_backward(ptr(dz), None, ptr(mask), ptr(y), rows, 64, ptr(bn.weight), ptr(save), 1,
+                                          ptr(_workspace(rows, 64, y.device)), ptr(dy), ptr(dres),
+                                          ptr(bn.weight.grad), ptr(bn.bias.grad), _stream(y)))
+
+    def __call__(self, x, action, target):
+        """x bf16 [B, 16 * 32] (board_onehot32 planes), action [B] (int), target fp32 [B] ->
+        (loss, mean Q(x)[action]) as 0-d tensors; gradients written into the parameters' .grad
+        (conv biases untouched: their gradient is zero)."""
+        net = self.net
+        B = x.shape[0]
+        x = x.reshape(B, 16, 32)
+        buf = self._buffers(B, x.device)
+        Y, Z, M, S, G = buf["y"], buf["z"], buf["m"], buf["save"], buf["g"]
+        convs = net.conv_layers()
+        fwd, dgrad = pack_resnet_train(convs)             # one launch, all 17 fragment sets
+        # ---- forward
+        conv3x3(x, fwd[0], convs[0].bias, out=Y[0])
+        self._bn_forward(0, Y[0], Z[0], M[0], S[0])
+        for b in range(4):
+            i1, i2 = 1 + 2 * b, 2 + 2 * b
+            h = Z[i1 - 1]
+            conv3x3(h, fwd[i1], convs[i1].bias, out=Y[i1])
+            self._bn_forward(i1, Y[i1], Z[i1], M[i1], S[i1])
+            conv3x3(Z[i1], fwd[i2], convs[i2].bias, out=Y[i2])
+            self._bn_forward(i2, Y[i2], Z[i2], M[i2], S[i2], residual=h)
+        h = Z[8].view(B, 1024)
+        q = q_head_forward(h, net.head.weight, net.head.bias)
+        # ---- Huber loss of Q(x)[action] and its gradient (d loss / d q)
+        a = action.long().view(-1, 1)
+        q_sa = q.gather(1, a).squeeze(1)
+        loss = F.smooth_l1_loss(q_sa, target)
+        dq = torch.zeros_like(q).scatter_(1, a, ((q_sa - target).clamp(-1.0, 1.0) / B).view(-1, 1))
+        # ---- backward
+        hw, hb = net.head.weight.grad, net.head.bias.grad
+        fused_head = hb.data_ptr() == hw.data_ptr() + 4 * hw.numel()        # one record: weight rows, bias
+        dh, dw, db = q_head_backward(dq, h, net.head.weight, out=hw if fused_head else None)
+        if not fused_head:
+            hw.copy_(dw)
+            hb.copy_(db)
+        # per block, backwards: BN2 (+ identity) -> conv2 data/weight gradients -> BN1 -> conv1
+        # data gradient + identity gradient (one epilogue) and weight gradient. The incoming
+        # gradient alternates between g[0] and g[5]; g[1..4] hold the block's temporaries.
+        cur = dh.view(B, 16, 64)
+        for b in range(3, -1, -1):
+            i1, i2 = 1 + 2 * b, 2 + 2 * b
+            h_in = Z[i1 - 1]
+            dy2, dres, dz1, dy1 = G[1], G[2], G[3], G[4]
+            self._bn_backward(i2, cur, M[i2], Y[i2], S[i2], dy2, dres=dres)
+            conv3x3(dy2, dgrad[i2], out=dz1)
+            conv3x3_wgrad(dy2, Z[i1], out=convs[i2].weight.grad)
+            self._bn_backward(i1, dz1, M[i1], Y[i1], S[i1], dy1)
+            nxt = G[5] if cur is G[0] else G[0]
+            conv3x3(dy1, dgrad[i1], add=dres, out=nxt)
+            conv3x3_wgrad(dy1, h_in, out=convs[i1].weight.grad)
+            cur = nxt
+        dy0 = G[1]
+        self._bn_backward(0, cur, M[0], Y[0], S[0], dy0)
+        conv3x3_wgrad(dy0, x, out=buf["stem_dw"])
+        convs[0].weight.grad.copy_(buf["stem_dw"][:, :convs[0].weight.shape[1]])
+        return loss.detach(), q_sa.detach().mean()

@@ -56,6 +56,7 @@ class DQNConfig:
     bf16: bool = True
     act_chunk: int = 1 << 18         # boards per Q forward while acting (PyTorch path)
     fused: bool = True               # eval-mode Q through r48_resnet_q_forward (bf16, C=64, 4 blocks)
+    fused_step: bool = True          # training step through train_step.ResNetTrainStep (bf16 GPU, C=64)
     seed: int = 0
 
 
@@ -100,6 +101,7 @@ class DQNLearner:
         for p in self.target.parameters():
             p.requires_grad_(False)
         self.opt = Adam(self.flat, cfg.lr)
+        self._train_step = None                           # train_step.ResNetTrainStep, built on first use
         self.updates = 0
         self._version = 0                                 # bumped by every optimizer step / sync
 
@@ -109,10 +111,17 @@ class DQNLearner:
         net follows every `target_sync` updates."""
         self.net.train()
         self.flat.zero_grad()
-        q = self.net(x)
-        q_sa = q.gather(1, action.long().view(-1, 1)).squeeze(1)
-        loss = F.smooth_l1_loss(q_sa, y)
-        loss.backward()
+        if self._fused_step_ok(x):
+            if self._train_step is None:
+                from .train_step import ResNetTrainStep
+                self._train_step = ResNetTrainStep(self.net)
+            loss, q_mean = self._train_step(x, action, y)
+        else:
+            q = self.net(x)
+            q_sa = q.gather(1, action.long().view(-1, 1)).squeeze(1)
+            loss = F.smooth_l1_loss(q_sa, y)
+            loss.backward()
+            q_mean = q_sa.detach().mean()
         self.flat.allreduce_grad()
         self.opt.step()
         self.bn_buffers.allreduce_mean_()
@@ -120,7 +129,16 @@ class DQNLearner:
         self.updates += 1
         if self.updates % self.cfg.target_sync == 0:
             self.sync_target()
-        return {"loss": float(loss.detach()), "q_mean": float(q_sa.detach().mean())}
+        return {"loss": float(loss.detach()), "q_mean": float(q_mean)}
+
+    def _fused_step_ok(self, x):
+        """The explicit fused step (train_step.py) takes the bf16 GPU net with the custom convs and
+        the padded 32-plane input; everything else goes through autograd."""
+        if not (self.cfg.fused_step and x.is_cuda and x.dim() == 2 and x.shape[1] == 16 * 32
+                and getattr(self.net, "custom_conv", False)):
+            return False
+        from .train_step import supported
+        return supported(self.net)
 
     def sync_target(self):
         self.target.load_state_dict(self.net.state_dict())

@@ -196,13 +196,18 @@ class Game:
     def _check(game_matrix):
         """(has_table_filled, has_game_over). On a non-square matrix the reference's game-over loop
         (GameClient.py:74-91) runs i and j over range(len(matrix)) = the row count: with fewer rows
-        than columns it only sees the leading rows x rows block, with more rows it indexes past the
-        end of a row (IndexError) -- reproduced here; has_table_filled (:96-100) scans every item."""
+        than columns it only sees the leading rows x rows block; with more rows its first row's last
+        column compares against m[0][cols] (IndexError) unless an equal pair met earlier in that
+        row's scan -- (0, j)-(0, j + 1) or (0, j)-(1, j) -- returned first; both reproduced here.
+        has_table_filled (:96-100) scans every item."""
         rows, cols = len(game_matrix), len(game_matrix[0])
         filled, over = Game._check_kernel(game_matrix)
         if rows == cols or not filled:
             return filled, over
         if rows > cols:
+            r0, r1 = game_matrix[0], game_matrix[1]
+            if any(r0[j] == r0[j + 1] for j in range(cols - 1)) or any(r0[j] == r1[j] for j in range(cols)):
+                return filled, False
             raise IndexError("list index out of range")
         return filled, Game._check_kernel([row[:rows] for row in game_matrix])[1]
 

@@ -484,3 +484,69 @@ def test_resnet_update_custom_conv_matches_structured_gemm():
     assert abs(losses[0] - losses[1]) <= 1e-2 * abs(losses[1])
     for ga, gb in zip(*grads):
         assert float((ga - gb).norm()) <= 5e-2 * float(gb.norm()) + 1e-6
+
+
+@pytest.mark.parametrize("B", [4096, 1000])
+def test_resnet_train_step_matches_autograd(B):
+    """train_step.ResNetTrainStep (explicit forward/backward: BN ReLU masks, the block-input
+    gradient summed in the data-gradient conv's epilogue, gradients straight into the flat buffer)
+    vs loss.backward() through nets.py's custom-conv autograd path on the same bf16 net: the
+    forward runs the same kernels, so the loss, Q and the BN running statistics are bit-identical;
+    gradients differ only by the rounding of the fused residual sum (once instead of twice in
+    bf16): relative norm <= 1e-2 per parameter, the head's gradients identical."""
+    from rein48_amd.a3c.optim import FlatParams
+    from rein48_amd.dqn.conv import board_onehot32
+    from rein48_amd.dqn.nets import ResNet10Q
+    from rein48_amd.dqn.train_step import ResNetTrainStep
+    torch.manual_seed(B)
+    net = ResNet10Q(dtype=torch.bfloat16).to(DEV).train()
+    with torch.no_grad():
+        net.head.weight.normal_(std=0.05)
+    flat = FlatParams(net)
+    rng = np.random.default_rng(B)
+    boards = torch.from_numpy(rng.integers(0, 14, size=(B, 16)).astype(np.int8)).to(DEV)
+    x = board_onehot32(boards).view(B, 512)
+    action = torch.from_numpy(rng.integers(0, 4, size=B).astype(np.int8)).to(DEV)
+    target = torch.from_numpy(rng.normal(size=B).astype(np.float32)).to(DEV)
+    stats0 = [(m.running_mean.clone(), m.running_var.clone()) for m in net.bns]
+    out = []
+    for fused in (False, True):
+        for m, (rm, rv) in zip(net.bns, stats0):
+            m.running_mean.copy_(rm)
+            m.running_var.copy_(rv)
+        flat.zero_grad()
+        if fused:
+            loss, q_mean = ResNetTrainStep(net)(x, action, target)
+        else:
+            q = net(x)
+            q_sa = q.gather(1, action.long().view(-1, 1)).squeeze(1)
+            loss = torch.nn.functional.smooth_l1_loss(q_sa, target)
+            loss.backward()
+            q_mean = q_sa.detach().mean()
+        out.append((float(loss), float(q_mean), [p.grad.detach().clone() for p in flat.params],
+                    [(m.running_mean.clone(), m.running_var.clone()) for m in net.bns]))
+    (la, qa, ga, sa), (lb, qb, gb, sb) = out
+    assert la == lb and qa == qb
+    for (ra, va), (rb, vb) in zip(sa, sb):
+        assert torch.equal(ra, rb) and torch.equal(va, vb)
+    names = [n for n, p in net.named_parameters() if p.requires_grad]
+    for n, a, b in zip(names, ga, gb):
+        if n.startswith("head"):
+            assert torch.equal(a, b), n
+        else:
+            assert float((a - b).norm()) <= 1e-2 * float(a.norm()) + 1e-9, n
+
+
+def test_conv_pack_resnet_matches_host_packing():
+    """r48_conv_pack_resnet (all 17 fragment sets of the update in one launch) is bit-identical to
+    pack_conv / pack_conv_dgrad per layer."""
+    from rein48_amd.dqn.conv import pack_conv, pack_conv_dgrad, pack_resnet_train
+    from rein48_amd.dqn.nets import ResNet10Q
+    torch.manual_seed(3)
+    net = ResNet10Q(dtype=torch.bfloat16).to(DEV)
+    convs = net.conv_layers()
+    fwd, dg = pack_resnet_train(convs)
+    for i, c in enumerate(convs):
+        assert torch.equal(fwd[i].view(-1), pack_conv(c.weight, 32 if i == 0 else 64).view(-1)), i
+        if i:
+            assert torch.equal(dg[i].view(-1), pack_conv_dgrad(c.weight).view(-1)), i

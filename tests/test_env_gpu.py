@@ -258,7 +258,7 @@ def test_game_over_on_non_square_matrices_follows_reference_loop(rows, cols):
     """has_game_over on rectangles (<= 4x4: r48_values_check; larger: r48_values_check_grid)
     reproduces the reference's square-index loop: columns past the row count are never compared,
     a zero anywhere means not over, and a filled matrix with more rows than columns raises
-    IndexError like the reference."""
+    IndexError like the reference unless its first row's scan meets an equal pair first."""
     from rein48_amd.game import Game
     rng = np.random.default_rng(rows * 31 + cols)
     for trial in range(40):
