@@ -294,6 +294,13 @@ int r48_egreedy_actions(const float *q, int64_t n, float eps, uint64_t seed, int
 int r48_td_target(const float *reward, const uint8_t *done, const float *q_next_target,
                   const float *q_next_online, int64_t n, float gamma, float *y, void *stream);
 
+/* Huber loss (smooth L1, beta 1) of the update: d = q[i][action[i]] - y[i]; out[0] = mean loss,
+ * out[1] = mean q[i][action[i]]; dq[i][a] = clamp(d, -1, 1) / n for a = action[i], else 0 (the
+ * gradient of the mean loss). q, dq float[n][4] 16-byte aligned; workspace float[512].
+ * Deterministic (fixed-order sums). Replaces trainer.py's gather + F.smooth_l1_loss + backward. */
+int r48_huber_grad(const float *q, const int8_t *action, const float *y, int64_t n, float *dq, float *out,
+                   float *workspace, void *stream);
+
 /* ---- The ResNet-10 update's 3x3 convolutions on the 4x4 grid (csrc/r48_conv.hip) ----
  * Channels-last bf16 activations [boards][16 cells][C], 64 output channels, 32 or 64 input
  * channels; only the 100 in-grid (cell, tap) pairs are computed. Replace the structured dense

@@ -95,8 +95,10 @@ int cu_count()
 // 16 boards one grid row at a time. Output row r needs input rows r - 1 .. r + 1, so the row
 // registers of a tile are refilled while it is still being computed: input rows 2 and 3 load under
 // output rows 0 and 1, and the NEXT tile's rows 0 and 1 load under output rows 2 and 3 (their
-// registers are free by then). A wave keeps 1-2 rows (8-16 KB) in flight behind its MFMAs.
+// registers are free by then). A wave keeps 1-2 rows (8-16 KB) in flight behind its MFMAs. Finished
+// output rows go through a per-wave LDS staging row so that they are stored in full 16-byte pieces.
 constexpr int kConvWaves = 8;
+constexpr int kOutPitch = 4 * 64 + 8;      // bf16 per board in the output-row staging (+16 B: banks)
 
 // ADD: y += add[b][p][co] (bf16, the same layout as y) before the bf16 rounding -- the data
 // gradient of a basic block's first conv plus the gradient of the identity path
@@ -111,6 +113,7 @@ __global__ __launch_bounds__(64 * kConvWaves, 1) void k_conv3x3(const uint16_t *
     constexpr int kCin = 32 * NC;
     __shared__ uint4 w_lds[kFrags * 64];
     __shared__ __attribute__((aligned(16))) float b_lds[kCout];
+    __shared__ __attribute__((aligned(16))) uint16_t o_lds[kConvWaves][16 * kOutPitch];
     for (int i = threadIdx.x; i < kFrags * 64; i += 64 * kConvWaves)
         w_lds[i] = wfrag[i];
     if (threadIdx.x < kCout)
@@ -123,6 +126,7 @@ __global__ __launch_bounds__(64 * kConvWaves, 1) void k_conv3x3(const uint16_t *
     int64_t tile = (int64_t)blockIdx.x * kConvWaves + wave;
     if (tile >= n_tiles)
         return;
+    uint16_t *orow = o_lds[wave];          // this wave's output row: 16 boards x 4 cells x 64 channels
     // xr[R][col][c]: input cell 4 R + col of this lane's board, channels 32 c + 8 g .. + 7
     uint4 xr[4][4][NC];
     auto load_row = [&](int64_t t, int R) {
@@ -140,7 +144,6 @@ __global__ __launch_bounds__(64 * kConvWaves, 1) void k_conv3x3(const uint16_t *
         const int64_t next = tile + stride;
         const int64_t b = tile * 16 + n;
         const bool live = b < boards;
-        uint16_t *yr = y + (live ? b : 0) * 16 * kCout + 4 * g;
 #pragma unroll
         for (int r = 0; r < 4; r++) {
             // rows r - 2 of this tile were last read by output row r - 1. Unconditional (the last
@@ -194,15 +197,23 @@ __global__ __launch_bounds__(64 * kConvWaves, 1) void k_conv3x3(const uint16_t *
                             acc[col][o][3] += __uint_as_float(ad[col][o].y & 0xFFFF0000u);
                         }
                 }
-                if (live) {
 #pragma unroll
-                    for (int col = 0; col < 4; col++)
+                for (int col = 0; col < 4; col++)
 #pragma unroll
-                        for (int o = 0; o < 2; o++)
-                            *reinterpret_cast<uint2 *>(yr + (4 * r + col) * kCout + 16 * (2 * oh + o)) =
-                                make_uint2(pack2(acc[col][o][0], acc[col][o][1]),
-                                           pack2(acc[col][o][2], acc[col][o][3]));
-                }
+                    for (int o = 0; o < 2; o++)
+                        *reinterpret_cast<uint2 *>(orow + n * kOutPitch + col * kCout + 16 * (2 * oh + o) + 4 * g) =
+                            make_uint2(pack2(acc[col][o][0], acc[col][o][1]), pack2(acc[col][o][2], acc[col][o][3]));
+            }
+            // the row leaves in 16-byte pieces, 1 KiB (two boards' 512-byte rows) per store
+            // instruction: 8-byte stores straight from the accumulator layout (16 boards x 32 bytes
+            // each) write at about 0.6 of the rate
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const int m = 64 * k + lane, bl = m >> 5, e = 8 * (m & 31);
+                const uint4 v = *reinterpret_cast<const uint4 *>(orow + bl * kOutPitch + e);
+                const int64_t bg = tile * 16 + bl;
+                if (bg < boards)
+                    *reinterpret_cast<uint4 *>(y + (bg * 16 + 4 * r) * kCout + e) = v;
             }
         }
     }
@@ -350,10 +361,11 @@ __global__ __launch_bounds__(64 * kWgWaves, 1) void k_conv_wgrad(const uint16_t 
                               lane);
         }
     };
-    auto compute = [&](int buf) {
+    static_assert(kKSteps == 2, "the step loop splits compute into its two k-steps");
+    auto compute = [&](int buf, int ks0, int ks1) {
         const uint16_t *img = lds + buf * kBuf;
 #pragma unroll
-        for (int ks = 0; ks < kKSteps; ks++) {
+        for (int ks = ks0; ks < ks1; ks++) {
             bf16x8 A[kCoT];
 #pragma unroll
             for (int j = 0; j < kCoT; j++)
@@ -395,8 +407,13 @@ __global__ __launch_bounds__(64 * kWgWaves, 1) void k_conv_wgrad(const uint16_t 
                 ximg[real * CIN + i] = 0;
             __syncthreads();
         }
-        stage(i + kRing - 1, (buf + kRing - 1) % kRing);          // buffer of step i - 1
-        compute(buf);
+        // the DMAs of step i + kRing - 1 (into the buffer of step i - 1) issue between the two
+        // k-steps, under the first one's MFMAs, not in a burst of all waves after the barrier
+        compute(buf, 0, 1);
+        __builtin_amdgcn_sched_barrier(0);
+        stage(i + kRing - 1, (buf + kRing - 1) % kRing);
+        __builtin_amdgcn_sched_barrier(0);
+        compute(buf, 1, 2);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");              // no DMA outlives the kernel
     // record: D[m = co 16][n = ci 16], lane l: column i16 (ci), rows 4g + i (co). 24 wait states

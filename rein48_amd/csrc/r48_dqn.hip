@@ -107,6 +107,71 @@ __global__ __launch_bounds__(kBlock) void k_td_target(const float *__restrict__ 
     y[i] = reward[i] + gamma * boot;
 }
 
+// ---- Huber loss of Q(s)[a] against the TD target and its gradient (DQNLearner.learn):
+// d = q[i][a_i] - y_i; loss = mean(0.5 d^2 if |d| < 1 else |d| - 0.5) (smooth L1, beta 1);
+// dq[i][a] = clamp(d, -1, 1) / n for a = a_i, else 0; also mean(q[i][a_i]). Per-block fp32 partials
+// in a fixed grid and order, summed by one block (deterministic).
+constexpr int kHuberBlocks = 256;
+
+__global__ __launch_bounds__(kBlock) void k_huber_grad(const float *__restrict__ q, const int8_t *__restrict__ action,
+                                                      const float *__restrict__ y, int64_t n, float *__restrict__ dq,
+                                                      float *__restrict__ part)
+{
+    __shared__ float red[2][kBlock];
+    float sl = 0.f, sq = 0.f;
+    const float inv_n = 1.0f / (float)n;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+        const float4 qi = reinterpret_cast<const float4 *>(q)[i];
+        const int a = action[i] & 3;
+        const float qa = pick(qi, (uint32_t)a);
+        const float d = qa - y[i], ad = fabsf(d);
+        sl += ad < 1.0f ? 0.5f * d * d : ad - 0.5f;
+        sq += qa;
+        const float g = fminf(fmaxf(d, -1.0f), 1.0f) * inv_n;
+        reinterpret_cast<float4 *>(dq)[i] =
+            make_float4(a == 0 ? g : 0.f, a == 1 ? g : 0.f, a == 2 ? g : 0.f, a == 3 ? g : 0.f);
+    }
+    red[0][threadIdx.x] = sl;
+    red[1][threadIdx.x] = sq;
+    __syncthreads();
+    for (int h = kBlock / 2; h > 0; h >>= 1) {
+        if ((int)threadIdx.x < h) {
+            red[0][threadIdx.x] += red[0][threadIdx.x + h];
+            red[1][threadIdx.x] += red[1][threadIdx.x + h];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        part[2 * blockIdx.x] = red[0][0];
+        part[2 * blockIdx.x + 1] = red[1][0];
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_huber_finish(const float *__restrict__ part, int nblk, int64_t n,
+                                                        float *__restrict__ out)
+{
+    __shared__ double red[2][kBlock];
+    double s0 = 0.0, s1 = 0.0;
+    for (int b = threadIdx.x; b < nblk; b += kBlock) {
+        s0 += (double)part[2 * b];
+        s1 += (double)part[2 * b + 1];
+    }
+    red[0][threadIdx.x] = s0;
+    red[1][threadIdx.x] = s1;
+    __syncthreads();
+    for (int h = kBlock / 2; h > 0; h >>= 1) {
+        if ((int)threadIdx.x < h) {
+            red[0][threadIdx.x] += red[0][threadIdx.x + h];
+            red[1][threadIdx.x] += red[1][threadIdx.x + h];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        out[0] = (float)(red[0][0] / (double)n);
+        out[1] = (float)(red[1][0] / (double)n);
+    }
+}
+
 // ---- structured 3x3 conv weight on the 4x4 grid (rein48_amd/dqn/nets.py dense_conv_weight)
 // dense[P co + o][Q ci + i] = w[o][i][dr + 1][dc + 1] when input cell Q = P + 4 dr + dc is one of
 // output cell P's in-grid 3x3 neighbours, else 0 (100 of the 256 (P, Q) blocks are nonzero). One
@@ -242,4 +307,17 @@ int r48_struct_conv_weight_grad(const void *gdense, int32_t co, int32_t ci, int3
     return launched("k_struct_weight_grad");
 }
 
+int r48_huber_grad(const float *q, const int8_t *action, const float *y, int64_t n, float *dq, float *out,
+                   float *workspace, void *stream)
+{
+    if (!q || !action || !y || !dq || !out || !workspace || n < 1 || !aligned16(q) || !aligned16(dq))
+        return fail(R48_EINVAL, "r48_huber_grad: NULL argument, n < 1 or q/dq not 16-byte aligned");
+    const int64_t want = (n + kBlock - 1) / kBlock;
+    const int nb = (int)(want < kHuberBlocks ? want : kHuberBlocks);
+    hipLaunchKernelGGL(k_huber_grad, dim3(nb), dim3(kBlock), 0, (hipStream_t)stream, q, action, y, n, dq, workspace);
+    hipLaunchKernelGGL(k_huber_finish, dim3(1), dim3(kBlock), 0, (hipStream_t)stream, workspace, nb, n, out);
+    return launched("k_huber_grad");
+}
+
 }  // extern "C"
+

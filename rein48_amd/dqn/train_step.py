@@ -19,7 +19,6 @@ bf16 rounding order only (the fused residual sum rounds once instead of twice): 
 test_dqn_gpu.py::test_resnet_train_step_matches_autograd.
 """
 import torch
-import torch.nn.functional as F
 
 from .. import _lib
 from .._lib import check, ptr
@@ -53,12 +52,13 @@ class ResNetTrainStep:
                 "save": [torch.empty(128, dtype=torch.float32, device=dev) for _ in range(9)],
                 "g": [act() for _ in range(6)],                 # gradient scratch
                 "stem_dw": torch.empty((64, 32, 3, 3), dtype=torch.float32, device=dev),
+                "loss": torch.empty(2, dtype=torch.float32, device=dev),        # mean loss, mean Q(s, a)
+                "huber_ws": torch.empty(512, dtype=torch.float32, device=dev),
             }
         return self._bufs[key]
 
     def _bn_forward(self, k, y, z, mask, save, residual=None):
         bn = self.net.bns[k]
-        bn.num_batches_tracked.add_(1)
         rows = y.numel() // 64
         mom = bn.momentum if bn.momentum is not None else 0.1
         check(_lib.load().r48_bn_forward(ptr(y), ptr(residual), rows, 64, ptr(bn.weight), ptr(bn.bias),
@@ -85,6 +85,7 @@ class ResNetTrainStep:
         convs = net.conv_layers()
         fwd, dgrad = pack_resnet_train(convs)             # one launch, all 17 fragment sets
         # ---- forward
+        torch._foreach_add_([m.num_batches_tracked for m in net.bns], 1)   # one launch for the 9 BNs
         conv3x3(x, fwd[0], convs[0].bias, out=Y[0])
         self._bn_forward(0, Y[0], Z[0], M[0], S[0])
         for b in range(4):
@@ -96,11 +97,12 @@ class ResNetTrainStep:
             self._bn_forward(i2, Y[i2], Z[i2], M[i2], S[i2], residual=h)
         h = Z[8].view(B, 1024)
         q = q_head_forward(h, net.head.weight, net.head.bias)
-        # ---- Huber loss of Q(x)[action] and its gradient (d loss / d q)
-        a = action.long().view(-1, 1)
-        q_sa = q.gather(1, a).squeeze(1)
-        loss = F.smooth_l1_loss(q_sa, target)
-        dq = torch.zeros_like(q).scatter_(1, a, ((q_sa - target).clamp(-1.0, 1.0) / B).view(-1, 1))
+        # ---- Huber loss of Q(x)[action] and its gradient (d loss / d q): one kernel + one finish
+        a8 = action if action.dtype == torch.int8 else action.to(torch.int8)
+        dq = torch.empty_like(q)
+        stats = buf["loss"]
+        check(_lib.load().r48_huber_grad(ptr(q), ptr(a8.contiguous()), ptr(target.float().contiguous()), B, ptr(dq),
+                                         ptr(stats), ptr(buf["huber_ws"]), _stream(q)))
         # ---- backward
         hw, hb = net.head.weight.grad, net.head.bias.grad
         fused_head = hb.data_ptr() == hw.data_ptr() + 4 * hw.numel()        # one record: weight rows, bias
@@ -128,4 +130,4 @@ class ResNetTrainStep:
         self._bn_backward(0, cur, M[0], Y[0], S[0], dy0)
         conv3x3_wgrad(dy0, x, out=buf["stem_dw"])
         convs[0].weight.grad.copy_(buf["stem_dw"][:, :convs[0].weight.shape[1]])
-        return loss.detach(), q_sa.detach().mean()
+        return stats[0], stats[1]

@@ -491,9 +491,10 @@ def test_resnet_train_step_matches_autograd(B):
     """train_step.ResNetTrainStep (explicit forward/backward: BN ReLU masks, the block-input
     gradient summed in the data-gradient conv's epilogue, gradients straight into the flat buffer)
     vs loss.backward() through nets.py's custom-conv autograd path on the same bf16 net: the
-    forward runs the same kernels, so the loss, Q and the BN running statistics are bit-identical;
-    gradients differ only by the rounding of the fused residual sum (once instead of twice in
-    bf16): relative norm <= 1e-2 per parameter, the head's gradients identical."""
+    forward runs the same kernels, so Q and the BN running statistics are bit-identical and the loss
+    (r48_huber_grad's fixed-order sum vs torch's reduction) agrees to 1e-6; gradients differ only by
+    the rounding of the fused residual sum (once instead of twice in bf16): relative norm <= 1e-2 per
+    parameter, the head's gradients identical."""
     from rein48_amd.a3c.optim import FlatParams
     from rein48_amd.dqn.conv import board_onehot32
     from rein48_amd.dqn.nets import ResNet10Q
@@ -526,7 +527,7 @@ def test_resnet_train_step_matches_autograd(B):
         out.append((float(loss), float(q_mean), [p.grad.detach().clone() for p in flat.params],
                     [(m.running_mean.clone(), m.running_var.clone()) for m in net.bns]))
     (la, qa, ga, sa), (lb, qb, gb, sb) = out
-    assert la == lb and qa == qb
+    assert abs(la - lb) <= 1e-6 * abs(la) and abs(qa - qb) <= 1e-6 * abs(qa) + 1e-7
     for (ra, va), (rb, vb) in zip(sa, sb):
         assert torch.equal(ra, rb) and torch.equal(va, vb)
     names = [n for n, p in net.named_parameters() if p.requires_grad]

@@ -17,9 +17,21 @@ B = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 16
 libs = sys.argv[2:] or [_lib.LIB_PATH]
 dev = torch.device("cuda:0")
 g = torch.Generator(device="cpu").manual_seed(0)
-x64 = torch.randn(B, 16, 64, generator=g).to(dev, torch.bfloat16)
-x32 = torch.randn(B, 16, 32, generator=g).to(dev, torch.bfloat16)
-dy = torch.randn(B, 16, 64, generator=g).to(dev, torch.bfloat16)
+# three copies of every input, used in rotation: successive calls read 3 x the Infinity Cache's
+# 256 MiB apart at 64K boards (HBM rates, as inside an update), not a cache-resident tensor
+NR = 3
+x64s = [torch.randn(B, 16, 64, generator=g).to(dev, torch.bfloat16) for _ in range(NR)]
+x32s = [torch.randn(B, 16, 32, generator=g).to(dev, torch.bfloat16) for _ in range(NR)]
+dys = [torch.randn(B, 16, 64, generator=g).to(dev, torch.bfloat16) for _ in range(NR)]
+x64, x32, dy = x64s[0], x32s[0], dys[0]
+_rot = [0]
+
+
+def rot(lst):
+    _rot[0] += 1
+    return lst[_rot[0] % NR]
+
+
 w64 = torch.randn(64, 64, 3, 3, generator=g).to(dev) * 0.05
 w32 = torch.randn(64, 32, 3, 3, generator=g).to(dev) * 0.05
 bias = torch.randn(64, generator=g).to(dev)
@@ -45,15 +57,17 @@ def timed(fn, reps=20):
 
 
 # algorithmic HBM bytes: activations in + out (bf16); wgrad reads dy and x
-io = {"fwd64": B * 16 * (64 + 64) * 2, "fwd32": B * 16 * (32 + 64) * 2,
+io = {"fwd64": B * 16 * (64 + 64) * 2, "fwd32": B * 16 * (32 + 64) * 2, "add64": B * 16 * (64 + 64 + 64) * 2,
       "wgrad64": B * 16 * (64 + 64) * 2, "wgrad32": B * 16 * (64 + 32) * 2}
 for path in libs:
     _lib.LIB_PATH, _lib._lib = path, None
     C._WS.clear()
-    runs = {"fwd64": lambda: C.conv3x3(x64, f64, bias), "fwd32": lambda: C.conv3x3(x32, f32, bias),
-            "wgrad64": lambda: C.conv3x3_wgrad(dy, x64), "wgrad32": lambda: C.conv3x3_wgrad(dy, x32)}
+    runs = {"fwd64": lambda: C.conv3x3(rot(x64s), f64, bias), "fwd32": lambda: C.conv3x3(rot(x32s), f32, bias),
+            "add64": lambda: C.conv3x3(rot(x64s), f64, bias, add=rot(dys)),
+            "wgrad64": lambda: C.conv3x3_wgrad(rot(dys), rot(x64s)), "wgrad32": lambda: C.conv3x3_wgrad(rot(dys), rot(x32s))}
     line = []
     for k, fn in runs.items():
+        _rot[0] = -1
         out = fn()
         torch.cuda.synchronize()
         us = timed(fn)
