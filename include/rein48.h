@@ -312,9 +312,12 @@ int r48_board_onehot32(const int8_t *boards, int64_t n, void *out, void *stream)
  * (+ add[b][p][co]) (the forward conv; with the flipped, transposed taps the data gradient).
  * wfrag: 9 x 4 x (cin/32) MFMA A fragments of 1 KiB (rein48_amd/dqn/conv.py pack_conv); bias fp32
  * [64] or NULL; add bf16 [boards][16][64] or NULL (cin 64 only: a basic block's input gradient
- * summed in the epilogue). All pointers 16-byte aligned. */
+ * summed in the epilogue). stats (NULL, or float[r48_conv_stats_floats()]; not with add): the
+ * per-channel sum and sum of squares of the bf16 outputs, one record [S1 64][S2 64] per CU, for
+ * r48_bn_forward_stats. All pointers 16-byte aligned. */
+int64_t r48_conv_stats_floats(void);
 int r48_conv3x3(const void *x, int64_t boards, int32_t cin, const void *wfrag, const float *bias, const void *add,
-                void *y, void *stream);
+                void *y, float *stats, void *stream);
 /* dw fp32 [64][cin][3][3] = sum over boards and in-grid cells of dy[b][p][co] x[b][p + off(t)][ci];
  * workspace of r48_conv_wgrad_workspace_floats(cin) floats (per-workgroup records, summed in a
  * fixed order: deterministic). */
@@ -380,6 +383,13 @@ int64_t r48_bn_workspace_floats(int64_t rows, int32_t C);
 int r48_bn_forward(const void *x, const void *residual, int64_t rows, int32_t C, const float *gamma,
                    const float *beta, float *running_mean, float *running_var, float momentum, float eps,
                    int32_t relu, float *save, float *workspace, void *y, uint8_t *mask, void *stream);
+/* The forward from statistics a producer already summed (r48_conv3x3 `stats`: nblk records of
+ * unshifted [S1 C][S2 C] sums over x): finish (mean, invstd, running statistics) + apply, as
+ * r48_bn_forward without its statistics pass over x. */
+int r48_bn_forward_stats(const float *part, int32_t nblk, const void *x, const void *residual, int64_t rows, int32_t C,
+                         const float *gamma, const float *beta, float *running_mean, float *running_var,
+                         float momentum, float eps, int32_t relu, float *save, float *workspace, void *y, uint8_t *mask,
+                         void *stream);
 int r48_bn_backward(const void *dy, const void *y, const uint8_t *mask, const void *x, int64_t rows, int32_t C,
                     const float *gamma, const float *save, int32_t relu, float *workspace, void *dx, void *dresidual,
                     float *dgamma, float *dbeta, void *stream);

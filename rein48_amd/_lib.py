@@ -37,10 +37,13 @@ SIGNATURES = {
     "r48_bn_workspace_floats": (_I64, [_I64, _I32]),
     "r48_bn_forward": (C.c_int, [_P, _P, _I64, _I32, _P, _P, _P, _P, C.c_float, C.c_float, _I32, _P, _P, _P, _P,
                                  _P]),
+    "r48_bn_forward_stats": (C.c_int, [_P, _I32, _P, _P, _I64, _I32, _P, _P, _P, _P, C.c_float, C.c_float, _I32, _P,
+                                       _P, _P, _P, _P]),
     "r48_bn_backward": (C.c_int, [_P, _P, _P, _P, _I64, _I32, _P, _P, _I32, _P, _P, _P, _P, _P, _P]),
     "r48_board_onehot": (C.c_int, [_P, _I64, _I32, _P, _P]),
     "r48_board_onehot32": (C.c_int, [_P, _I64, _P, _P]),
-    "r48_conv3x3": (C.c_int, [_P, _I64, _I32, _P, _P, _P, _P, _P]),
+    "r48_conv3x3": (C.c_int, [_P, _I64, _I32, _P, _P, _P, _P, _P, _P]),
+    "r48_conv_stats_floats": (_I64, []),
     "r48_conv_wgrad_workspace_floats": (_I64, [_I32]),
     "r48_conv3x3_wgrad": (C.c_int, [_P, _P, _I64, _I32, _P, _P, _P]),
     "r48_q_head_forward": (C.c_int, [_P, _I64, _P, _P, _P, _P]),

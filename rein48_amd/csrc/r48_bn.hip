@@ -210,7 +210,7 @@ __global__ __launch_bounds__(kBlock) void k_bn_finish(const uint16_t *__restrict
     channel_totals(part, nblk, C, c, s1, s2);
     if (threadIdx.x != 0)
         return;
-    const double x0 = (double)__uint_as_float((uint32_t)x[c] << 16);
+    const double x0 = x ? (double)__uint_as_float((uint32_t)x[c] << 16) : 0.0;   // shift (NULL: unshifted sums)
     const double n = (double)rows;
     const double dm = s1 / n;
     double var = s2 / n - dm * dm;                 // biased (normalisation), as BN training mode
@@ -481,6 +481,26 @@ int forward_c(const uint16_t *x, const uint16_t *res, int64_t rows, const float 
     return launched("k_bn_apply");
 }
 
+// finish + apply from per-block sums a producer computed (r48_conv3x3 `stats`: unshifted)
+template <int C>
+int forward_stats_c(const float *part, int nblk, const uint16_t *x, const uint16_t *res, int64_t rows,
+                    const float *gamma, const float *beta, float *rm, float *rv, float momentum, float eps, int relu,
+                    float *save, float *coef, uint16_t *y, uint8_t *mask, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_bn_finish, dim3(C), dim3(kBlock), 0, s, nullptr, part, nblk, C, rows, gamma, beta, rm, rv,
+                       momentum, eps, save, coef);
+    const dim3 g(apply_blocks(rows, C));
+    if (relu && res)
+        launch_apply<C, true, true>(g, s, x, res, rows, coef, y, mask);
+    else if (relu)
+        launch_apply<C, true, false>(g, s, x, res, rows, coef, y, mask);
+    else if (res)
+        launch_apply<C, false, true>(g, s, x, res, rows, coef, y, mask);
+    else
+        launch_apply<C, false, false>(g, s, x, res, rows, coef, y, mask);
+    return launched("k_bn_apply");
+}
+
 template <int C, bool RELU, bool MASK>
 void launch_bwd(int nb, dim3 g, hipStream_t s, const uint16_t *dy, const uint16_t *y, const uint8_t *mask,
                 const uint16_t *x, int64_t rows, const float *gamma, const float *save, float *ws, float *coef,
@@ -547,6 +567,35 @@ int r48_bn_forward(const void *x, const void *residual, int64_t rows, int32_t C,
     default:
         return forward_c<128>(xs, rs, rows, gamma, beta, running_mean, running_var, momentum, eps, relu, save,
                               workspace, (uint16_t *)y, mask, s);
+    }
+}
+
+int r48_bn_forward_stats(const float *part, int32_t nblk, const void *x, const void *residual, int64_t rows, int32_t C,
+                         const float *gamma, const float *beta, float *running_mean, float *running_var,
+                         float momentum, float eps, int32_t relu, float *save, float *workspace, void *y, uint8_t *mask,
+                         void *stream)
+{
+    int rc = check_args(x, rows, C);
+    if (rc)
+        return rc;
+    if (!part || nblk < 1 || !gamma || !beta || !save || !workspace || !y || !aligned16(y) ||
+        (residual && !aligned16(residual)))
+        return fail(R48_EINVAL, "r48_bn_forward_stats: null or misaligned argument");
+    if ((running_mean == nullptr) != (running_var == nullptr))
+        return fail(R48_EINVAL, "r48_bn_forward_stats: running_mean and running_var go together");
+    const uint16_t *xs = (const uint16_t *)x, *rs = (const uint16_t *)residual;
+    hipStream_t s = (hipStream_t)stream;
+    float *coef = workspace + (int64_t)reduce_blocks(rows, C) * 2 * C;
+    switch (C) {
+    case 32:
+        return forward_stats_c<32>(part, nblk, xs, rs, rows, gamma, beta, running_mean, running_var, momentum, eps,
+                                   relu, save, coef, (uint16_t *)y, mask, s);
+    case 64:
+        return forward_stats_c<64>(part, nblk, xs, rs, rows, gamma, beta, running_mean, running_var, momentum, eps,
+                                   relu, save, coef, (uint16_t *)y, mask, s);
+    default:
+        return forward_stats_c<128>(part, nblk, xs, rs, rows, gamma, beta, running_mean, running_var, momentum, eps,
+                                    relu, save, coef, (uint16_t *)y, mask, s);
     }
 }
 

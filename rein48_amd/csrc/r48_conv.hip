@@ -101,19 +101,26 @@ constexpr int kConvWaves = 8;
 constexpr int kOutPitch = 4 * 64 + 8;      // bf16 per board in the output-row staging (+16 B: banks)
 
 // ADD: y += add[b][p][co] (bf16, the same layout as y) before the bf16 rounding -- the data
-// gradient of a basic block's first conv plus the gradient of the identity path
-template <int NC, bool ADD>
+// gradient of a basic block's first conv plus the gradient of the identity path.
+// STATS: the per-channel sums S1 = sum y, S2 = sum y^2 of the bf16 outputs (the statistics of the
+// training-mode BN that follows), accumulated from the staged 16-byte pieces (a lane's pieces are
+// always the same 8 channels), one record [S1 64][S2 64] per workgroup (the grid is then exactly
+// one workgroup per CU, idle ones write zeros). Passes of PO row tiles: 2, or 1 with STATS to
+// make room for its 16 accumulators.
+template <int NC, bool ADD, bool STATS>
 __global__ __launch_bounds__(64 * kConvWaves, 1) void k_conv3x3(const uint16_t *__restrict__ x, int64_t boards,
                                                                const uint4 *__restrict__ wfrag,
                                                                const float *__restrict__ bias,
                                                                const uint16_t *__restrict__ add,
-                                                               uint16_t *__restrict__ y)
+                                                               uint16_t *__restrict__ y, float *__restrict__ stats)
 {
+    constexpr int PO = STATS ? 1 : 2;
     constexpr int kFrags = 9 * 4 * NC;
     constexpr int kCin = 32 * NC;
     __shared__ uint4 w_lds[kFrags * 64];
     __shared__ __attribute__((aligned(16))) float b_lds[kCout];
     __shared__ __attribute__((aligned(16))) uint16_t o_lds[kConvWaves][16 * kOutPitch];
+    __shared__ float st_lds[STATS ? kConvWaves : 1][8][16];
     for (int i = threadIdx.x; i < kFrags * 64; i += 64 * kConvWaves)
         w_lds[i] = wfrag[i];
     if (threadIdx.x < kCout)
@@ -124,9 +131,10 @@ __global__ __launch_bounds__(64 * kConvWaves, 1) void k_conv3x3(const uint16_t *
     const int64_t n_tiles = (boards + 15) / 16;
     const int64_t stride = (int64_t)gridDim.x * kConvWaves;
     int64_t tile = (int64_t)blockIdx.x * kConvWaves + wave;
-    if (tile >= n_tiles)
+    if (!STATS && tile >= n_tiles)
         return;
     uint16_t *orow = o_lds[wave];          // this wave's output row: 16 boards x 4 cells x 64 channels
+    float s1[8] = {}, s2[8] = {};          // STATS: channels 8 (lane & 7) .. + 7
     // xr[R][col][c]: input cell 4 R + col of this lane's board, channels 32 c + 8 g .. + 7
     uint4 xr[4][4][NC];
     auto load_row = [&](int64_t t, int R) {
@@ -138,8 +146,10 @@ __global__ __launch_bounds__(64 * kConvWaves, 1) void k_conv3x3(const uint16_t *
             for (int c = 0; c < NC; c++)
                 xr[R][col][c] = *reinterpret_cast<const uint4 *>(src + col * kCin + 32 * c);
     };
-    load_row(tile, 0);
-    load_row(tile, 1);
+    if (tile < n_tiles) {
+        load_row(tile, 0);
+        load_row(tile, 1);
+    }
     for (; tile < n_tiles; tile += stride) {
         const int64_t next = tile + stride;
         const int64_t b = tile * 16 + n;
@@ -152,16 +162,16 @@ __global__ __launch_bounds__(64 * kConvWaves, 1) void k_conv3x3(const uint16_t *
             load_row(r < 2 ? tile : (next < n_tiles ? next : tile), r < 2 ? r + 2 : r - 2);
             __builtin_amdgcn_sched_barrier(0);   // issue the row loads here, ahead of this row's MFMAs
 #pragma unroll
-            for (int oh = 0; oh < 2; oh++) {   // two passes of two row tiles: 32 accumulator registers
-                f32x4 acc[4][2];               // [output column][row tile 2 oh + o]
-                uint2 ad[4][2];
+            for (int oh = 0; oh < 4 / PO; oh++) {   // passes of PO row tiles
+                f32x4 acc[4][PO];                    // [output column][row tile PO oh + o]
+                uint2 ad[4][PO];
                 if (ADD) {
                     const uint16_t *ar = add + (live ? b : 0) * 16 * kCout + 4 * g;
 #pragma unroll
                     for (int col = 0; col < 4; col++)
 #pragma unroll
-                        for (int o = 0; o < 2; o++)
-                            ad[col][o] = *reinterpret_cast<const uint2 *>(ar + (4 * r + col) * kCout + 16 * (2 * oh + o));
+                        for (int o = 0; o < PO; o++)
+                            ad[col][o] = *reinterpret_cast<const uint2 *>(ar + (4 * r + col) * kCout + 16 * (PO * oh + o));
                 }
 #pragma unroll
                 for (int k = 0; k < 9 * NC; k++) {
@@ -169,19 +179,19 @@ __global__ __launch_bounds__(64 * kConvWaves, 1) void k_conv3x3(const uint16_t *
                     const int dr = t / 3 - 1, dc = t % 3 - 1;
                     if (r + dr < 0 || r + dr > 3)
                         continue;
-                    bf16x8 A[2];
+                    bf16x8 A[PO];
 #pragma unroll
-                    for (int o = 0; o < 2; o++)
-                        A[o] = as_frag(w_lds[((t * 4 + 2 * oh + o) * NC + c) * 64 + lane]);
+                    for (int o = 0; o < PO; o++)
+                        A[o] = as_frag(w_lds[((t * 4 + PO * oh + o) * NC + c) * 64 + lane]);
 #pragma unroll
                     for (int col = 0; col < 4; col++) {
                         if (col + dc < 0 || col + dc > 3)
                             continue;
 #pragma unroll
-                        for (int o = 0; o < 2; o++)
+                        for (int o = 0; o < PO; o++)
                             acc[col][o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
                                 A[o], as_frag(xr[r + dr][col + dc][c]),
-                                k == 0 ? *reinterpret_cast<const f32x4 *>(b_lds + 16 * (2 * oh + o) + 4 * g)
+                                k == 0 ? *reinterpret_cast<const f32x4 *>(b_lds + 16 * (PO * oh + o) + 4 * g)
                                        : acc[col][o],
                                 0, 0, 0);
                     }
@@ -190,7 +200,7 @@ __global__ __launch_bounds__(64 * kConvWaves, 1) void k_conv3x3(const uint16_t *
 #pragma unroll
                     for (int col = 0; col < 4; col++)
 #pragma unroll
-                        for (int o = 0; o < 2; o++) {
+                        for (int o = 0; o < PO; o++) {
                             acc[col][o][0] += __uint_as_float(ad[col][o].x << 16);
                             acc[col][o][1] += __uint_as_float(ad[col][o].x & 0xFFFF0000u);
                             acc[col][o][2] += __uint_as_float(ad[col][o].y << 16);
@@ -200,8 +210,8 @@ __global__ __launch_bounds__(64 * kConvWaves, 1) void k_conv3x3(const uint16_t *
 #pragma unroll
                 for (int col = 0; col < 4; col++)
 #pragma unroll
-                    for (int o = 0; o < 2; o++)
-                        *reinterpret_cast<uint2 *>(orow + n * kOutPitch + col * kCout + 16 * (2 * oh + o) + 4 * g) =
+                    for (int o = 0; o < PO; o++)
+                        *reinterpret_cast<uint2 *>(orow + n * kOutPitch + col * kCout + 16 * (PO * oh + o) + 4 * g) =
                             make_uint2(pack2(acc[col][o][0], acc[col][o][1]), pack2(acc[col][o][2], acc[col][o][3]));
             }
             // the row leaves in 16-byte pieces, 1 KiB (two boards' 512-byte rows) per store
@@ -212,9 +222,47 @@ __global__ __launch_bounds__(64 * kConvWaves, 1) void k_conv3x3(const uint16_t *
                 const int m = 64 * k + lane, bl = m >> 5, e = 8 * (m & 31);
                 const uint4 v = *reinterpret_cast<const uint4 *>(orow + bl * kOutPitch + e);
                 const int64_t bg = tile * 16 + bl;
-                if (bg < boards)
+                if (bg < boards) {
                     *reinterpret_cast<uint4 *>(y + (bg * 16 + 4 * r) * kCout + e) = v;
+                    if (STATS) {
+                        const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                        for (int q = 0; q < 4; q++) {
+                            const float lo = __uint_as_float(w4[q] << 16), hi = __uint_as_float(w4[q] & 0xFFFF0000u);
+                            s1[2 * q] += lo;
+                            s2[2 * q] = __builtin_fmaf(lo, lo, s2[2 * q]);
+                            s1[2 * q + 1] += hi;
+                            s2[2 * q + 1] = __builtin_fmaf(hi, hi, s2[2 * q + 1]);
+                        }
+                    }
+                }
             }
+        }
+    }
+    if (STATS) {
+        // lanes l, l ^ 8, l ^ 16, l ^ 32 ... share channels 8 (l & 7) .. + 7: fixed-order butterfly,
+        // then the 8 waves in wave order
+#pragma unroll
+        for (int m = 8; m < 64; m <<= 1)
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                s1[k] += __shfl_xor(s1[k], m);
+                s2[k] += __shfl_xor(s2[k], m);
+            }
+        if (lane < 8)
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                st_lds[wave][lane][k] = s1[k];
+                st_lds[wave][lane][8 + k] = s2[k];
+            }
+        __syncthreads();
+        if (threadIdx.x < 2 * kCout) {
+            const int v = threadIdx.x >> 6, c = threadIdx.x & 63;
+            float t = 0.f;
+#pragma unroll
+            for (int w = 0; w < kConvWaves; w++)
+                t += st_lds[w][c >> 3][8 * v + (c & 7)];
+            stats[(int64_t)blockIdx.x * 2 * kCout + threadIdx.x] = t;
         }
     }
 }
@@ -769,29 +817,36 @@ int r48_board_onehot32(const int8_t *boards, int64_t n, void *out, void *stream)
     return launched("k_onehot32");
 }
 
+int64_t r48_conv_stats_floats(void) { return (int64_t)cu_count() * 2 * kCout; }
+
 int r48_conv3x3(const void *x, int64_t boards, int32_t cin, const void *wfrag, const float *bias, const void *add,
-                void *y, void *stream)
+                void *y, float *stats, void *stream)
 {
     if (!x || !wfrag || !y || boards < 1 || (cin != 32 && cin != 64))
         return fail(R48_EINVAL, "r48_conv3x3: NULL argument, boards < 1 or cin not 32/64");
     if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(wfrag) | reinterpret_cast<uintptr_t>(y) |
          reinterpret_cast<uintptr_t>(bias) | reinterpret_cast<uintptr_t>(add)) & 15u)
         return fail(R48_EINVAL, "r48_conv3x3: x, wfrag, bias, add and y must be 16-byte aligned");
-    if (add && cin != 64)
-        return fail(R48_EINVAL, "r48_conv3x3: add needs 64 input channels");
+    if (add && (cin != 64 || stats))
+        return fail(R48_EINVAL, "r48_conv3x3: add needs 64 input channels and no stats");
     const int64_t tiles = (boards + 15) / 16;
     const int64_t want = (tiles + kConvWaves - 1) / kConvWaves;
-    const int grid = (int)(want < cu_count() ? want : cu_count());
-    const uint16_t *a = (const uint16_t *)add;
+    const int grid = stats ? cu_count() : (int)(want < cu_count() ? want : cu_count());
+    const uint16_t *xs = (const uint16_t *)x, *a = (const uint16_t *)add;
+    const uint4 *wf = (const uint4 *)wfrag;
+    uint16_t *ys = (uint16_t *)y;
+    const dim3 g(grid), blk(64 * kConvWaves);
+    hipStream_t s = (hipStream_t)stream;
     if (cin == 64 && add)
-        hipLaunchKernelGGL((k_conv3x3<2, true>), dim3(grid), dim3(64 * kConvWaves), 0, (hipStream_t)stream,
-                           (const uint16_t *)x, boards, (const uint4 *)wfrag, bias, a, (uint16_t *)y);
+        hipLaunchKernelGGL((k_conv3x3<2, true, false>), g, blk, 0, s, xs, boards, wf, bias, a, ys, stats);
+    else if (cin == 64 && stats)
+        hipLaunchKernelGGL((k_conv3x3<2, false, true>), g, blk, 0, s, xs, boards, wf, bias, a, ys, stats);
     else if (cin == 64)
-        hipLaunchKernelGGL((k_conv3x3<2, false>), dim3(grid), dim3(64 * kConvWaves), 0, (hipStream_t)stream,
-                           (const uint16_t *)x, boards, (const uint4 *)wfrag, bias, a, (uint16_t *)y);
+        hipLaunchKernelGGL((k_conv3x3<2, false, false>), g, blk, 0, s, xs, boards, wf, bias, a, ys, stats);
+    else if (stats)
+        hipLaunchKernelGGL((k_conv3x3<1, false, true>), g, blk, 0, s, xs, boards, wf, bias, a, ys, stats);
     else
-        hipLaunchKernelGGL((k_conv3x3<1, false>), dim3(grid), dim3(64 * kConvWaves), 0, (hipStream_t)stream,
-                           (const uint16_t *)x, boards, (const uint4 *)wfrag, bias, a, (uint16_t *)y);
+        hipLaunchKernelGGL((k_conv3x3<1, false, false>), g, blk, 0, s, xs, boards, wf, bias, a, ys, stats);
     return launched("k_conv3x3");
 }
 

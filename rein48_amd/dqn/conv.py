@@ -72,8 +72,9 @@ def board_onehot32(boards, out=None):
     return out
 
 
-def conv3x3(x, frags, bias=None, add=None, out=None):
-    """x bf16 [B, 16, cin] (cin 32 or 64) -> y bf16 [B, 16, 64] (+ add, bf16 [B, 16, 64])."""
+def conv3x3(x, frags, bias=None, add=None, out=None, stats=None):
+    """x bf16 [B, 16, cin] (cin 32 or 64) -> y bf16 [B, 16, 64] (+ add, bf16 [B, 16, 64]); stats: a
+    float[r48_conv_stats_floats()] buffer that receives the per-CU [S1 64][S2 64] sums of y."""
     if not (x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous() and x.dim() == 3 and x.shape[1] == 16):
         raise ValueError("x must be a contiguous bf16 CUDA tensor [B, 16, cin]")
     B, _, cin = x.shape
@@ -81,7 +82,7 @@ def conv3x3(x, frags, bias=None, add=None, out=None):
         raise ValueError("add must be a contiguous bf16 tensor of B x 16 x 64")
     y = torch.empty((B, 16, 64), dtype=torch.bfloat16, device=x.device) if out is None else out
     b = None if bias is None else bias.detach().float().contiguous()
-    check(_lib.load().r48_conv3x3(ptr(x), B, cin, ptr(frags), ptr(b), ptr(add), ptr(y), _stream(x)))
+    check(_lib.load().r48_conv3x3(ptr(x), B, cin, ptr(frags), ptr(b), ptr(add), ptr(y), ptr(stats), _stream(x)))
     return y
 
 

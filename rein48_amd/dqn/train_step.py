@@ -2,6 +2,8 @@
 GPU -- the same arithmetic as `loss.backward()` through nets.py's custom-conv path, without
 autograd's bookkeeping, and with the fusions it cannot express:
 
+  * every conv of the forward sums its bf16 outputs per channel in its epilogue (r48_conv3x3
+    `stats`), so BN's forward is finish + apply with no statistics pass over the activations;
   * every BN+ReLU forward writes a ReLU mask (1 bit per activation, r48_bn_forward `mask`), and
     its backward reads the mask instead of the 16x larger BN output;
   * a basic block's input gradient (first conv's data gradient + the identity path's gradient)
@@ -15,8 +17,9 @@ Semantics = DQNLearner.learn's autograd path: Huber (smooth L1, beta 1) loss of 
 against the TD target, mean over the batch; BatchNorm in training mode (batch statistics, running
 statistics updated with momentum, num_batches_tracked + 1); conv biases are constants (every conv
 feeds a training-mode BN: their gradient is exactly zero). Differences from the autograd path are
-bf16 rounding order only (the fused residual sum rounds once instead of twice): tests/
-test_dqn_gpu.py::test_resnet_train_step_matches_autograd.
+summation order and bf16 rounding only (BN statistics summed unshifted in the conv epilogue, the
+fused residual sum rounded once instead of twice): tests/test_dqn_gpu.py::
+test_resnet_train_step_matches_autograd.
 """
 import torch
 
@@ -53,18 +56,21 @@ class ResNetTrainStep:
                 "g": [act() for _ in range(6)],                 # gradient scratch
                 "stem_dw": torch.empty((64, 32, 3, 3), dtype=torch.float32, device=dev),
                 "loss": torch.empty(2, dtype=torch.float32, device=dev),        # mean loss, mean Q(s, a)
+                "stats": torch.empty(int(_lib.load().r48_conv_stats_floats()), dtype=torch.float32, device=dev),
                 "huber_ws": torch.empty(512, dtype=torch.float32, device=dev),
             }
         return self._bufs[key]
 
-    def _bn_forward(self, k, y, z, mask, save, residual=None):
+    def _bn_forward(self, k, y, z, mask, save, stats, residual=None):
+        """BN k + ReLU (+ residual) of the conv output y, from the conv's fused per-CU sums."""
         bn = self.net.bns[k]
         rows = y.numel() // 64
         mom = bn.momentum if bn.momentum is not None else 0.1
-        check(_lib.load().r48_bn_forward(ptr(y), ptr(residual), rows, 64, ptr(bn.weight), ptr(bn.bias),
-                                         ptr(bn.running_mean), ptr(bn.running_var), float(mom), float(bn.eps), 1,
-                                         ptr(save), ptr(_workspace(rows, 64, y.device)), ptr(z), ptr(mask),
-                                         _stream(y)))
+        L = _lib.load()
+        check(L.r48_bn_forward_stats(ptr(stats), stats.numel() // 128, ptr(y), ptr(residual), rows, 64, ptr(bn.weight),
+                                     ptr(bn.bias), ptr(bn.running_mean), ptr(bn.running_var), float(mom),
+                                     float(bn.eps), 1, ptr(save), ptr(_workspace(rows, 64, y.device)), ptr(z),
+                                     ptr(mask), _stream(y)))
 
     def _bn_backward(self, k, dz, mask, y, save, dy, dres=None):
         bn = self.net.bns[k]
@@ -86,15 +92,16 @@ class ResNetTrainStep:
         fwd, dgrad = pack_resnet_train(convs)             # one launch, all 17 fragment sets
         # ---- forward
         torch._foreach_add_([m.num_batches_tracked for m in net.bns], 1)   # one launch for the 9 BNs
-        conv3x3(x, fwd[0], convs[0].bias, out=Y[0])
-        self._bn_forward(0, Y[0], Z[0], M[0], S[0])
+        st = buf["stats"]                                  # the conv epilogues' BN sums
+        conv3x3(x, fwd[0], convs[0].bias, out=Y[0], stats=st)
+        self._bn_forward(0, Y[0], Z[0], M[0], S[0], st)
         for b in range(4):
             i1, i2 = 1 + 2 * b, 2 + 2 * b
             h = Z[i1 - 1]
-            conv3x3(h, fwd[i1], convs[i1].bias, out=Y[i1])
-            self._bn_forward(i1, Y[i1], Z[i1], M[i1], S[i1])
-            conv3x3(Z[i1], fwd[i2], convs[i2].bias, out=Y[i2])
-            self._bn_forward(i2, Y[i2], Z[i2], M[i2], S[i2], residual=h)
+            conv3x3(h, fwd[i1], convs[i1].bias, out=Y[i1], stats=st)
+            self._bn_forward(i1, Y[i1], Z[i1], M[i1], S[i1], st)
+            conv3x3(Z[i1], fwd[i2], convs[i2].bias, out=Y[i2], stats=st)
+            self._bn_forward(i2, Y[i2], Z[i2], M[i2], S[i2], st, residual=h)
         h = Z[8].view(B, 1024)
         q = q_head_forward(h, net.head.weight, net.head.bias)
         # ---- Huber loss of Q(x)[action] and its gradient (d loss / d q): one kernel + one finish

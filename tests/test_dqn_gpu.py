@@ -447,6 +447,29 @@ def test_q_head_matches_linear(B):
     assert torch.equal(hh.grad, dh) and torch.equal(w.grad, dw) and torch.equal(b.grad, db)
 
 
+@pytest.mark.parametrize("ci,B", [(64, 4099), (18, 1037)])
+def test_conv3x3_stats_match_fp64_sums(ci, B):
+    """r48_conv3x3's fused BN statistics: the per-CU records summed equal the fp64 per-channel sum
+    and sum of squares of the bf16 outputs it wrote (fp32 partials: 1e-5 relative), and the
+    outputs equal the stats-free launch's bit for bit."""
+    from rein48_amd import _lib
+    from rein48_amd.dqn.conv import board_onehot32, conv3x3, pack_conv
+    g = torch.Generator(device="cpu").manual_seed(ci + B)
+    w = (torch.randn(64, ci, 3, 3, generator=g) * 0.1).to(DEV)
+    bias = (torch.randn(64, generator=g) * 0.5 + 2.0).to(DEV)          # means well away from 0
+    if ci == 18:
+        x = board_onehot32(torch.randint(0, 18, (B, 16), generator=g, dtype=torch.int8).to(DEV))
+    else:
+        x = torch.randn(B, 16, ci, generator=g).to(DEV).to(torch.bfloat16)
+    st = torch.empty(int(_lib.load().r48_conv_stats_floats()), dtype=torch.float32, device=DEV)
+    y = conv3x3(x.contiguous(), pack_conv(w, x.shape[2]), bias, stats=st)
+    assert torch.equal(y, conv3x3(x.contiguous(), pack_conv(w, x.shape[2]), bias))
+    rec = st.view(-1, 2, 64).double().sum(0)
+    yd = y.reshape(-1, 64).double()
+    for got, want in ((rec[0], yd.sum(0)), (rec[1], (yd * yd).sum(0))):
+        assert float((got - want).abs().max()) <= 1e-5 * float(want.abs().max())
+
+
 def test_onehot32_exact():
     from rein48_amd.dqn.conv import board_onehot32
     b = np.random.default_rng(5).integers(0, 18, size=(3001, 16)).astype(np.int8)
@@ -488,15 +511,18 @@ def test_resnet_update_custom_conv_matches_structured_gemm():
 
 @pytest.mark.parametrize("B", [4096, 1000])
 def test_resnet_train_step_matches_autograd(B):
-    """train_step.ResNetTrainStep (explicit forward/backward: BN ReLU masks, the block-input
-    gradient summed in the data-gradient conv's epilogue, gradients straight into the flat buffer)
-    vs loss.backward() through nets.py's custom-conv autograd path on the same bf16 net: the
-    forward runs the same kernels, so Q and the BN running statistics are bit-identical and the loss
-    (r48_huber_grad's fixed-order sum vs torch's reduction) agrees to 1e-6; gradients differ only by
-    the rounding of the fused residual sum (once instead of twice in bf16): relative norm <= 1e-2 per
-    parameter, the head's gradients identical."""
+    """train_step.ResNetTrainStep (explicit forward/backward: BN statistics summed in the conv
+    epilogues, BN ReLU masks, the block-input gradient summed in the data-gradient conv's epilogue,
+    gradients straight into the flat buffer) vs loss.backward() through nets.py's custom-conv
+    autograd path on the same bf16 net, both against the same net in fp32 (structured GEMMs + torch
+    BN). The two bf16 computations differ in summation order and rounding only (unshifted conv-fused
+    statistics vs k_bn_stats; the residual sum rounded once instead of twice; a bf16 flip moves a
+    value by 2^-8 and flips propagate through 9 layers), so: loss and mean Q agree to 5e-4, running
+    statistics to 1e-4 relative, and every gradient's relative error against fp32 is within 1.5x
+    (+ 2e-3) of the autograd path's own bf16 error; test_conv3x3_stats_match_fp64_sums pins the sums."""
     from rein48_amd.a3c.optim import FlatParams
     from rein48_amd.dqn.conv import board_onehot32
+    from rein48_amd.dqn.kernels import board_onehot
     from rein48_amd.dqn.nets import ResNet10Q
     from rein48_amd.dqn.train_step import ResNetTrainStep
     torch.manual_seed(B)
@@ -511,31 +537,37 @@ def test_resnet_train_step_matches_autograd(B):
     target = torch.from_numpy(rng.normal(size=B).astype(np.float32)).to(DEV)
     stats0 = [(m.running_mean.clone(), m.running_var.clone()) for m in net.bns]
     out = []
-    for fused in (False, True):
+    for mode in ("autograd", "fused", "fp32"):
         for m, (rm, rv) in zip(net.bns, stats0):
             m.running_mean.copy_(rm)
             m.running_var.copy_(rv)
         flat.zero_grad()
-        if fused:
+        net.dtype = torch.float32 if mode == "fp32" else torch.bfloat16
+        if mode == "fused":
             loss, q_mean = ResNetTrainStep(net)(x, action, target)
         else:
-            q = net(x)
+            xin = board_onehot(boards, dtype=torch.float32) if mode == "fp32" else x
+            q = net(xin)
             q_sa = q.gather(1, action.long().view(-1, 1)).squeeze(1)
             loss = torch.nn.functional.smooth_l1_loss(q_sa, target)
             loss.backward()
             q_mean = q_sa.detach().mean()
         out.append((float(loss), float(q_mean), [p.grad.detach().clone() for p in flat.params],
                     [(m.running_mean.clone(), m.running_var.clone()) for m in net.bns]))
-    (la, qa, ga, sa), (lb, qb, gb, sb) = out
-    assert abs(la - lb) <= 1e-6 * abs(la) and abs(qa - qb) <= 1e-6 * abs(qa) + 1e-7
+    net.dtype = torch.bfloat16
+    (la, qa, ga, sa), (lb, qb, gb, sb), (_, _, g32, _) = out
+    assert abs(la - lb) <= 5e-4 * abs(la) and abs(qa - qb) <= 5e-4 * abs(qa) + 1e-6
     for (ra, va), (rb, vb) in zip(sa, sb):
-        assert torch.equal(ra, rb) and torch.equal(va, vb)
+        assert float((ra - rb).abs().max()) <= 1e-4 * float(ra.abs().max()) + 1e-6
+        assert float((va - vb).abs().max()) <= 1e-4 * float(va.abs().max()) + 1e-6
     names = [n for n, p in net.named_parameters() if p.requires_grad]
-    for n, a, b in zip(names, ga, gb):
-        if n.startswith("head"):
-            assert torch.equal(a, b), n
-        else:
-            assert float((a - b).norm()) <= 1e-2 * float(a.norm()) + 1e-9, n
+    for n, a, b, r in zip(names, ga, gb, g32):
+        if float(r.norm()) == 0.0:                  # conv biases: zero gradient on every path
+            assert float(a.norm()) == 0.0 and float(b.norm()) == 0.0, n
+            continue
+        ea = float((a - r).norm()) / float(r.norm())
+        eb = float((b - r).norm()) / float(r.norm())
+        assert eb <= 1.5 * ea + 2e-3, (n, ea, eb)
 
 
 def test_conv_pack_resnet_matches_host_packing():
