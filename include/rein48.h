@@ -316,6 +316,13 @@ int r48_board_onehot32(const int8_t *boards, int64_t n, void *out, void *stream)
  * per-channel sum and sum of squares of the bf16 outputs, one record [S1 64][S2 64] per CU, for
  * r48_bn_forward_stats. All pointers 16-byte aligned. */
 int64_t r48_conv_stats_floats(void);
+/* A data-gradient conv (64 -> 64 channels, wfrag from pack_conv_dgrad; + add as r48_conv3x3) whose
+ * output dx is the gradient reaching a training-mode BN + ReLU, with that BN's backward reduction
+ * fused in the epilogue: bn_part (float[r48_conv_stats_floats()]) gets per-CU records [sum g 64]
+ * [sum g (bn_x - mean) 64], g = dx . bn_mask, bn_x the BN's input, mean = bn_save[0..63] -- the
+ * input of r48_bn_backward_part. */
+int r48_conv3x3_bn_grad(const void *dy, int64_t boards, const void *wfrag, const void *add, void *dx,
+                        const void *bn_x, const uint8_t *bn_mask, const float *bn_save, float *bn_part, void *stream);
 int r48_conv3x3(const void *x, int64_t boards, int32_t cin, const void *wfrag, const float *bias, const void *add,
                 void *y, float *stats, void *stream);
 /* dw fp32 [64][cin][3][3] = sum over boards and in-grid cells of dy[b][p][co] x[b][p + off(t)][ci];
@@ -390,6 +397,12 @@ int r48_bn_forward_stats(const float *part, int32_t nblk, const void *x, const v
                          const float *gamma, const float *beta, float *running_mean, float *running_var,
                          float momentum, float eps, int32_t relu, float *save, float *workspace, void *y, uint8_t *mask,
                          void *stream);
+/* The backward (with ReLU mask) from sums a producer already reduced (r48_conv3x3_bn_grad: nblk
+ * records of [sum g C][sum g (x - mean) C], g = dy . mask): finish + apply, as r48_bn_backward
+ * without its reduction pass over dy and x. */
+int r48_bn_backward_part(const float *part, int32_t nblk, const void *dy, const uint8_t *mask, const void *x,
+                         int64_t rows, int32_t C, const float *gamma, const float *save, float *workspace, void *dx,
+                         void *dresidual, float *dgamma, float *dbeta, void *stream);
 int r48_bn_backward(const void *dy, const void *y, const uint8_t *mask, const void *x, int64_t rows, int32_t C,
                     const float *gamma, const float *save, int32_t relu, float *workspace, void *dx, void *dresidual,
                     float *dgamma, float *dbeta, void *stream);

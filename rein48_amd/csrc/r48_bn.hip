@@ -516,6 +516,25 @@ void launch_bwd(int nb, dim3 g, hipStream_t s, const uint16_t *dy, const uint16_
                            dx, dres);
 }
 
+// finish + apply from per-block sums a producer computed (r48_conv3x3_bn_grad)
+template <int C>
+int backward_part_c(const float *part, int nblk, const uint16_t *dy, const uint8_t *mask, const uint16_t *x,
+                    int64_t rows, const float *gamma, const float *save, float *coef, uint16_t *dx, uint16_t *dres,
+                    float *dgamma, float *dbeta, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_bn_bwd_finish, dim3(C), dim3(kBlock), 0, s, part, nblk, C, rows, gamma, save, dgamma, dbeta,
+                       coef);
+    const dim3 g(apply_blocks(rows, C));
+    const uint16_t *y = nullptr;
+    if (dres)
+        hipLaunchKernelGGL((k_bn_bwd_apply<C, true, true, true>), g, dim3(kBlock), 0, s, dy, y, mask, x, rows, coef,
+                           dx, dres);
+    else
+        hipLaunchKernelGGL((k_bn_bwd_apply<C, true, false, true>), g, dim3(kBlock), 0, s, dy, y, mask, x, rows, coef,
+                           dx, dres);
+    return launched("k_bn_bwd_apply");
+}
+
 template <int C>
 int backward_c(const uint16_t *dy, const uint16_t *y, const uint8_t *mask, const uint16_t *x, int64_t rows,
                const float *gamma, const float *save, int relu, float *ws, uint16_t *dx, uint16_t *dres,
@@ -596,6 +615,32 @@ int r48_bn_forward_stats(const float *part, int32_t nblk, const void *x, const v
     default:
         return forward_stats_c<128>(part, nblk, xs, rs, rows, gamma, beta, running_mean, running_var, momentum, eps,
                                     relu, save, coef, (uint16_t *)y, mask, s);
+    }
+}
+
+int r48_bn_backward_part(const float *part, int32_t nblk, const void *dy, const uint8_t *mask, const void *x,
+                         int64_t rows, int32_t C, const float *gamma, const float *save, float *workspace, void *dx,
+                         void *dresidual, float *dgamma, float *dbeta, void *stream)
+{
+    int rc = check_args(x, rows, C);
+    if (rc)
+        return rc;
+    if (!part || nblk < 1 || !dy || !aligned16(dy) || !mask || !gamma || !save || !workspace || !dx ||
+        !aligned16(dx) || (dresidual && !aligned16(dresidual)))
+        return fail(R48_EINVAL, "r48_bn_backward_part: null or misaligned argument");
+    const uint16_t *d = (const uint16_t *)dy, *xs = (const uint16_t *)x;
+    hipStream_t s = (hipStream_t)stream;
+    float *coef = workspace + (int64_t)reduce_blocks(rows, C) * 2 * C;
+    switch (C) {
+    case 32:
+        return backward_part_c<32>(part, nblk, d, mask, xs, rows, gamma, save, coef, (uint16_t *)dx,
+                                   (uint16_t *)dresidual, dgamma, dbeta, s);
+    case 64:
+        return backward_part_c<64>(part, nblk, d, mask, xs, rows, gamma, save, coef, (uint16_t *)dx,
+                                   (uint16_t *)dresidual, dgamma, dbeta, s);
+    default:
+        return backward_part_c<128>(part, nblk, d, mask, xs, rows, gamma, save, coef, (uint16_t *)dx,
+                                    (uint16_t *)dresidual, dgamma, dbeta, s);
     }
 }
 

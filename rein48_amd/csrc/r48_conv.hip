@@ -105,15 +105,23 @@ constexpr int kOutPitch = 4 * 64 + 8;      // bf16 per board in the output-row s
 // STATS: the per-channel sums S1 = sum y, S2 = sum y^2 of the bf16 outputs (the statistics of the
 // training-mode BN that follows), accumulated from the staged 16-byte pieces (a lane's pieces are
 // always the same 8 channels), one record [S1 64][S2 64] per workgroup (the grid is then exactly
-// one workgroup per CU, idle ones write zeros). Passes of PO row tiles: 2, or 1 with STATS to
-// make room for its 16 accumulators.
-template <int NC, bool ADD, bool STATS>
+// one workgroup per CU, idle ones write zeros). SM = 1.
+// SM = 2 (a data-gradient conv whose output y is the gradient reaching a training-mode BN + ReLU):
+// the BN backward's reduction fused the same way -- g = y . [relu mask], records [sum g 64]
+// [sum g (bn_x - mean) 64] with bn_x the BN's input (the forward conv output) and mean from its
+// save (r48_bn_backward's k_bn_bwd_reduce, without its second pass over y and bn_x).
+// Passes of PO row tiles: 2, or 1 with statistics to make room for their 16 accumulators.
+template <int NC, bool ADD, int SM>
 __global__ __launch_bounds__(64 * kConvWaves, 1) void k_conv3x3(const uint16_t *__restrict__ x, int64_t boards,
                                                                const uint4 *__restrict__ wfrag,
                                                                const float *__restrict__ bias,
                                                                const uint16_t *__restrict__ add,
-                                                               uint16_t *__restrict__ y, float *__restrict__ stats)
+                                                               uint16_t *__restrict__ y, float *__restrict__ stats,
+                                                               const uint16_t *__restrict__ bn_x,
+                                                               const uint8_t *__restrict__ bn_mask,
+                                                               const float *__restrict__ bn_save)
 {
+    constexpr bool STATS = SM != 0;
     constexpr int PO = STATS ? 1 : 2;
     constexpr int kFrags = 9 * 4 * NC;
     constexpr int kCin = 32 * NC;
@@ -121,10 +129,13 @@ __global__ __launch_bounds__(64 * kConvWaves, 1) void k_conv3x3(const uint16_t *
     __shared__ __attribute__((aligned(16))) float b_lds[kCout];
     __shared__ __attribute__((aligned(16))) uint16_t o_lds[kConvWaves][16 * kOutPitch];
     __shared__ float st_lds[STATS ? kConvWaves : 1][8][16];
+    __shared__ __attribute__((aligned(16))) float mean_lds[SM == 2 ? kCout : 4];
     for (int i = threadIdx.x; i < kFrags * 64; i += 64 * kConvWaves)
         w_lds[i] = wfrag[i];
     if (threadIdx.x < kCout)
         b_lds[threadIdx.x] = bias ? bias[threadIdx.x] : 0.0f;
+    if (SM == 2 && threadIdx.x < kCout)
+        mean_lds[threadIdx.x] = bn_save[threadIdx.x];
     __syncthreads();
     const int lane = threadIdx.x & 63, n = lane & 15, g = lane >> 4;
     const int wave = threadIdx.x >> 6;
@@ -134,7 +145,7 @@ __global__ __launch_bounds__(64 * kConvWaves, 1) void k_conv3x3(const uint16_t *
     if (!STATS && tile >= n_tiles)
         return;
     uint16_t *orow = o_lds[wave];          // this wave's output row: 16 boards x 4 cells x 64 channels
-    float s1[8] = {}, s2[8] = {};          // STATS: channels 8 (lane & 7) .. + 7
+    float s1[8] = {}, s2[8] = {};          // statistics of channels 8 (lane & 7) .. + 7
     // xr[R][col][c]: input cell 4 R + col of this lane's board, channels 32 c + 8 g .. + 7
     uint4 xr[4][4][NC];
     auto load_row = [&](int64_t t, int R) {
@@ -219,12 +230,31 @@ __global__ __launch_bounds__(64 * kConvWaves, 1) void k_conv3x3(const uint16_t *
             // each) write at about 0.6 of the rate
 #pragma unroll
             for (int k = 0; k < 8; k++) {
+                if (SM == 2 && k == 4)
+                    __builtin_amdgcn_sched_barrier(0);   // two batches of BN-input loads: registers
                 const int m = 64 * k + lane, bl = m >> 5, e = 8 * (m & 31);
                 const uint4 v = *reinterpret_cast<const uint4 *>(orow + bl * kOutPitch + e);
                 const int64_t bg = tile * 16 + bl;
                 if (bg < boards) {
-                    *reinterpret_cast<uint4 *>(y + (bg * 16 + 4 * r) * kCout + e) = v;
-                    if (STATS) {
+                    const int64_t o = (bg * 16 + 4 * r) * kCout + e;
+                    *reinterpret_cast<uint4 *>(y + o) = v;
+                    if (SM == 2) {
+                        const uint4 xb = *reinterpret_cast<const uint4 *>(bn_x + o);
+                        const uint32_t mk = bn_mask[o >> 3];
+                        const uint32_t w4[4] = {v.x, v.y, v.z, v.w}, x4[4] = {xb.x, xb.y, xb.z, xb.w};
+                        const float4 m0 = *reinterpret_cast<const float4 *>(mean_lds + (e & 63));
+                        const float4 m1 = *reinterpret_cast<const float4 *>(mean_lds + (e & 63) + 4);
+                        const float mn[8] = {m0.x, m0.y, m0.z, m0.w, m1.x, m1.y, m1.z, m1.w};
+#pragma unroll
+                        for (int q = 0; q < 8; q++) {
+                            const uint32_t wv = (q & 1) ? (w4[q >> 1] & 0xFFFF0000u) : (w4[q >> 1] << 16);
+                            const uint32_t xv = (q & 1) ? (x4[q >> 1] & 0xFFFF0000u) : (x4[q >> 1] << 16);
+                            const float gq = (mk >> q) & 1u ? __uint_as_float(wv) : 0.f;
+                            s1[q] += gq;
+                            s2[q] = __builtin_fmaf(gq, __uint_as_float(xv) - mn[q], s2[q]);
+                        }
+                    }
+                    if (SM == 1) {
                         const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
                         for (int q = 0; q < 4; q++) {
@@ -837,17 +867,42 @@ int r48_conv3x3(const void *x, int64_t boards, int32_t cin, const void *wfrag, c
     uint16_t *ys = (uint16_t *)y;
     const dim3 g(grid), blk(64 * kConvWaves);
     hipStream_t s = (hipStream_t)stream;
+    const uint16_t *nx = nullptr;
+    const uint8_t *nm = nullptr;
+    const float *ns = nullptr;
     if (cin == 64 && add)
-        hipLaunchKernelGGL((k_conv3x3<2, true, false>), g, blk, 0, s, xs, boards, wf, bias, a, ys, stats);
+        hipLaunchKernelGGL((k_conv3x3<2, true, 0>), g, blk, 0, s, xs, boards, wf, bias, a, ys, stats, nx, nm, ns);
     else if (cin == 64 && stats)
-        hipLaunchKernelGGL((k_conv3x3<2, false, true>), g, blk, 0, s, xs, boards, wf, bias, a, ys, stats);
+        hipLaunchKernelGGL((k_conv3x3<2, false, 1>), g, blk, 0, s, xs, boards, wf, bias, a, ys, stats, nx, nm, ns);
     else if (cin == 64)
-        hipLaunchKernelGGL((k_conv3x3<2, false, false>), g, blk, 0, s, xs, boards, wf, bias, a, ys, stats);
+        hipLaunchKernelGGL((k_conv3x3<2, false, 0>), g, blk, 0, s, xs, boards, wf, bias, a, ys, stats, nx, nm, ns);
     else if (stats)
-        hipLaunchKernelGGL((k_conv3x3<1, false, true>), g, blk, 0, s, xs, boards, wf, bias, a, ys, stats);
+        hipLaunchKernelGGL((k_conv3x3<1, false, 1>), g, blk, 0, s, xs, boards, wf, bias, a, ys, stats, nx, nm, ns);
     else
-        hipLaunchKernelGGL((k_conv3x3<1, false, false>), g, blk, 0, s, xs, boards, wf, bias, a, ys, stats);
+        hipLaunchKernelGGL((k_conv3x3<1, false, 0>), g, blk, 0, s, xs, boards, wf, bias, a, ys, stats, nx, nm, ns);
     return launched("k_conv3x3");
+}
+
+int r48_conv3x3_bn_grad(const void *dy, int64_t boards, const void *wfrag, const void *add, void *dx,
+                        const void *bn_x, const uint8_t *bn_mask, const float *bn_save, float *bn_part, void *stream)
+{
+    if (!dy || !wfrag || !dx || !bn_x || !bn_mask || !bn_save || !bn_part || boards < 1)
+        return fail(R48_EINVAL, "r48_conv3x3_bn_grad: NULL argument or boards < 1");
+    if ((reinterpret_cast<uintptr_t>(dy) | reinterpret_cast<uintptr_t>(wfrag) | reinterpret_cast<uintptr_t>(dx) |
+         reinterpret_cast<uintptr_t>(add) | reinterpret_cast<uintptr_t>(bn_x) | reinterpret_cast<uintptr_t>(bn_save)) &
+        15u)
+        return fail(R48_EINVAL, "r48_conv3x3_bn_grad: dy, wfrag, add, dx, bn_x and bn_save must be 16-byte aligned");
+    const dim3 g(cu_count()), blk(64 * kConvWaves);
+    hipStream_t s = (hipStream_t)stream;
+    const uint16_t *xs = (const uint16_t *)dy, *a = (const uint16_t *)add, *bx = (const uint16_t *)bn_x;
+    const uint4 *wf = (const uint4 *)wfrag;
+    if (add)
+        hipLaunchKernelGGL((k_conv3x3<2, true, 2>), g, blk, 0, s, xs, boards, wf, nullptr, a, (uint16_t *)dx, bn_part,
+                           bx, bn_mask, bn_save);
+    else
+        hipLaunchKernelGGL((k_conv3x3<2, false, 2>), g, blk, 0, s, xs, boards, wf, nullptr, a, (uint16_t *)dx,
+                           bn_part, bx, bn_mask, bn_save);
+    return launched("k_conv3x3 (bn grad)");
 }
 
 int64_t r48_conv_wgrad_workspace_floats(int32_t cin)

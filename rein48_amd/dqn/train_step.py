@@ -6,6 +6,9 @@ autograd's bookkeeping, and with the fusions it cannot express:
     `stats`), so BN's forward is finish + apply with no statistics pass over the activations;
   * every BN+ReLU forward writes a ReLU mask (1 bit per activation, r48_bn_forward `mask`), and
     its backward reads the mask instead of the 16x larger BN output;
+  * every data-gradient conv reduces the BN backward of the layer below in its epilogue
+    (r48_conv3x3_bn_grad): its output IS that BN's output gradient, so BN's backward is finish +
+    apply with no reduction pass (only the last BN, fed by the head, reduces on its own);
   * a basic block's input gradient (first conv's data gradient + the identity path's gradient)
     is summed in the data-gradient conv's epilogue (r48_conv3x3 `add`), not by a separate add;
   * parameter gradients are written straight into their .grad views of the flat gradient buffer
@@ -72,6 +75,22 @@ class ResNetTrainStep:
                                      float(bn.eps), 1, ptr(save), ptr(_workspace(rows, 64, y.device)), ptr(z),
                                      ptr(mask), _stream(y)))
 
+    def _bn_backward_part(self, k, part, dz, mask, y, save, dy, dres=None):
+        """BN k's backward from the reduction its gradient's producer fused (r48_conv3x3_bn_grad)."""
+        bn = self.net.bns[k]
+        rows = y.numel() // 64
+        check(_lib.load().r48_bn_backward_part(ptr(part), part.numel() // 128, ptr(dz), ptr(mask), ptr(y), rows, 64,
+                                               ptr(bn.weight), ptr(save), ptr(_workspace(rows, 64, y.device)), ptr(dy),
+                                               ptr(dres), ptr(bn.weight.grad), ptr(bn.bias.grad), _stream(y)))
+
+    def _conv_bn_grad(self, dy, frags, out, k, add=None, part=None):
+        """out = data gradient conv of dy (+ add) -- the gradient reaching BN k's output -- with BN
+        k's backward reduction summed into `part` in the same pass."""
+        check(_lib.load().r48_conv3x3_bn_grad(ptr(dy), dy.shape[0], ptr(frags), ptr(add), ptr(out),
+                                              ptr(self._Y[k]), ptr(self._M[k]), ptr(self._S[k]), ptr(part),
+                                              _stream(dy)))
+        return out
+
     def _bn_backward(self, k, dz, mask, y, save, dy, dres=None):
         bn = self.net.bns[k]
         rows = y.numel() // 64
@@ -120,21 +139,28 @@ class ResNetTrainStep:
         # per block, backwards: BN2 (+ identity) -> conv2 data/weight gradients -> BN1 -> conv1
         # data gradient + identity gradient (one epilogue) and weight gradient. The incoming
         # gradient alternates between g[0] and g[5]; g[1..4] hold the block's temporaries.
+        # Every data-gradient conv also reduces the BN backward of the layer below (its output is
+        # that BN's output gradient); only BN 8's reduction (the head's gradient) runs on its own.
+        self._Y, self._M, self._S = Y, M, S
+        part = buf["stats"]
         cur = dh.view(B, 16, 64)
         for b in range(3, -1, -1):
             i1, i2 = 1 + 2 * b, 2 + 2 * b
             h_in = Z[i1 - 1]
             dy2, dres, dz1, dy1 = G[1], G[2], G[3], G[4]
-            self._bn_backward(i2, cur, M[i2], Y[i2], S[i2], dy2, dres=dres)
-            conv3x3(dy2, dgrad[i2], out=dz1)
+            if b == 3:
+                self._bn_backward(i2, cur, M[i2], Y[i2], S[i2], dy2, dres=dres)
+            else:
+                self._bn_backward_part(i2, part, cur, M[i2], Y[i2], S[i2], dy2, dres=dres)
+            self._conv_bn_grad(dy2, dgrad[i2], dz1, i1, part=part)
             conv3x3_wgrad(dy2, Z[i1], out=convs[i2].weight.grad)
-            self._bn_backward(i1, dz1, M[i1], Y[i1], S[i1], dy1)
+            self._bn_backward_part(i1, part, dz1, M[i1], Y[i1], S[i1], dy1)
             nxt = G[5] if cur is G[0] else G[0]
-            conv3x3(dy1, dgrad[i1], add=dres, out=nxt)
+            self._conv_bn_grad(dy1, dgrad[i1], nxt, i1 - 1, add=dres, part=part)
             conv3x3_wgrad(dy1, h_in, out=convs[i1].weight.grad)
             cur = nxt
         dy0 = G[1]
-        self._bn_backward(0, cur, M[0], Y[0], S[0], dy0)
+        self._bn_backward_part(0, part, cur, M[0], Y[0], S[0], dy0)
         conv3x3_wgrad(dy0, x, out=buf["stem_dw"])
         convs[0].weight.grad.copy_(buf["stem_dw"][:, :convs[0].weight.shape[1]])
         return stats[0], stats[1]
