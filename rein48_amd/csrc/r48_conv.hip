@@ -301,16 +301,16 @@ __global__ __launch_bounds__(64 * kConvWaves, 1) void k_conv3x3(const uint16_t *
 // Per step a workgroup stages kStepRows rows (kStepRows / 16 boards) of dy [rows][64] and x
 // [rows][CIN] into LDS images by LDS-DMA (global_load_lds_dwordx4: no staging registers): row-major,
 // the 16-byte chunk index XOR-ed with swz(row) (applied to the per-lane SOURCE address, the LDS side
-// of one DMA is lane-linear). A ring of kRing buffers keeps steps s + 1 .. s + 5 in flight while
-// step s computes (~64-80 KB per CU), waited for with a counted vmcnt and a raw barrier. The x image
+// of one DMA is lane-linear). A ring of kRing buffers keeps steps s + 1, s + 2 in flight while
+// step s computes (32-64 KB per CU), waited for with a counted vmcnt and a raw barrier. The x image
 // has a zero band: rows kStepRows + 32 ks, one per k-step, so that every transposed-read address of
 // k-step ks is the k-step-0 address plus the constant 32 ks rows (an immediate offset) -- also for
 // the out-of-grid taps, which read the zero row.
-constexpr int kStepRows = 64;
+constexpr int kStepRows = 128;
 constexpr int kKSteps = kStepRows / 32;
 constexpr int kZeroRow = kStepRows;                              // zero band: kZeroRow + 32 ks
 constexpr int kXRows = kStepRows + 32 * (kKSteps - 1) + 1;
-constexpr int kRing = 6;                                          // LDS buffers: 5 steps ahead
+constexpr int kRing = 3;                                          // LDS buffers: 2 steps ahead
 constexpr int kRedGroup = 16;                                     // records per first-pass group
 
 // chunk swizzle of image row `row`: XOR with row & 7 spreads a transposed read's 4 consecutive rows
@@ -439,7 +439,7 @@ __global__ __launch_bounds__(64 * kWgWaves, 1) void k_conv_wgrad(const uint16_t 
                               lane);
         }
     };
-    static_assert(kKSteps == 2, "the step loop splits compute into its two k-steps");
+    static_assert(kKSteps == 4, "the step loop splits compute into two halves");
     auto compute = [&](int buf, int ks0, int ks1) {
         const uint16_t *img = lds + buf * kBuf;
 #pragma unroll
@@ -467,11 +467,11 @@ __global__ __launch_bounds__(64 * kWgWaves, 1) void k_conv_wgrad(const uint16_t 
         // this wave's DMAs of step s done (steps s + 1, s + 2 may stay in flight), then the barrier
         // that orders them for every reader -- and that every wave passes only after its reads of
         // step s - 1, whose buffer is restaged below
-        if (my_dmas == 2)
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"((kRing - 2) * 2) : "memory");
+        if (my_dmas == 4)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"((kRing - 2) * 4) : "memory");
         else
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kRing - 2) : "memory");
-        static_assert(kDmas <= 2 * kWgWaves && kDmas > kWgWaves, "one or two DMAs per wave and step");
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"((kRing - 2) * 3) : "memory");
+        static_assert(kDmas <= 4 * kWgWaves && kDmas > 2 * kWgWaves && kDmas % kWgWaves == 0, "3 or 4 DMAs a step");
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         if (s == steps_total - 1 && rows_total - s * kStepRows < kStepRows) {
@@ -487,11 +487,11 @@ __global__ __launch_bounds__(64 * kWgWaves, 1) void k_conv_wgrad(const uint16_t 
         }
         // the DMAs of step i + kRing - 1 (into the buffer of step i - 1) issue between the two
         // k-steps, under the first one's MFMAs, not in a burst of all waves after the barrier
-        compute(buf, 0, 1);
+        compute(buf, 0, 2);
         __builtin_amdgcn_sched_barrier(0);
         stage(i + kRing - 1, (buf + kRing - 1) % kRing);
         __builtin_amdgcn_sched_barrier(0);
-        compute(buf, 1, 2);
+        compute(buf, 2, 4);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");              // no DMA outlives the kernel
     // record: D[m = co 16][n = ci 16], lane l: column i16 (ci), rows 4g + i (co). 24 wait states
