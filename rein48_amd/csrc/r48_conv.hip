@@ -11,18 +11,18 @@
 //   its 16 boards (16-byte chunks, lane = board l & 15, channel group g = l >> 4) and the 3x3 tap
 //   (dr, dc) of output cell p is just the input cell p + 4dr + dc of the same lane -- no lane
 //   movement; one LDS weight fragment (tap, O, k-chunk) feeds every cell that has the tap (9, 12
-//   or 16 MFMAs). Accumulators start at the bias; a finished row tile stores 4 channels (8 B) per
-//   lane and cell. Weights: 9 x 4 x NC fragments of 1 KiB in LDS (72 KiB at 64 input channels),
-//   two workgroups of 4 waves per CU.
+//   or 16 MFMAs). Accumulators start at the bias; finished output rows are staged through a per-wave
+//   LDS row and stored in 16-byte pieces. Weights: 9 x 4 x NC fragments of 1 KiB in LDS (72 KiB at
+//   64 input channels), one workgroup of 8 waves per CU. Epilogue options: + a residual gradient,
+//   the BN forward statistics of the output, the BN backward reduction of the layer below.
 // k_conv_wgrad (weight gradient, summed over boards and cells)
 //   dW[t][co][ci] = sum over (board, cell p in grid for t) of dy[b][p][co] x[b][p + off(t)][ci]:
 //   a contraction over rows, so rows go to the MFMA K dimension through LDS images read back with
-//   ds_read_b64_tr_b16. Per step a workgroup stages 4 boards (64 rows) of dy and x (double-buffered
-//   images, the global loads two steps ahead in registers); the x operand of tap t is the same image
-//   read with per-lane row addresses shifted by the tap (rows outside the grid point at a zero row).
-//   Wave w owns input-channel tile (16 channels) w for every tap and output tile: 36 accumulators of
-//   16x16 (AGPRs). Each workgroup writes one fp32 record; k_conv_wgrad_reduce sums the records in a
-//   fixed order (deterministic).
+//   ds_read_b64_tr_b16. Per step a workgroup stages kStepRows rows of dy and x by LDS-DMA into a
+//   ring of kRing buffers; the x operand of tap t is the same image read with per-lane row addresses
+//   shifted by the tap (rows outside the grid point at a zero row). 8 waves, each owning one
+//   input-channel tile and its share of the output tiles, accumulate in AGPRs. Each workgroup writes
+//   one fp32 record; k_conv_wgrad_reduce1/2 sum the records in a fixed order (deterministic).
 #include <hip/hip_runtime.h>
 
 #include <cstdint>

@@ -20,6 +20,7 @@ using r48::Board;
 namespace {
 
 constexpr int kBlock = 256;
+constexpr int kStepNP = 1;   // board pairs per lane in k_step_n
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -272,29 +273,6 @@ __global__ __launch_bounds__(kBlock) void k_step(int8_t *boards, int64_t n, int6
     }
 }
 
-#ifdef R48_STAMP
-// Diagnostic build only (tools/exp_stamps.py): per wave of k_step_n, the core clock (s_memtime)
-// and the 100 MHz reference clock (s_memrealtime) at entry and exit, and HW_ID (CU / SIMD).
-__device__ unsigned long long r48_stamp_buf[65536 * 4];
-#define R48_STAMP_BEGIN                                                                  \
-    const unsigned long long st_t0 = __builtin_amdgcn_s_memtime(), st_r0 = __builtin_amdgcn_s_memrealtime();
-#define R48_STAMP_END                                                                    \
-    if ((threadIdx.x & 63) == 0) {                                                       \
-        const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime(); \
-        const unsigned w = blockIdx.x * (kBlock / 64) + threadIdx.x / 64;                \
-        if (w < 65536) {                                                                 \
-            unsigned hw, xcc;                                                            \
-            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));             \
-            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));           \
-            hw = (hw & 0x0FFFFFFFu) | ((xcc & 0xFu) << 28);                              \
-            r48_stamp_buf[4 * w] = st_t0; r48_stamp_buf[4 * w + 1] = st_r0;              \
-            r48_stamp_buf[4 * w + 2] = t1 - st_t0; r48_stamp_buf[4 * w + 3] = ((r1 - st_r0) << 32) | hw; \
-        }                                                                                \
-    }
-#else
-#define R48_STAMP_BEGIN
-#define R48_STAMP_END
-#endif
 
 // ---------------------------------------------------------------- K steps in one launch
 // r48_env_step_n: n_steps consecutive steps of every board in ONE launch. Boards are independent,
@@ -304,9 +282,6 @@ __device__ unsigned long long r48_stamp_buf[65536 * 4];
 // are overwritten by every step). Same draw contract as k_step, step counter step0 + t. Bound:
 // VALU issue (~200 VALU per board-step); HBM traffic is 34 B per board per
 // call, not per step.
-#ifndef R48_STEPN_NP
-#define R48_STEPN_NP 1
-#endif
 // TRAJ (r48_env_rollout): also every step's action and done into row t of traj_actions /
 // traj_done ([n_steps][n], each nullable) -- one 2-byte store per plane per pair and step.
 template <bool RANDOM, bool AUTO_RESET, bool REWARD, int NP, bool TRAJ = false>
@@ -321,7 +296,6 @@ __global__ __launch_bounds__(kBlock) void k_step_n(int8_t *boards, int64_t n, in
     const int64_t base = (int64_t)blockIdx.x * kTile + 2 * (int64_t)threadIdx.x;
     const bool want_score = score != nullptr;
     const int32_t last = n_steps - 1;
-    R48_STAMP_BEGIN
     __shared__ __attribute__((aligned(16))) r48::Orient tab[16];
     load_orient_table(tab);
     // trajectory rows whose pair addresses are not all 2-byte aligned (odd n or odd row pointers)
@@ -355,16 +329,9 @@ __global__ __launch_bounds__(kBlock) void k_step_n(int8_t *boards, int64_t n, in
         // last ones run with too few partners to fill the VALU. Dropping a wave's priority as it
         // passes 1/8, 3/8 and 3/4 of the call lets the laggards catch up at each boundary, so all
         // 8 stay to the end (boundaries measured on three boxes: profiles/r02/exp_stepn_priority*).
-#ifndef R48_PRIO_Q   // priority boundaries in eighths of the call (ablation builds: tools/exp_stepn.py A/B)
-#define R48_PRIO_Q 1, 3, 6
-#endif
-        constexpr int kQ[3] = {R48_PRIO_Q};
+        constexpr int kQ[3] = {1, 3, 6};   // priority boundaries in eighths of the call
         const int32_t q1 = (n_steps * kQ[0]) >> 3, q2 = (n_steps * kQ[1]) >> 3, q3 = (n_steps * kQ[2]) >> 3;
-#ifdef R48_NO_PRIO   // ablation build (tools/exp_stepn.py A/B)
-        constexpr bool kPrio = false;
-#else
         constexpr bool kPrio = true;
-#endif
         if (kPrio)
             __builtin_amdgcn_s_setprio(3);
         for (int32_t t = 0; t < n_steps; t++) {
@@ -434,7 +401,6 @@ __global__ __launch_bounds__(kBlock) void k_step_n(int8_t *boards, int64_t n, in
             }
         }
     }
-    R48_STAMP_END
 }
 
 // ---------------------------------------------------------------- injected-draw step
@@ -937,13 +903,6 @@ int r48_env_reset_with_draws(r48_env *env, const uint8_t *mask, const uint8_t *r
     return launched("k_reset_draws");
 }
 
-#ifdef R48_STAMP
-int r48_debug_stamps(unsigned long long *out, int64_t n_waves)
-{
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(r48_stamp_buf), sizeof(unsigned long long) * 4 * n_waves) == hipSuccess
-               ? 0 : -1;
-}
-#endif
 }  // extern "C"
 
 namespace {
@@ -973,13 +932,13 @@ void launch_steps(r48_env *env, int32_t n_steps, int8_t *actions, uint32_t flags
                            env->err);
     };
     auto many = [&](auto kern) {
-        const int64_t tile = (int64_t)kBlock * 2 * R48_STEPN_NP;
+        const int64_t tile = (int64_t)kBlock * 2 * kStepNP;
         hipLaunchKernelGGL(kern, dim3((unsigned)((env->n + tile - 1) / tile)), dim3(kBlock), 0, stream, env->boards,
                            env->n, env->gid0, k0, k1, env->step_ctr, n_steps, actions, done, changed, reward, score,
                            env->err, (int8_t *)nullptr, (uint8_t *)nullptr);
     };
 #define R48_GO(RN, AR, RW) \
-    (n_steps == 1 ? one(k_step<RN, AR, RW>) : many(k_step_n<RN, AR, RW, R48_STEPN_NP>))
+    (n_steps == 1 ? one(k_step<RN, AR, RW>) : many(k_step_n<RN, AR, RW, kStepNP>))
     if (rnd) {
         if (ar) rw ? R48_GO(true, true, true) : R48_GO(true, true, false);
         else rw ? R48_GO(true, false, true) : R48_GO(true, false, false);
@@ -1081,8 +1040,8 @@ int r48_env_rollout(r48_env *env, int32_t n_steps, int8_t *actions, uint8_t *don
         return R48_OK;
     DeviceGuard g(env->device);
     // = r48_env_step_n(random policy, auto-reset) that also writes every step's action and done
-    const int64_t tile = (int64_t)kBlock * 2 * R48_STEPN_NP;
-    hipLaunchKernelGGL((k_step_n<true, true, false, R48_STEPN_NP, true>), dim3((unsigned)((env->n + tile - 1) / tile)),
+    const int64_t tile = (int64_t)kBlock * 2 * kStepNP;
+    hipLaunchKernelGGL((k_step_n<true, true, false, kStepNP, true>), dim3((unsigned)((env->n + tile - 1) / tile)),
                        dim3(kBlock), 0, (hipStream_t)stream, env->boards, env->n, env->gid0, (uint32_t)env->seed,
                        (uint32_t)(env->seed >> 32), env->step_ctr, n_steps, (int8_t *)nullptr, (uint8_t *)nullptr,
                        (uint8_t *)nullptr, (int32_t *)nullptr, (int32_t *)nullptr, env->err, actions, done);

@@ -1,6 +1,6 @@
-"""GPU experiment: per-wave clock stamps of k_step_n (diagnostic build with -DR48_STAMP).
+"""GPU experiment: per-wave clock stamps of k_step_n (diagnostic build made by tools/stamp_env.py).
 
-Build:  tools/build_variant.sh rein48_amd/csrc/r48_env.hip r48_env build/librein48_stamp.so -DR48_STAMP
+Build:  python tools/stamp_env.py
 Run:    R48_LIB=build/librein48_stamp.so python tools/exp_stamps.py [boards] [K]
 Prints, for one K-step call after a settle period: the effective core clock of each wave
 (s_memtime ticks / s_memrealtime at 100 MHz), wave lifetimes, the span from the first wave's
