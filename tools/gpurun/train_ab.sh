@@ -8,4 +8,4 @@ P=rein48_amd/lib/librein48.so
 timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_a3c_gpu.py \
     -k "update or trainer" > $O/pytest.txt 2>&1 && tail -2 $O/pytest.txt \
 && timeout -k 10 300 python -u tools/exp_train.py 16777216 $P "$@" $P "$@" > $O/train.txt 2>&1 && cat $O/train.txt \
-&& if [ -f build/librein48_stamp.so ]; then timeout -k 10 120 python -u tools/exp_train_stamps.py build/librein48_stamp.so > $O/stamps.txt 2>&1 && cat $O/stamps.txt; fi
+&& if [ -f build/lib_train_stamp.so ]; then timeout -k 10 120 python -u tools/exp_train_stamps.py build/lib_train_stamp.so > $O/stamps.txt 2>&1 && cat $O/stamps.txt; fi

@@ -4,27 +4,30 @@ the cycles spent in each phase (summed over its tiles) over the first 8 words of
 (so that build's gradients are wrong: timing only). The product source holds no diagnostic code.
 Phases: 0 tile head (inputs, Xt), 1 forward, 2 loss, 3 dh2 + dWh + dh2^T + db2, 5 position loop.
 
-    python tools/stamp_train.py && tools/build_variant.sh build/var/r48_a3c_train_stamp.hip \\
-        r48_a3c_train build/librein48_stamp.so -mllvm -amdgpu-mfma-vgpr-form=1
-    python tools/exp_train_stamps.py build/librein48_stamp.so      (on the GPU)"""
+    python tools/stamp_train.py [source.hip [out.hip]] && tools/build_variant.sh \\
+        build/var/r48_a3c_train_stamp.hip r48_a3c_train build/lib_train_stamp.so -mllvm -amdgpu-mfma-vgpr-form=1
+    python tools/exp_train_stamps.py build/lib_train_stamp.so      (on the GPU)"""
 import os
+import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "rein48_amd", "csrc", "r48_a3c_train.hip")
 OUT = os.path.join(ROOT, "build", "var", "r48_a3c_train_stamp.hip")
 
 MARKS = [
-    ("        // ---------------- forward (r48_policy.hip k_cnn_forward", 0),
+    ("        // ---------------- forward (", 0),
     ("        // ---------------- loss gradient per row", 1),
     ("        // ---------------- dh2 = Wh^T dout", 2),
-    ("            fwd_conv2_heads_chain(w, bl, lane, h, h1, ws, h2, out, my, la);", 6),
+    ("            fwd_conv2_heads_", 6),
     ("        // ---------------- per conv1 position R", 3),
     ("        const RowIn in = next;", 5),
 ]
 
 
 def main():
-    s = open(SRC).read()
+    src = sys.argv[1] if len(sys.argv) > 1 else SRC
+    out = sys.argv[2] if len(sys.argv) > 2 else OUT
+    s = open(src).read()
     s = s.replace('#include "r48_cnn_common.h"', '#include "r48_cnn_common.h"\n'
                   "#define R48_STAMP(k) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); "
                   "st_acc[k] += t_ - st_last; st_last = t_; }\n", 1)
@@ -38,9 +41,9 @@ def main():
     assert s.count(end) == 1
     s = s.replace(end, end + "    R48_STAMP(5)\n    if (lane == 0)\n        for (int k = 0; k < 8; k++)\n"
                   "            reinterpret_cast<unsigned long long *>(rec)[k] = st_acc[k];\n", 1)
-    os.makedirs(os.path.dirname(OUT), exist_ok=True)
-    open(OUT, "w").write(s)
-    print(OUT)
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    open(out, "w").write(s)
+    print(out)
 
 
 if __name__ == "__main__":
