@@ -320,7 +320,7 @@ def _allreduce_label(world):
     return "%s all_reduce(SUM)/world" % ("RCCL (torch backend 'nccl')" if b == "nccl" else "torch backend '%s'" % b)
 
 
-def a3c_config3(dev, seed, n_boards, updates=2, world=1, mode="textbook", features="exponents"):
+def a3c_config3(dev, seed, n_boards, updates=3, world=1, mode="textbook", features="exponents", warmup=2):
     """BASELINE configs[2] (world 1: 2^20 boards + 2-layer CNN policy on 1 MI355X) and configs[3]
     (world > 1: 2^20 boards per GPU, 8M boards on 8 GPUs, one all-reduce of the flat fp32
     gradient per update): A3C rollout (MAX_STEP_NUM = 100 steps: fused CNN inference + softmax +
@@ -333,7 +333,8 @@ def a3c_config3(dev, seed, n_boards, updates=2, world=1, mode="textbook", featur
     cfg = A3CConfig(n_boards=n_boards, max_steps=100, mode=mode, net="cnn", bf16=True,
                     features=features, seed=seed, update_chunk=10)
     tr = A3CTrainer(cfg, device=dev)
-    tr.train_step()                                   # warm-up (allocator, kernels, first collective)
+    for _ in range(warmup):                           # warm-up (allocator, kernels, first collective, clocks)
+        tr.train_step()
     s = torch.cuda.current_stream(dev)
     roll_ms, upd_ms, steps = [], [], 0
     for _ in range(updates):
@@ -359,13 +360,13 @@ def a3c_config3(dev, seed, n_boards, updates=2, world=1, mode="textbook", featur
             "rollout_ms": r, "update_ms": u,
             "rollout_env_steps_per_s": board_steps / (r * 1e-3),
             "train_env_steps_per_s": board_steps / ((r + u) * 1e-3),
-            "valid_segment_steps_per_update": steps / updates,
+            "valid_segment_steps_per_update": steps / updates, "warmup_updates": warmup, "timed_updates": updates,
             "last_losses": {k: out[k] for k in ("actor_loss", "critic_loss")}}
 
 
-def dqn_config5(dev, seed, n_boards, steps=3, world=1):
+def dqn_config5(dev, seed, n_boards, steps=5, world=1, warmup=3):
     """BASELINE configs[4] (16M boards over 8 GPUs = 2^21 per GPU): ResNet-10 Q-network in bf16
-    (fused MFMA inference kernel for acting, structured-GEMM training path), epsilon-greedy acting
+    (fused MFMA inference kernel for acting, hand-written training step: dqn/train_step.py), epsilon-greedy acting
     on every board, env step with merge reward + auto-reset, (s, a, r, s', done) of every board
     into the HBM replay ring, one 64K-transition double-DQN update per env step (gradient and BN
     running statistics all-reduced when world > 1; each rank samples its own ring shard)."""
@@ -373,7 +374,10 @@ def dqn_config5(dev, seed, n_boards, steps=3, world=1):
     cfg = DQNConfig(n_boards=n_boards, replay_capacity=1 << 25, batch=1 << 16, learn_start=1, seed=seed,
                     act_chunk=1 << 18)
     tr = DQNTrainer(cfg, device=dev)
-    tr.train_step()                                   # warm-up (hipBLASLt heuristics, allocator)
+    # warm-up: allocator, packing caches, clocks; the first acts after start-up run 10-25 % slow
+    # (tools/probe_act2.py: 11.0, 9.8, 9.2, then 8.9-9.2 ms per 2^21-board act)
+    for _ in range(warmup):
+        tr.train_step()
     s = torch.cuda.current_stream(dev)
     act, env, upd = [], [], []
     for _ in range(steps):
@@ -405,6 +409,7 @@ def dqn_config5(dev, seed, n_boards, steps=3, world=1):
             "gradient_allreduce": ("%s of %d fp32 per update (+ %d BN running-statistics floats)"
                                    % (lab, tr.flat.grad.numel(), tr.bn_buffers.data.numel())) if lab else None,
             "act_ms": a_ms, "env_step_store_ms": e_ms, "update_ms": u_ms,
+            "warmup_steps": warmup, "timed_steps": steps,
             "env_steps_per_s": world * n_boards / ((a_ms + e_ms + u_ms) * 1e-3),
             "act_useful_TFLOPs": n_boards * useful / (a_ms * 1e-3) / 1e12,
             "act_frac_of_bf16_dense_peak": n_boards * useful / (a_ms * 1e-3) / 2.5e15,
