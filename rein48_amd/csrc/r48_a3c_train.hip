@@ -488,20 +488,21 @@ __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
         //     image, B = Dt with the column selector; 16x16x32, 8 feature tiles x 2 row steps)
         //   the dh2 image, block m written over h2 block m once its last dWh read is issued (one
         //     wave's LDS operations execute in order), then read back transposed: dh2^T (AGPRs)
-        //   db2 += row sums of dh2^T (16x16x32 with a selector B), one block behind
-        // Per step m (= 2p + g = feature block): dh2 MFMA m + 1, two dWh MFMAs, two db2 MFMAs, then
-        // the epilogue of m (bf16 pack + ReLU') -- the pipe runs under every epilogue.
+        //   db2 += row sums of dh2^T (16x16x32 with a selector B), two blocks behind
+        // Per step m (= 2p + g = feature block): dh2 MFMA m + 1, two dWh MFMAs (their h2^T operands
+        // read two MFMAs ahead), two db2 MFMAs, then the epilogue of m (bf16 pack + ReLU') -- the
+        // pipe runs under every epilogue.
         bf16x8 dh2[4][2][2];
         bf16x8 dh2t[4][2][2];
         {
             const bf16x8 sel0 = splat_frag(n16 == (g16 & 1) ? one2 : 0u);
             const bf16x8 sel1 = splat_frag(n16 == 2 + (g16 & 1) ? one2 : 0u);
             const bf16x8 bd0 = lds_frag(my + la.dr), bd1 = lds_frag(my + la.dr + 16);
-            bf16x8 A = trr(my, la, 0, 0);
+            bf16x8 A = trr(my, la, 0, 0), A1 = trr(my, la, 0, 1);
             f32x16 acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_at(w, kOffWhT, lane), dout, zero, 0, 0, 0);
             bf16x8 q = frag_at(w, kOffWhT + 1, lane);
 #pragma unroll
-            for (int m = 0; m <= 8; m++) {              // m = 2p + g = the feature block
+            for (int m = 0; m <= 9; m++) {              // m = 2p + g = the feature block
                 f32x16 nxt = acc;
                 if (m + 1 < 8) {
                     const bf16x8 wa = q;
@@ -513,13 +514,14 @@ __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
                 if (m < 8) {
 #pragma unroll
                     for (int k = 2 * m; k < 2 * m + 2; k++) {
-                        const bf16x8 An = k + 1 < 16 ? trr(my, la, (k + 1) >> 1, (k + 1) & 1) : A;
+                        const bf16x8 An = k + 2 < 16 ? trr(my, la, (k + 2) >> 1, (k + 2) & 1) : A;
                         acc16_lds(dwh[m], A, (k & 1) ? bd1 : bd0);
-                        A = An;
+                        A = A1;
+                        A1 = An;
                     }
                 }
-                if (m >= 1) {                           // db2 of block m - 1 (read at step m - 1)
-                    const int b = m - 1;
+                if (m >= 2) {                           // db2 of block m - 2 (read at step m - 2)
+                    const int b = m - 2;
 #pragma unroll
                     for (int s = 0; s < 2; s++) {
                         if (b == 0 && s == 0)
@@ -546,7 +548,8 @@ __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
         }
         // ---------------- per conv1 position R: h1^T_R, dh1^T_R, dW2, dW1. Software-pipelined: the
         // h1^T MFMA of R + 1 and the dh1^T epilogue + dW1 MFMAs of R - 1 are issued in the shadow of
-        // R's first dh1 MFMA, so no MFMA waits on an epilogue at a position boundary
+        // R's first dh1 MFMA, so no MFMA waits on an epilogue at a position boundary; the dW2 MFMAs
+        // of R alternate with the dh1 chain's, so no two consecutive MFMAs share an accumulator
         {
             const float b1c = bl[col];
             f32x16 b1s;
@@ -567,8 +570,9 @@ __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
                 const bf16x8 w1n = frag_at(w, R + 1 < 9 ? R + 1 : 0, lane);
                 bf16x8 h1t[2], t0, t1;
                 f32x16 d = zero, a1n = a1;
-                // (1) the dh1^T chain of R (independent of h1^T_R); the h1^T epilogue of R and the
-                // dh1^T epilogue of R - 1 run under it, the h1^T MFMA of R + 1 issues after its first
+                // (1) the dh1^T chain of R (independent of h1^T_R), interleaved with (2); the h1^T
+                // epilogue of R and the dh1^T epilogue of R - 1 run under it, the h1^T MFMA of R + 1
+                // issues after its first
 #pragma unroll
                 for (int m = 4 * kRFirst[R]; m < 4 * kRFirst[R + 1]; m++) {
                     const int n = m >> 2, p = kDh1P[n], g = (m >> 1) & 1, s = m & 1;
@@ -590,20 +594,26 @@ __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
                         t0 = mask_pk(acc_to_frag(dprev, 0), hprev[0]);
                         t1 = mask_pk(acc_to_frag(dprev, 1), hprev[1]);
                     }
+                    // (2) interleaved: dW2[ot = g'][kk'] += dh2_p'^T (o-tile g', row step s') x
+                    // h1^T_R (row step s') for step m - 1 of R, between two MFMAs of the dh1 chain
+                    if (m > first) {
+                        const int mp = m - 1, np = mp >> 2, pp = kDh1P[np], kp = kDh1K[np];
+                        const int gp = (mp >> 1) & 1, sp = mp & 1;
+                        if (mp < first + 2)   // the first may follow the h1^T epilogue closely
+                            acc32_av(dw2[gp][kp], dh2t[pp][gp][sp], h1t[sp]);
+                        else
+                            acc32_a(dw2[gp][kp], dh2t[pp][gp][sp], h1t[sp]);
+                    }
+                    wfence();
                 }
                 if (R > 0) {
                     acc16_v(dw1, t0, xprev[0]);
                     acc16_v(dw1, t1, xprev[1]);
                 }
-                // (2) dW2[ot = g][kk] += dh2_p^T (o-tile g, row step s) x h1^T_R (row step s) for
-                // every (p, kk) of R
-#pragma unroll
-                for (int m = 4 * kRFirst[R]; m < 4 * kRFirst[R + 1]; m++) {
-                    const int n = m >> 2, p = kDh1P[n], kk = kDh1K[n], g = (m >> 1) & 1, s = m & 1;
-                    if (m < 4 * kRFirst[R] + 4)   // the first pair may follow the h1^T epilogue closely
-                        acc32_av(dw2[g][kk], dh2t[p][g][s], h1t[s]);
-                    else
-                        acc32_a(dw2[g][kk], dh2t[p][g][s], h1t[s]);
+                {   // the last dW2 MFMA of R
+                    const int mp = 4 * kRFirst[R + 1] - 1, np = mp >> 2, pp = kDh1P[np], kp = kDh1K[np];
+                    const int gp = (mp >> 1) & 1, sp = mp & 1;
+                    acc32_a(dw2[gp][kp], dh2t[pp][gp][sp], h1t[sp]);
                 }
                 dprev = d;
                 hprev[0] = h1t[0], hprev[1] = h1t[1];

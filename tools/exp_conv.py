@@ -1,5 +1,7 @@
 """GPU experiment: device time of the config-5 update convolutions (r48_conv3x3 forward at 64 and 32
-input channels, r48_conv3x3_wgrad at 64 and 32) for the product library and variant libraries
+input channels, with the BN statistics epilogue (fwd64s), the data gradient with the BN-backward
+reduction epilogue with and without the residual add (dg64bn, add64bn), r48_conv3x3_wgrad at 64 and
+32) for the product library and variant libraries
 (tools/build_variant.sh), at `boards` boards, with a bit-level digest of every output.
 
     python tools/exp_conv.py [boards] [lib.so ...]
@@ -36,6 +38,17 @@ w64 = torch.randn(64, 64, 3, 3, generator=g).to(dev) * 0.05
 w32 = torch.randn(64, 32, 3, 3, generator=g).to(dev) * 0.05
 bias = torch.randn(64, generator=g).to(dev)
 f64, f32 = C.pack_conv(w64, 64), C.pack_conv(w32, 32)
+masks = [torch.randint(0, 256, (B * 16, 8), generator=g, dtype=torch.uint8).to(dev) for _ in range(NR)]
+save = torch.cat([torch.randn(64, generator=g), torch.rand(64, generator=g) + 0.5]).to(dev)
+stats = None
+part = None
+
+
+def bn_grad(dy_, add_, bnx, mask):
+    out = torch.empty_like(dy_)
+    C.check(_lib.load().r48_conv3x3_bn_grad(C.ptr(dy_), B, C.ptr(f64), C.ptr(add_), C.ptr(out), C.ptr(bnx),
+                                            C.ptr(mask), C.ptr(save), C.ptr(part), C._stream(dy_)))
+    return out
 
 
 def digest(t):
@@ -58,12 +71,18 @@ def timed(fn, reps=20):
 
 # algorithmic HBM bytes: activations in + out (bf16); wgrad reads dy and x
 io = {"fwd64": B * 16 * (64 + 64) * 2, "fwd32": B * 16 * (32 + 64) * 2, "add64": B * 16 * (64 + 64 + 64) * 2,
+      "fwd64s": B * 16 * (64 + 64) * 2, "dg64bn": B * 16 * (3 * 64 * 2 + 8), "add64bn": B * 16 * (4 * 64 * 2 + 8),
       "wgrad64": B * 16 * (64 + 64) * 2, "wgrad32": B * 16 * (64 + 32) * 2}
 for path in libs:
     _lib.LIB_PATH, _lib._lib = path, None
     C._WS.clear()
+    stats = torch.empty(int(_lib.load().r48_conv_stats_floats()), dtype=torch.float32, device=dev)
+    part = stats
     runs = {"fwd64": lambda: C.conv3x3(rot(x64s), f64, bias), "fwd32": lambda: C.conv3x3(rot(x32s), f32, bias),
             "add64": lambda: C.conv3x3(rot(x64s), f64, bias, add=rot(dys)),
+            "fwd64s": lambda: C.conv3x3(rot(x64s), f64, bias, stats=stats),
+            "dg64bn": lambda: bn_grad(rot(dys), None, rot(x64s), rot(masks)),
+            "add64bn": lambda: bn_grad(rot(dys), rot(x64s), rot(x64s), rot(masks)),
             "wgrad64": lambda: C.conv3x3_wgrad(rot(dys), rot(x64s)), "wgrad32": lambda: C.conv3x3_wgrad(rot(dys), rot(x32s))}
     line = []
     for k, fn in runs.items():
