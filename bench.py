@@ -153,9 +153,14 @@ def timed_steps(env, plan, W, chunk, world, dev):
         torch.cuda.synchronize(dev)
     s = torch.cuda.current_stream(dev)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in plan]
-    for a, b in ev:       # torch creates the HIP events at their first record: not inside the region
+    # one untimed pass through the region's exact host path (event records, the calls, the closing
+    # event wait): torch creates the HIP events at their first record, and the first pass through
+    # this path runs slower on the host than every later one -- neither belongs in the region
+    for (a, b), c in zip(ev, plan):
         a.record(s)
+        env.step_n(c, auto_reset=True)
         b.record(s)
+    ev[-1][1].synchronize()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
