@@ -154,8 +154,8 @@ def timed_steps(env, plan, W, chunk, world, dev):
     s = torch.cuda.current_stream(dev)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in plan]
     # one untimed pass through the region's exact host path (event records, the calls, the closing
-    # event wait): torch creates the HIP events at their first record, and the first pass through
-    # this path runs slower on the host than every later one -- neither belongs in the region
+    # event wait): torch creates the HIP events at their first record, which does not belong in the
+    # region (a first-pass host effect beyond that was not measurable: tools/show_bench20.py runs)
     for (a, b), c in zip(ev, plan):
         a.record(s)
         env.step_n(c, auto_reset=True)
