@@ -439,7 +439,17 @@ __global__ __launch_bounds__(64 * kWgWaves, 1) void k_conv_wgrad(const uint16_t 
                               lane);
         }
     };
-    static_assert(kKSteps == 4, "the step loop splits compute into two halves");
+    // one DMA of this wave (its k-th of the step) for step i into ring buffer `buf`
+    auto stage_one = [&](int64_t i, int buf, int k) {
+        uint16_t *dimg = lds + buf * kBuf, *ximg = dimg + kDyImg;
+        const int64_t row0 = ((int64_t)blockIdx.x + i * gridDim.x) * kStepRows;
+        const int d = wave + k * kWgWaves;
+        if (d < kDyDmas)
+            dma_rows<kCout>(dy, row0 + d * kDyRowsPerDma, last, dimg, d * kDyRowsPerDma, lane);
+        else if (d < kDmas)
+            dma_rows<CIN>(x, row0 + (d - kDyDmas) * kXRowsPerDma, last, ximg, (d - kDyDmas) * kXRowsPerDma, lane);
+    };
+    static_assert(kKSteps == 4 && kDmas <= kKSteps * kWgWaves, "one DMA per wave and k-step");
     auto compute = [&](int buf, int ks0, int ks1) {
         const uint16_t *img = lds + buf * kBuf;
 #pragma unroll
@@ -485,13 +495,26 @@ __global__ __launch_bounds__(64 * kWgWaves, 1) void k_conv_wgrad(const uint16_t 
                 ximg[real * CIN + i] = 0;
             __syncthreads();
         }
-        // the DMAs of step i + kRing - 1 (into the buffer of step i - 1) issue between the two
-        // k-steps, under the first one's MFMAs, not in a burst of all waves after the barrier
-        compute(buf, 0, 2);
-        __builtin_amdgcn_sched_barrier(0);
-        stage(i + kRing - 1, (buf + kRing - 1) % kRing);
-        __builtin_amdgcn_sched_barrier(0);
-        compute(buf, 2, 4);
+        if constexpr (kDmas == kKSteps * kWgWaves) {
+            // one DMA of step i + kRing - 1 (into the buffer of step i - 1) per k-step and wave: the
+            // CU's 32 DMAs of a step issue in four bursts of 8 instead of one burst right after the
+            // barrier, which queued each wave's issue behind the others' (tools/exp_conv.py, inputs
+            // past the Infinity Cache: 92-95 -> 85-87 us; inside the update, with dy just written and
+            // cache-resident: 77 us either way)
+#pragma unroll
+            for (int ks = 0; ks < kKSteps; ks++) {
+                stage_one(i + kRing - 1, (buf + kRing - 1) % kRing, ks);
+                compute(buf, ks, ks + 1);
+            }
+        } else {
+            // 3 DMAs per wave (32 input channels): issued between the two k-step halves, under the
+            // first one's MFMAs (measured faster here than one per k-step)
+            compute(buf, 0, 2);
+            __builtin_amdgcn_sched_barrier(0);
+            stage(i + kRing - 1, (buf + kRing - 1) % kRing);
+            __builtin_amdgcn_sched_barrier(0);
+            compute(buf, 2, 4);
+        }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");              // no DMA outlives the kernel
     // record: D[m = co 16][n = ci 16], lane l: column i16 (ci), rows 4g + i (co). 24 wait states

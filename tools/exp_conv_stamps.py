@@ -1,5 +1,5 @@
 """Reads the k_conv_wgrad<64> phase stamps of a tools/stamp_conv.py build (GPU): mean cycles per
-step and wave in (vmcnt wait, barrier, DMA issue, compute) at `boards` boards.
+step and wave in (vmcnt wait, barrier, k-steps + DMA issue) at `boards` boards.
     python tools/exp_conv_stamps.py build/lib_conv_stamp.so [boards]"""
 import os
 import sys
@@ -23,10 +23,10 @@ ws = C._WS[(64, str(dev))]
 grid = torch.cuda.get_device_properties(0).multi_processor_count
 rec = 9 * 64 * 64
 W = 8                                                                            # waves per workgroup
-st = torch.stack([ws[g * rec:g * rec + 8 * W].view(torch.int64) for g in range(grid)]).cpu()   # [grid, 4 W]
-steps = (B * 16 + 63) // 64 / grid
-names = ["vmcnt wait", "barrier", "DMA issue", "compute"]
-tot = st.double().mean(0).view(W, 4).mean(0)
+st = torch.stack([ws[g * rec:g * rec + 16 * W].view(torch.int64) for g in range(grid)]).cpu()   # [grid, 8 W]
+steps = (B * 16 + 127) // 128 / grid
+names = ["vmcnt wait", "barrier", "-", "-", "k-steps + DMAs"]
+tot = st.double().mean(0).view(W, 8).mean(0)[:5]
 print("boards %d, %.1f steps per workgroup; cycles per step per wave:" % (B, steps))
 for k, n in enumerate(names):
     print("  %-12s %8.1f" % (n, float(tot[k]) / steps))
