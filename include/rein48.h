@@ -301,6 +301,14 @@ int r48_td_target(const float *reward, const uint8_t *done, const float *q_next_
 int r48_huber_grad(const float *q, const int8_t *action, const float *y, int64_t n, float *dq, float *out,
                    float *workspace, void *stream);
 
+/* Adam (torch.optim.Adam: bias-corrected, eps outside the square root) over one flat fp32
+ * parameter buffer of n floats (n % 4 == 0, all four buffers 16-byte aligned), step = the 1-based
+ * step count t: m = b1 m + (1 - b1) g; v = b2 v + (1 - b2) g^2;
+ * param -= lr / (1 - b1^t) * m / (sqrt(v / (1 - b2^t)) + eps). One launch. Replaces the flat
+ * optimizer step of rein48_amd/dqn/trainer.py's Adam on the GPU. */
+int r48_adam(float *param, const float *grad, float *m, float *v, int64_t n, float lr, float beta1, float beta2,
+             float eps, int64_t step, void *stream);
+
 /* ---- The ResNet-10 update's 3x3 convolutions on the 4x4 grid (csrc/r48_conv.hip) ----
  * Channels-last bf16 activations [boards][16 cells][C], 64 output channels, 32 or 64 input
  * channels; only the 100 in-grid (cell, tap) pairs are computed. Replace the structured dense

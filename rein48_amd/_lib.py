@@ -51,6 +51,7 @@ SIGNATURES = {
     "r48_q_head_forward": (C.c_int, [_P, _I64, _P, _P, _P, _P]),
     "r48_conv_pack_resnet": (C.c_int, [_P, _P, _P, _P]),
     "r48_huber_grad": (C.c_int, [_P, _P, _P, _I64, _P, _P, _P, _P]),
+    "r48_adam": (C.c_int, [_P, _P, _P, _P, _I64, C.c_float, C.c_float, C.c_float, C.c_float, _I64, _P]),
     "r48_q_head_workspace_floats": (_I64, []),
     "r48_q_head_backward": (C.c_int, [_P, _P, _I64, _P, _P, _P, _P, _P]),
     "r48_egreedy_actions": (C.c_int, [_P, _I64, C.c_float, _U64, _I64, _U32, _P, _P]),

@@ -21,6 +21,7 @@ Each rank owns boards [rank*N, (rank+1)*N) and its own ring shard; no replay tra
 GPUs.
 """
 import copy
+import ctypes as C
 import math
 from dataclasses import dataclass
 
@@ -73,6 +74,15 @@ class Adam:
     def step(self):
         self.t += 1
         g = self.flat.grad
+        p = self.flat.data
+        if p.is_cuda and p.dtype == torch.float32 and p.numel() % 4 == 0 and g.is_contiguous():
+            # one fused launch (r48_adam) instead of the ~8 elementwise launches below
+            from .. import _lib
+            from .._lib import check, ptr
+            check(_lib.load().r48_adam(ptr(p), ptr(g), ptr(self.m), ptr(self.v), p.numel(), float(self.lr),
+                                       float(self.b1), float(self.b2), float(self.eps), self.t,
+                                       C.c_void_p(torch.cuda.current_stream(p.device).cuda_stream)))
+            return
         self.m.mul_(self.b1).add_(g, alpha=1 - self.b1)
         self.v.mul_(self.b2).addcmul_(g, g, value=1 - self.b2)
         c1, c2 = 1 - self.b1 ** self.t, 1 - self.b2 ** self.t

@@ -616,3 +616,30 @@ def test_conv_pack_resnet_matches_host_packing():
         assert torch.equal(fwd[i].view(-1), pack_conv(c.weight, 32 if i == 0 else 64).view(-1)), i
         if i:
             assert torch.equal(dg[i].view(-1), pack_conv_dgrad(c.weight).view(-1)), i
+
+
+def test_fused_adam_matches_torch_adam():
+    """r48_adam (trainer.Adam on a GPU fp32 flat buffer: one launch) vs torch.optim.Adam over the same
+    parameters and gradients for 6 steps: the same fp32 update formula, fused (contractions may round
+    differently), so parameters agree to 1e-6 relative; the first step's update is exactly lr in
+    size where the gradient is nonzero."""
+    from rein48_amd.a3c.optim import FlatParams
+    from rein48_amd.dqn.trainer import Adam
+    torch.manual_seed(7)
+    a = torch.nn.Linear(64, 36).to(DEV)                 # 64*36 + 36 = 2340 floats: a multiple of 4
+    b = torch.nn.Linear(64, 36).to(DEV)
+    b.load_state_dict(a.state_dict())
+    flat = FlatParams(a)
+    assert flat.data.numel() % 4 == 0
+    mine = Adam(flat, lr=1e-3)
+    ref = torch.optim.Adam(b.parameters(), lr=1e-3)
+    for _ in range(6):
+        x = torch.randn(32, 64, device=DEV)
+        flat.zero_grad()
+        a(x).square().sum().backward()
+        mine.step()
+        ref.zero_grad()
+        b(x).square().sum().backward()
+        ref.step()
+    torch.testing.assert_close(a.weight, b.weight, rtol=1e-6, atol=1e-7)
+    torch.testing.assert_close(a.bias, b.bias, rtol=1e-6, atol=1e-7)
