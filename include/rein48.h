@@ -188,6 +188,19 @@ int r48_discounted_returns(const float *rewards, const int32_t *lengths, const f
                            int32_t T, int64_t n, float gamma, int32_t drop_last, float *out,
                            void *stream);
 
+/* Per-segment constants of the A3C loss (losses.segment_stats; a3c.py:99-123) for n segments of
+ * lengths[i] (1..T) steps, time-major [T][n]: B[i] = max(lengths[i], 1); with td_sum (nullable):
+ * td_sum[i] = sum over t < lengths[i] of targets[t][i] - values[t][i]; counts float[n][4] (16-byte
+ * aligned) = per-segment action counts over t < lengths[i]. Replaces the masked sums and the
+ * scatter-add of the tensor form (fp32 sums in step order). */
+int r48_a3c_segment_stats(const float *values, const float *targets, const int8_t *actions, const int32_t *lengths,
+                          int32_t T, int64_t n, float *B, float *td_sum, float *counts, void *stream);
+/* The fused update's per-row weights over [T][n]: wn = (m / B[i]) * (1 / n) with m = t < lengths[i];
+ * cm (nullable, the reference loss) = ((td_sum[i] / ((4 B[i]) B[i])) m) * (1 / n) -- the operation
+ * order (and fp32 reciprocal) of the tensor form in rein48_amd/a3c/trainer.py, bit-identical to it. */
+int r48_a3c_row_weights(const int32_t *lengths, const float *B, const float *td_sum, int32_t T, int64_t n, float *wn,
+                        float *cm, void *stream);
+
 /* tf.train.RMSPropOptimizer(lr) (a3c.py:264-265; TF1 semantics: ms slot starts at ONES, eps
  * inside the sqrt, momentum 0 by default) over one flat float32 parameter buffer of n values. */
 int r48_rmsprop_tf1(float *var, const float *grad, float *ms, float *mom, int64_t n, float lr,

@@ -58,6 +58,42 @@ def discounted_returns(rewards, lengths, bootstrap, gamma=0.9, drop_last=True):
     return out
 
 
+def segment_stats(actions, lengths, values=None, targets=None):
+    """losses.segment_stats for segments of `lengths` steps (mask = t < lengths), as one launch:
+    actions int8 [T, n], lengths int32 [n], values/targets float32 [T, n] (both or neither) ->
+    dict(B [n], counts [n, 4], and td_sum [n] when values/targets are given)."""
+    _dev(actions, "actions", torch.int8)
+    _dev(lengths, "lengths", torch.int32)
+    if (values is None) != (targets is None):
+        raise ValueError("values and targets go together")
+    if values is not None:
+        _dev(values, "values", torch.float32)
+        _dev(targets, "targets", torch.float32)
+    T, n = actions.shape
+    dev = actions.device
+    out = {"B": torch.empty(n, dtype=torch.float32, device=dev),
+           "counts": torch.empty((n, 4), dtype=torch.float32, device=dev)}
+    if values is not None:
+        out["td_sum"] = torch.empty(n, dtype=torch.float32, device=dev)
+    check(_lib.load().r48_a3c_segment_stats(ptr(values), ptr(targets), ptr(actions), ptr(lengths), T, n, ptr(out["B"]),
+                                            ptr(out.get("td_sum")), ptr(out["counts"]), _stream(actions)))
+    return out
+
+
+def row_weights(lengths, B, T, td_sum=None):
+    """The fused update's per-row weights [T, n]: wn = mask / B / n and, with td_sum (the
+    reference loss), cm = td_sum / (4 B B) * mask / n, in the tensor form's operation order."""
+    _dev(lengths, "lengths", torch.int32)
+    _dev(B, "B", torch.float32)
+    n = lengths.numel()
+    wn = torch.empty((T, n), dtype=torch.float32, device=lengths.device)
+    cm = torch.empty_like(wn) if td_sum is not None else None
+    if td_sum is not None:
+        _dev(td_sum, "td_sum", torch.float32)
+    check(_lib.load().r48_a3c_row_weights(ptr(lengths), ptr(B), ptr(td_sum), T, n, ptr(wn), ptr(cm), _stream(wn)))
+    return wn, cm
+
+
 def rmsprop_tf1_(var, grad, ms, mom, lr, decay=0.9, momentum=0.0, eps=1e-10):
     """In-place TF1 RMSProp step on flat float32 buffers."""
     for t, name in ((var, "var"), (grad, "grad"), (ms, "ms"), (mom, "mom")):

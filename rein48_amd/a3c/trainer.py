@@ -204,7 +204,9 @@ class A3CTrainer:
             boot = torch.where(self.finished, torch.zeros_like(v_last), v_last.view(n)).float().contiguous()
             targets = K.discounted_returns(self.rewards, self.lengths, boot, cfg.gamma,
                                            drop_last=cfg.mode == "reference")
-            if v_all is not None:
+            if self.actions.is_cuda:    # one launch (r48_a3c_segment_stats) for the masked sums + counts
+                stats = K.segment_stats(self.actions, self.lengths, v_all, None if v_all is None else targets)
+            elif v_all is not None:
                 stats = segment_stats(v_all, targets, self.actions, self.mask)
             else:
                 stats = {"B": self.mask.float().sum(0).clamp(min=1.0)}
@@ -242,12 +244,11 @@ class A3CTrainer:
         from .fused import cnn_train_grad, pack_cnn_train
         cfg = self.cfg
         n = cfg.n_boards
-        m = self.mask.float()
-        wn = (m / stats["B"][None, :] / n).contiguous()
-        cm = counts = None
-        if cfg.mode == "reference":
-            cm = ((stats["td_sum"] / (4.0 * stats["B"] * stats["B"]))[None, :] * m / n).contiguous()
-            counts = stats["counts"].float().contiguous()
+        ref = cfg.mode == "reference"
+        # wn = mask / (B n), cm = (td_sum / (4 B^2)) mask / n as one launch (r48_a3c_row_weights)
+        wn, cm = K.row_weights(self.lengths, stats["B"].contiguous(), cfg.max_steps,
+                               stats["td_sum"].contiguous() if ref else None)
+        counts = stats["counts"].float().contiguous() if ref else None
         if getattr(self, "_train_ws", None) is None:
             self._train_ws = torch.empty(_lib_workspace_floats(), dtype=torch.float32, device=self.device)
         grads, actor, critic = cnn_train_grad(

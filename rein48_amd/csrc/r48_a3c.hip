@@ -181,6 +181,76 @@ int launched(const char *what)
     return R48_OK;
 }
 
+// Per-segment constants of the A3C loss (losses.segment_stats, a3c.py:99-123) for segments of
+// length len[i] (mask = t < len[i]): B[i] = max(len[i], 1); td_sum[i] = sum over t < len[i] of
+// targets[t][i] - values[t][i]; counts[i][k] = #{t < len[i] : actions[t][i] == k}. One lane per
+// segment; the T rows are coalesced across lanes, 8 rows of loads in flight.
+template <bool TD>
+__global__ __launch_bounds__(kBlock) void k_segment_stats(const float *__restrict__ values,
+                                                          const float *__restrict__ targets,
+                                                          const int8_t *__restrict__ actions,
+                                                          const int32_t *__restrict__ len, int32_t T, int64_t n,
+                                                          float *__restrict__ B, float *__restrict__ td_sum,
+                                                          float4 *__restrict__ counts)
+{
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n)
+        return;
+    const int32_t L = min(max(len[i], 0), T);
+    float td = 0.0f, c[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    constexpr int kAhead = 8;
+    int32_t t = 0;
+    for (; t + kAhead <= L; t += kAhead) {
+        float d[kAhead];
+        int a[kAhead];
+#pragma unroll
+        for (int k = 0; k < kAhead; k++) {
+            const int64_t o = (int64_t)(t + k) * n + i;
+            d[k] = TD ? targets[o] - values[o] : 0.0f;
+            a[k] = actions[o] & 3;
+        }
+#pragma unroll
+        for (int k = 0; k < kAhead; k++) {
+            td += d[k];
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                c[q] += a[k] == q ? 1.0f : 0.0f;
+        }
+    }
+    for (; t < L; t++) {
+        const int64_t o = (int64_t)t * n + i;
+        if (TD)
+            td += targets[o] - values[o];
+        const int a = actions[o] & 3;
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            c[q] += a == q ? 1.0f : 0.0f;
+    }
+    B[i] = (float)max(L, 1);
+    if (TD)
+        td_sum[i] = td;
+    counts[i] = make_float4(c[0], c[1], c[2], c[3]);
+}
+
+// The fused update's per-row weights (trainer._fused_gradient) over the [T][n] rows, in
+// PyTorch's operation order so both are bit-identical to the tensor form (a tensor divided by a
+// scalar is multiplied by the fp32 reciprocal there): m = t < len[i]; wn = (m / B[i]) (1 / n);
+// reference loss: cm = ((td_sum[i] / ((4 B[i]) B[i])) m) (1 / n).
+__global__ __launch_bounds__(kBlock) void k_row_weights(const int32_t *__restrict__ len, const float *__restrict__ B,
+                                                        const float *__restrict__ td_sum, int32_t T, int64_t n,
+                                                        float *__restrict__ wn, float *__restrict__ cm)
+{
+    const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (r >= (int64_t)T * n)
+        return;
+    const int64_t i = r % n;
+    const int32_t t = (int32_t)(r / n);
+    const float m = t < len[i] ? 1.0f : 0.0f, inv_n = 1.0f / (float)n, b = B[i];
+    wn[r] = (m / b) * inv_n;
+    if (cm)
+        cm[r] = ((td_sum[i] / ((4.0f * b) * b)) * m) * inv_n;
+}
+
 }  // namespace
 
 extern "C" {
@@ -249,6 +319,37 @@ int r48_discounted_returns(const float *rewards, const int32_t *lengths, const f
         hipLaunchKernelGGL(k_returns<false>, grid_for(n), dim3(kBlock), 0, (hipStream_t)stream, rewards, lengths,
                            bootstrap, T, n, gamma, out);
     return launched("k_returns");
+}
+
+int r48_a3c_segment_stats(const float *values, const float *targets, const int8_t *actions, const int32_t *lengths,
+                          int32_t T, int64_t n, float *B, float *td_sum, float *counts, void *stream)
+{
+    const bool td = td_sum != nullptr;
+    if (!actions || !lengths || !B || !counts || T < 1 || n < 0 || (td && (!values || !targets)) ||
+        (reinterpret_cast<uintptr_t>(counts) & 15))
+        return fail(R48_EINVAL, "r48_a3c_segment_stats: NULL argument (values/targets needed with td_sum), T < 1, "
+                                "n < 0 or counts not 16-byte aligned");
+    if (n == 0)
+        return R48_OK;
+    if (td)
+        hipLaunchKernelGGL(k_segment_stats<true>, grid_for(n), dim3(kBlock), 0, (hipStream_t)stream, values, targets,
+                           actions, lengths, T, n, B, td_sum, reinterpret_cast<float4 *>(counts));
+    else
+        hipLaunchKernelGGL(k_segment_stats<false>, grid_for(n), dim3(kBlock), 0, (hipStream_t)stream, values, targets,
+                           actions, lengths, T, n, B, td_sum, reinterpret_cast<float4 *>(counts));
+    return launched("k_segment_stats");
+}
+
+int r48_a3c_row_weights(const int32_t *lengths, const float *B, const float *td_sum, int32_t T, int64_t n, float *wn,
+                        float *cm, void *stream)
+{
+    if (!lengths || !B || !wn || T < 1 || n < 0 || (cm && !td_sum))
+        return fail(R48_EINVAL, "r48_a3c_row_weights: NULL argument (td_sum needed with cm), T < 1 or n < 0");
+    if (n == 0)
+        return R48_OK;
+    hipLaunchKernelGGL(k_row_weights, grid_for((int64_t)T * n), dim3(kBlock), 0, (hipStream_t)stream, lengths, B,
+                       td_sum, T, n, wn, cm);
+    return launched("k_row_weights");
 }
 
 }  // extern "C"

@@ -351,3 +351,30 @@ def test_rollout_megakernel_equals_per_step_rollout(mode, n_boards):
             assert torch.equal(a, b)
         else:
             assert a == b
+
+
+def test_segment_stats_and_row_weights_match_tensor_forms():
+    """r48_a3c_segment_stats / r48_a3c_row_weights (the fused update's per-segment constants and
+    per-row weights) vs losses.segment_stats and the tensor formulas they replace, on ragged segment
+    lengths 1..T: B and the action counts exact, td_sum to fp32 summation order (1e-5 of the summed
+    magnitudes), wn and cm bit-identical (same operation order and fp32 reciprocal of n)."""
+    from rein48_amd.a3c import kernels as K
+    from rein48_amd.a3c.losses import segment_stats
+    T, n = 100, 70001
+    g = torch.Generator(device="cpu").manual_seed(11)
+    lengths = torch.randint(1, T + 1, (n,), generator=g, dtype=torch.int32).to(DEV)
+    lengths[:5] = torch.tensor([1, T, 2, T - 1, 50], dtype=torch.int32)
+    actions = torch.randint(0, 4, (T, n), generator=g, dtype=torch.int8).to(DEV)
+    values = torch.randn(T, n, generator=g).to(DEV)
+    targets = torch.randn(T, n, generator=g).to(DEV)
+    mask = torch.arange(T, device=DEV).unsqueeze(1) < lengths.unsqueeze(0)
+    want = segment_stats(values, targets, actions, mask)
+    got = K.segment_stats(actions, lengths, values, targets)
+    assert torch.equal(got["B"], want["B"]) and torch.equal(got["counts"], want["counts"])
+    mag = ((targets - values).abs() * mask).sum(0)
+    assert bool(((got["td_sum"] - want["td_sum"]).abs() <= 1e-5 * mag + 1e-30).all())
+    assert torch.equal(K.segment_stats(actions, lengths)["counts"], want["counts"])
+    m = mask.float()
+    wn, cm = K.row_weights(lengths, got["B"], T, got["td_sum"])
+    assert torch.equal(wn, m / got["B"][None, :] / n)
+    assert torch.equal(cm, (got["td_sum"] / (4.0 * got["B"] * got["B"]))[None, :] * m / n)
