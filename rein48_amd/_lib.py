@@ -97,8 +97,8 @@ SIGNATURES = {
     "r48_a3c_segment_stats": (C.c_int, [_P, _P, _P, _P, _I32, _I64, _P, _P, _P, _P]),
     "r48_a3c_row_weights": (C.c_int, [_P, _P, _P, _I32, _I64, _P, _P, _P]),
     "r48_rmsprop_tf1": (C.c_int, [_P, _P, _P, _P, _I64, C.c_float, C.c_float, C.c_float, C.c_float, _P]),
-    "r48_cnn_rollout": (C.c_int, [_P, _I64, _I32, _P, _P, _I32, _P, _P, _P, _P, _P, _U64, _I64, _U32, _U64, _U32,
-                                  _U32, _P]),
+    "r48_cnn_rollout": (C.c_int, [_P, _I64, _I32, _P, _P, _I32, _P, _P, _P, _P, _P, _P, _U64, _I64, _U32, _U64,
+                                  _U32, _U32, _P]),
     "r48_cnn_policy_forward": (C.c_int, [_P, _I64, _P, _P, _I32, _P, _P, _P, _P, _U64, _I64, _U32, _P]),
     "r48_last_error": (C.c_char_p, []),
     "r48_version": (C.c_char_p, []),

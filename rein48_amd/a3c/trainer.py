@@ -52,6 +52,7 @@ class A3CConfig:
     fused_policy: bool = True     # cnn + bf16: rollout inference in one fused MFMA kernel (r48_policy.hip)
     fused_update: bool = True     # cnn + bf16: the whole update's gradient in one fused pass (r48_a3c_train.hip)
     fused_rollout: bool = True    # cnn + bf16: all max_steps policy + env steps in one launch (r48_cnn_rollout)
+    rollout_values: bool = True   # fused rollout, reference loss: V(s_t) written by the rollout (no value pass)
 
 
 class A3CTrainer:
@@ -74,6 +75,7 @@ class A3CTrainer:
         self.rewards = torch.zeros((T, n), dtype=torch.float32, device=self.device)
         self.sample_ctr = 0
         self.updates = 0
+        self._rollout_v = None       # [T, n] V(boards[t]) from the last megakernel rollout, or None
 
     # ------------------------------------------------------------------ helpers
     def _features(self, boards):
@@ -88,6 +90,7 @@ class A3CTrainer:
     def rollout(self):
         cfg, env = self.cfg, self.env
         env.reset()
+        self._rollout_v = None
         merge = cfg.mode == "textbook"
         if not merge:
             self.rewards.zero_()  # GameClient.py:138: reward is always 0
@@ -159,16 +162,26 @@ class A3CTrainer:
         T, n = cfg.max_steps, cfg.n_boards
         step0, resets = env.counters
         self._lengths = torch.empty(n, dtype=torch.int32, device=self.device)
+        # the reference loss needs V of every training state (a3c.py:218-223): the rollout's policy
+        # pass computes the value head anyway, so it writes V(boards[t]) (same arithmetic as the
+        # r48_cnn_policy_forward value pass it replaces, bit for bit)
+        values = None
+        if cfg.mode == "reference" and cfg.rollout_values:
+            if getattr(self, "_v_buf", None) is None:
+                self._v_buf = torch.empty((T, n), dtype=torch.float32, device=self.device)
+            values = self._v_buf
         _lib.check(_lib.load().r48_cnn_rollout(
             env.boards.data_ptr(), n, T, wfrag.data_ptr(), bias.data_ptr(),
             _lib.FEAT_EXPONENTS if cfg.features == "exponents" else _lib.FEAT_VALUES,
             self.boards.data_ptr(), self.actions.data_ptr(), self.done.data_ptr(),
             self._rewards_i32.data_ptr() if merge else None, self._lengths.data_ptr(),
-            int(cfg.seed) & (2 ** 64 - 1), self.gid0,
+            None if values is None else values.data_ptr(), int(cfg.seed) & (2 ** 64 - 1), self.gid0,
             self.sample_ctr & 0xFFFFFFFF, int(env.seed) & (2 ** 64 - 1), step0,
             _lib.MERGE_REWARD if merge else 0, torch.cuda.current_stream(self.device).cuda_stream))
         self.sample_ctr += T
         env.counters = (step0 + T, resets)
+        if values is not None:
+            self._rollout_v = (values, self.updates)   # valid while the weights are those of this rollout
 
     # ------------------------------------------------------------------ update (a3c.py:218-234)
     def _states(self):
@@ -192,7 +205,16 @@ class A3CTrainer:
             # per-segment td_sum, so only the reference loss (or the unfused path) pays this pass
             need_values = not (fused and cfg.fused_update and cfg.mode == "textbook")
             v_all = None
-            if need_values:
+            rv = self._rollout_v
+            if need_values and rv is not None and rv[1] == self.updates:
+                # V(boards[t]) from the rollout; reference states are boards[1..T], so the rows shift
+                # by one and only V(boards[T]) (never a rollout input) takes a forward pass
+                v_all = torch.empty((T, n), dtype=torch.float32, device=self.device)
+                off = 1 if cfg.mode == "reference" else 0
+                v_all[0:T - off].copy_(rv[0][off:T])
+                if off:
+                    v_all[T - 1] = value(self.boards[T]).view(n)
+            elif need_values:
                 v_all = torch.empty((T, n), dtype=torch.float32, device=self.device)
                 for t0 in range(0, T, T if fused else cfg.update_chunk):
                     t1 = min(T, t0 + (T if fused else cfg.update_chunk))

@@ -171,6 +171,37 @@ __device__ __forceinline__ LaneOut step_lane_lines(Board &L, uint32_t &ob, const
     return r;
 }
 
+// k_step_n's random-policy step on a board ALREADY reoriented to the line form of this step's
+// action (d.x >> 30). `s_next` holds the caller's read-ahead of the next step's selector record,
+// taken from the line form of this action; boards this step resets are back in rows, so theirs is
+// re-read from the rows entry (offset a16n).
+template <bool AUTO_RESET, bool REWARD>
+__device__ __forceinline__ LaneOut step_lane_pre(Board &L, r48::Orient &s_next, uint32_t a16n, const r48::Orient *tab,
+                                                 Draw d, bool want_score)
+{
+    LaneOut r;
+    r.a = d.x >> 30;
+    const r48::StepOut o = r48::step_lines<REWARD, true>(L, r.a, d.y, (d.x & 0x3FFFFFFFu) < r48::kFourThresh30);
+    r.score = 0u;
+    if (want_score) {
+        asm volatile("" ::: "memory");
+        r.score = r48::tile_sum(L);
+    }
+    if (AUTO_RESET && __ballot(o.done) != 0) {
+        Board z;
+        r48::reset_board(z, d.y >> 28, (d.y & 0x0FFFFFFFu) < r48::kFourThresh28);   // rows
+        L = Board{r48::sel(o.done, z.w0, L.w0), r48::sel(o.done, z.w1, L.w1), r48::sel(o.done, z.w2, L.w2),
+                  r48::sel(o.done, z.w3, L.w3)};
+        const r48::Orient z0 = orient_at(tab, a16n);
+        s_next = r48::Orient{r48::sel(o.done, z0.x0, s_next.x0), r48::sel(o.done, z0.x1, s_next.x1),
+                             r48::sel(o.done, z0.te, s_next.te), r48::sel(o.done, z0.to, s_next.to)};
+    }
+    r.done = o.done;
+    r.changed = o.changed;
+    r.reward = o.reward;
+    return r;
+}
+
 template <bool RANDOM, bool REWARD>
 __device__ __forceinline__ void emit(const LaneOut &r, int64_t i, int8_t *boards, int8_t *actions, uint8_t *done,
                                      uint8_t *changed, int32_t *reward, int32_t *score)
@@ -285,7 +316,9 @@ __global__ __launch_bounds__(kBlock) void k_step(int8_t *boards, int64_t n, int6
 // TRAJ (r48_env_rollout): also every step's action and done into row t of traj_actions /
 // traj_done ([n_steps][n], each nullable) -- one 2-byte store per plane per pair and step.
 template <bool RANDOM, bool AUTO_RESET, bool REWARD, int NP, bool TRAJ = false>
-__global__ __launch_bounds__(kBlock) void k_step_n(int8_t *boards, int64_t n, int64_t gid0, uint32_t k0, uint32_t k1,
+// The read-ahead below needs ~62 VGPRs; waves_per_eu(8) holds the allocator to the 64 that keep the
+// 8 waves per SIMD the VALU issue bound needs.
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_step_n(int8_t *boards, int64_t n, int64_t gid0, uint32_t k0, uint32_t k1,
                                                    uint32_t step0, int32_t n_steps, int8_t *__restrict__ actions,
                                                    uint8_t *__restrict__ done, uint8_t *__restrict__ changed,
                                                    int32_t *__restrict__ reward, int32_t *__restrict__ score,
@@ -329,48 +362,89 @@ __global__ __launch_bounds__(kBlock) void k_step_n(int8_t *boards, int64_t n, in
         // last ones run with too few partners to fill the VALU. Dropping a wave's priority as it
         // passes 1/8, 3/8 and 3/4 of the call lets the laggards catch up at each boundary, so all
         // 8 stay to the end (boundaries measured on three boxes: profiles/r02/exp_stepn_priority*).
+        // The call runs as four phases at priority 3, 2, 1, 0, the boundaries at {1, 3, 6}/8 of the
+        // call: an outer loop over the phases around the step loop, so the priority change is one
+        // scalar branch per phase and no per-step counter compares.
         constexpr int kQ[3] = {1, 3, 6};   // priority boundaries in eighths of the call
-        const int32_t q1 = (n_steps * kQ[0]) >> 3, q2 = (n_steps * kQ[1]) >> 3, q3 = (n_steps * kQ[2]) >> 3;
-        constexpr bool kPrio = true;
-        if (kPrio)
-            __builtin_amdgcn_s_setprio(3);
-        for (int32_t t = 0; t < n_steps; t++) {
-            const uint32_t step = step0 + (uint32_t)t;
-            const bool sc = want_score && t == last;
-            if (kPrio && t == q1)
-                __builtin_amdgcn_s_setprio(2);
-            if (kPrio && t == q2)
-                __builtin_amdgcn_s_setprio(1);
-            if (kPrio && t == q3)
-                __builtin_amdgcn_s_setprio(0);
+        const int32_t ends[4] = {(n_steps * kQ[0]) >> 3, (n_steps * kQ[1]) >> 3, (n_steps * kQ[2]) >> 3, n_steps};
+        // Read-ahead (random policy): the draws depend on (pair, step) only, so step t + 1's Philox
+        // runs under step t's board chain -- two independent dependency chains per wave -- and
+        // step t + 1's selector record (last action -> next action, both known from the draws)
+        // is read from LDS while step t moves. Measured on the 2^20-board A/B
+        // (profiles/r03/stepn_readahead_ab.txt, with the phase loop below): K = 20 82.0 -> 81.3 us,
+        // K = 1000 3.597 -> 3.46 us per step; bit-identical boards.
+        Draw de[NP], dd[NP];
 #pragma unroll
-            for (int j = 0; j < NP; j++) {
-                Draw de, dd;
-                pair_draws(q[j], step, k0, k1, de, dd);
-                r[2 * j] = step_lane_lines<RANDOM, AUTO_RESET, REWARD>(b[2 * j], ob[2 * j], tab, a[2 * j], de, sc);
-                r[2 * j + 1] =
-                    step_lane_lines<RANDOM, AUTO_RESET, REWARD>(b[2 * j + 1], ob[2 * j + 1], tab, a[2 * j + 1], dd, sc);
-                if (TRAJ) {
-                    const int64_t at = (int64_t)t * n + base + 2 * kBlock * j;
-                    if (traj_bytes) {   // wave-uniform
-                        if (traj_actions) {
-                            traj_actions[at] = (int8_t)r[2 * j].a;
-                            traj_actions[at + 1] = (int8_t)r[2 * j + 1].a;
-                        }
-                        if (traj_done) {
-                            traj_done[at] = (uint8_t)r[2 * j].done;
-                            traj_done[at + 1] = (uint8_t)r[2 * j + 1].done;
-                        }
+        for (int j = 0; j < NP; j++)
+            pair_draws(q[j], step0, k0, k1, de[j], dd[j]);
+        r48::Orient se[NP], sd[NP];   // this step's selector records (from rows on entry)
+#pragma unroll
+        for (int j = 0; j < NP; j++) {
+            se[j] = orient_at(tab, (de[j].x >> 26) & 0x30u);
+            sd[j] = orient_at(tab, (dd[j].x >> 26) & 0x30u);
+        }
+        int32_t t = 0;
+#pragma nounroll
+        for (int ph = 0; ph < 4; ph++) {
+            switch (ph) {   // s_setprio takes an immediate
+            case 0: __builtin_amdgcn_s_setprio(3); break;
+            case 1: __builtin_amdgcn_s_setprio(2); break;
+            case 2: __builtin_amdgcn_s_setprio(1); break;
+            default: __builtin_amdgcn_s_setprio(0); break;
+            }
+            for (const int32_t end = ends[ph]; t < end; t++) {
+                const uint32_t step = step0 + (uint32_t)t;
+                const bool sc = want_score && t == last;
+#pragma unroll
+                for (int j = 0; j < NP; j++) {
+                    Draw ne, nd;
+                    pair_draws(q[j], step + 1u, k0, k1, ne, nd);
+                    if (RANDOM) {
+                        const uint32_t ane = (ne.x >> 26) & 0x30u, and_ = (nd.x >> 26) & 0x30u;
+                        // this step's reorient first, then the next step's selector reads into the
+                        // same registers: their LDS latency runs under this step's move
+                        r48::Orient xe = orient_at(tab, ((de[j].x >> 24) & 0xC0u) + ane);
+                        r48::Orient xd = orient_at(tab, ((dd[j].x >> 24) & 0xC0u) + and_);
+                        b[2 * j] = r48::reorient(b[2 * j], se[j]);
+                        b[2 * j + 1] = r48::reorient(b[2 * j + 1], sd[j]);
+                        r[2 * j] = step_lane_pre<AUTO_RESET, REWARD>(b[2 * j], xe, ane, tab, de[j], sc);
+                        r[2 * j + 1] = step_lane_pre<AUTO_RESET, REWARD>(b[2 * j + 1], xd, and_, tab, dd[j], sc);
+                        se[j] = xe;
+                        sd[j] = xd;
                     } else {
-                        if (traj_actions)
-                            *reinterpret_cast<uint16_t *>(traj_actions + at) =
-                                (uint16_t)(r[2 * j].a | (r[2 * j + 1].a << 8));
-                        if (traj_done)
-                            *reinterpret_cast<uint16_t *>(traj_done + at) =
-                                (uint16_t)(r[2 * j].done | (r[2 * j + 1].done << 8));
+                        r[2 * j] = step_lane_lines<RANDOM, AUTO_RESET, REWARD>(b[2 * j], ob[2 * j], tab, a[2 * j], de[j], sc);
+                        r[2 * j + 1] = step_lane_lines<RANDOM, AUTO_RESET, REWARD>(b[2 * j + 1], ob[2 * j + 1], tab,
+                                                                                   a[2 * j + 1], dd[j], sc);
+                    }
+                    de[j] = ne;
+                    dd[j] = nd;
+                    if (TRAJ) {
+                        const int64_t at = (int64_t)t * n + base + 2 * kBlock * j;
+                        if (traj_bytes) {   // wave-uniform
+                            if (traj_actions) {
+                                traj_actions[at] = (int8_t)r[2 * j].a;
+                                traj_actions[at + 1] = (int8_t)r[2 * j + 1].a;
+                            }
+                            if (traj_done) {
+                                traj_done[at] = (uint8_t)r[2 * j].done;
+                                traj_done[at + 1] = (uint8_t)r[2 * j + 1].done;
+                            }
+                        } else {
+                            if (traj_actions)
+                                *reinterpret_cast<uint16_t *>(traj_actions + at) =
+                                    (uint16_t)(r[2 * j].a | (r[2 * j + 1].a << 8));
+                            if (traj_done)
+                                *reinterpret_cast<uint16_t *>(traj_done + at) =
+                                    (uint16_t)(r[2 * j].done | (r[2 * j + 1].done << 8));
+                        }
                     }
                 }
             }
+        }
+        if (RANDOM) {   // the line form of the last action, or rows after a reset in the last step
+#pragma unroll
+            for (int j = 0; j < 2 * NP; j++)
+                ob[j] = r[j].done ? 0u : r[j].a << 6;
         }
 #pragma unroll
         for (int j = 0; j < NP; j++) {

@@ -224,7 +224,8 @@ __global__ __launch_bounds__(kThreads, kOccRoll) void k_cnn_rollout(int8_t *__re
                                                              const float *__restrict__ bias,
                                                              int8_t *__restrict__ traj, int8_t *__restrict__ actions,
                                                              uint8_t *__restrict__ done, int32_t *__restrict__ reward,
-                                                             int32_t *__restrict__ lengths, int64_t gid0, uint32_t pk0,
+                                                             int32_t *__restrict__ lengths, float *__restrict__ values,
+                                                             int64_t gid0, uint32_t pk0,
                                                              uint32_t pk1, uint32_t ctr0, uint32_t ek0, uint32_t ek1,
                                                              uint32_t step0)
 {
@@ -264,6 +265,14 @@ __global__ __launch_bounds__(kThreads, kOccRoll) void k_cnn_rollout(int8_t *__re
                 *reinterpret_cast<uint2 *>(traj + 16 * (row0 + bB) + 8 * h) = rawB;
             const f32x16 oA = policy_out<MODE>(w_lds, b_lds, lane, h, rawA);
             const f32x16 oB = policy_out<MODE>(w_lds, b_lds, lane, h, rawB);
+            // V(pre-step board): the value head sits in register 0 of lane half 1 (as in
+            // k_cnn_forward, same bias add), so the reference loss needs no separate value pass
+            if (values && h == 1) {
+                if (liveA)
+                    values[row0 + bA] = oA[0] + b_lds[100];
+                if (liveB)
+                    values[row0 + bB] = oB[0] + b_lds[100];
+            }
             // one draw pass for both tiles: half 0 samples A's board col, half 1 B's (whose logits
             // sit in half 0 of oB) -- the lane's action is the one its env step below needs
             float z[4];
@@ -355,7 +364,7 @@ int r48_cnn_policy_forward(const int8_t *boards, int64_t n, const void *wfrag, c
 
 int r48_cnn_rollout(int8_t *boards, int64_t n, int32_t n_steps, const void *wfrag, const float *bias, int32_t mode,
                     int8_t *traj_boards, int8_t *actions, uint8_t *done, int32_t *reward, int32_t *lengths,
-                    uint64_t policy_seed, int64_t gid0, uint32_t sample_ctr, uint64_t env_seed, uint32_t env_step,
+                    float *values, uint64_t policy_seed, int64_t gid0, uint32_t sample_ctr, uint64_t env_seed, uint32_t env_step,
                     uint32_t flags, void *stream)
 {
     if (!boards || !wfrag || !bias || !traj_boards || !actions || !done || n < 0 || gid0 < 0 || n_steps < 1 ||
@@ -376,7 +385,7 @@ int r48_cnn_rollout(int8_t *boards, int64_t n, int32_t n_steps, const void *wfra
                                         : (rw ? k_cnn_rollout<R48_FEAT_EXPONENTS, true>
                                               : k_cnn_rollout<R48_FEAT_EXPONENTS, false>);
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kThreads), 0, (hipStream_t)stream, boards, n, n_steps,
-                       (const uint4 *)wfrag, bias, traj_boards, actions, done, reward, lengths, gid0, (uint32_t)policy_seed,
+                       (const uint4 *)wfrag, bias, traj_boards, actions, done, reward, lengths, values, gid0, (uint32_t)policy_seed,
                        (uint32_t)(policy_seed >> 32), sample_ctr, (uint32_t)env_seed, (uint32_t)(env_seed >> 32),
                        env_step);
     const hipError_t e = hipGetLastError();

@@ -353,6 +353,32 @@ def test_rollout_megakernel_equals_per_step_rollout(mode, n_boards):
             assert a == b
 
 
+@pytest.mark.parametrize("n_boards", [5003, 65])
+def test_rollout_values_replace_the_value_pass(n_boards):
+    """The megakernel's value output (reference loss, a3c.py:218-223) equals the separate
+    r48_cnn_policy_forward value pass over the trajectory boards bit for bit, and an update that
+    reads it leaves the same parameters and losses as one that runs the value pass."""
+    from rein48_amd.a3c import A3CConfig, A3CTrainer
+    from rein48_amd.a3c.fused import cnn_forward, pack_cnn
+    res = []
+    for rv in (True, False):
+        cfg = A3CConfig(n_boards=n_boards, max_steps=23, mode="reference", net="cnn", bf16=True, features="values",
+                        seed=5, rollout_values=rv)
+        tr = A3CTrainer(cfg, device=DEV)
+        tr.rollout()
+        if rv:
+            wfrag, bias = pack_cnn(tr.net)
+            T = cfg.max_steps
+            v = cnn_forward(tr.boards[0:T].reshape(-1, 16).contiguous(), wfrag, bias, exponents=False,
+                            logits=False, value=True)[1].view(T, n_boards)
+            assert torch.equal(tr._rollout_v[0], v)
+        losses = tr.update()
+        torch.cuda.synchronize()
+        res.append((losses["actor_loss"], losses["critic_loss"], tr.flat.data.clone()))
+    assert res[0][0] == res[1][0] and res[0][1] == res[1][1]
+    assert torch.equal(res[0][2], res[1][2])
+
+
 def test_segment_stats_and_row_weights_match_tensor_forms():
     """r48_a3c_segment_stats / r48_a3c_row_weights (the fused update's per-segment constants and
     per-row weights) vs losses.segment_stats and the tensor formulas they replace, on ragged segment
