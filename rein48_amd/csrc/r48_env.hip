@@ -363,10 +363,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         // passes 1/8, 3/8 and 3/4 of the call lets the laggards catch up at each boundary, so all
         // 8 stay to the end (boundaries measured on three boxes: profiles/r02/exp_stepn_priority*).
         // The call runs as four phases at priority 3, 2, 1, 0, the boundaries at {1, 3, 6}/8 of the
-        // call: an outer loop over the phases around the step loop, so the priority change is one
-        // scalar branch per phase and no per-step counter compares.
-        constexpr int kQ[3] = {1, 3, 6};   // priority boundaries in eighths of the call
-        const int32_t ends[4] = {(n_steps * kQ[0]) >> 3, (n_steps * kQ[1]) >> 3, (n_steps * kQ[2]) >> 3, n_steps};
+        // call ({1, 3, 5}/8 for calls of at most 64 steps, where the last phase needs the longer
+        // run-in): an outer loop over the phases around the step loop, so the priority change is
+        // one scalar branch per phase and no per-step counter compares. Boundary sweeps at 2^20
+        // boards (profiles/r03/stepn_priority_sweep_r03.txt): K = 20 81.3 -> 80.2 us with the last
+        // boundary at 5/8, K = 1000 best at 6/8 (3.47 vs 3.50 us per step).
+        const int32_t q3 = n_steps <= 64 ? 5 : 6;
+        const int32_t ends[4] = {n_steps >> 3, (n_steps * 3) >> 3, (n_steps * q3) >> 3, n_steps};
         // Read-ahead (random policy): the draws depend on (pair, step) only, so step t + 1's Philox
         // runs under step t's board chain -- two independent dependency chains per wave -- and
         // step t + 1's selector record (last action -> next action, both known from the draws)
