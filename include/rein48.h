@@ -125,6 +125,19 @@ int r48_env_move(r48_env *env, const int8_t *actions, uint32_t flags, uint8_t *c
 int r48_env_spawn(r48_env *env, const uint8_t *mask, const uint8_t *rank, const uint8_t *four,
                   uint8_t *done, void *stream);
 
+/* Game.step of ONE board (the drop-in Game, GameClient.py:40-51) in one launch and one result
+ * read: board = 16 exponent cells (host memory, copied into the kernel arguments), action 0..3.
+ * One wave moves the board and, for every blank rank r (row-major, GameClient.py:109-114) and
+ * tile (f = 0: 2, f = 1: 4), spawns it and evaluates has_game_over (:74-93), so the caller draws
+ * the spawn with its own RNG (randint over the blank count, :121; uniform > 0.1, :125) after the
+ * launch and picks candidate 2r + f. out (device memory, 16-byte aligned,
+ * r48_game_step1_out_bytes() bytes): int8 [32][16] candidate boards; uint8 [512] changed (when 0
+ * every candidate is the unchanged board, no spawn); uint8 [513] blank count after the move;
+ * uint32 [516] game-over mask, bit 2r + f for candidate 2r + f. Replaces r48_env_move +
+ * r48_env_spawn (two launches and two host round trips) for the single-board drop-in. */
+int r48_game_step1(const int8_t *board, int32_t action, uint8_t *out, void *stream);
+int r48_game_step1_out_bytes(void);
+
 /* Random-policy rollout (README.md:19 "random-policy data generation on GPU"; the
  * main.py:36-42 loop batched): n_steps Philox-mode steps with R48_RANDOM_POLICY |
  * R48_AUTO_RESET, boards held in registers across steps. Per step t it writes

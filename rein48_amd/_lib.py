@@ -87,6 +87,8 @@ SIGNATURES = {
     "r48_env_score": (C.c_int, [_P, _P, _P]),
     "r48_env_error_count": (C.c_int, [_P, C.POINTER(_I64), _P]),
     "r48_env_clear_errors": (C.c_int, [_P, _P]),
+    "r48_game_step1": (C.c_int, [_P, _I32, _P, _P]),
+    "r48_game_step1_out_bytes": (C.c_int, []),
     "r48_values_move": (C.c_int, [_P, _P, _I64, _P, _P, _P]),
     "r48_values_check": (C.c_int, [_P, _I64, _I32, _I32, _P, _P, _P]),
     "r48_values_move_grid": (C.c_int, [_P, _I64, _I32, _I32, _P, _P, _P]),

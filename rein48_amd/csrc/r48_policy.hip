@@ -289,7 +289,7 @@ __global__ __launch_bounds__(kThreads, kOccRoll) void k_cnn_rollout(int8_t *__re
             uint32_t dx, dy;
             r48::step_draw(gE, step0 + (uint32_t)t, ek0, ek1, dx, dy);
             const r48::StepOut o =
-                r48::step_board<REWARD, false, false>(bd, act, dy, (dx & 0x3FFFFFFFu) < r48::kFourThresh30);
+                r48::step_board<REWARD, false, true>(bd, act, dy, (dx & 0x3FFFFFFFu) < r48::kFourThresh30);
             // return the halves: half 0 keeps A's rows 0-1, half 1 keeps B's rows 2-3, and each sends
             // the other half of its board to its partner
             const uint2 back = h == 0 ? make_uint2(bd.w2, bd.w3) : make_uint2(bd.w0, bd.w1);

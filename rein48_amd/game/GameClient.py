@@ -11,8 +11,9 @@ Actions: "UP"/"Up"/"U"/"up"/"u"/0, ... /3 matched by equality like the reference
 (:140, :182, :206, :230), so True means DOWN and 2.0 means LEFT; anything else raises
 ValueError (:254).
 
-Compute runs on the GPU through librein48.so: a Game owns a one-board VecGame and each step
-is the move kernel (update_matrix) + the spawn/game-over kernel. The spawn DRAWS are taken
+Compute runs on the GPU through librein48.so: each 4x4 step is ONE r48_game_step1 launch that
+moves the board and evaluates every spawn outcome (blank rank x tile) with its game over, then
+the host's draw picks one. The spawn DRAWS are taken
 from Python's global `random` exactly as the reference takes them (randint over the
 row-major blank list, then uniform(0,1) > 0.1 -> 2 else 4, GameClient.py:121-125), so
 `random.seed(s)` gives the reference's trajectory bit for bit. The batched VecGame draws
@@ -28,9 +29,9 @@ drawn from the global `random` on the host, so it follows the reference's trajec
 import copy
 import random
 
+import numpy as np
 import torch
 
-from ..env import VecGame
 from .. import _lib
 from .._lib import check, ptr
 
@@ -119,18 +120,20 @@ class Game:
         self.action_space_size = 4
         self.state_space_size = 4 if table_matrix_size < 4 else table_matrix_size
         dev = _device()
-        # 4x4: the exponent env kernels on a one-board env whose board is byte 0..15 of a 32-byte
-        # device scratch ([16] action, [17] rank, [18] four, [19] spawn mask, [20] changed,
-        # [21] blanks after the move, [22] done), staged through one pinned host buffer: a step
-        # is 2 kernels, 3 small copies in, 2 out, 2 stream synchronisations. Larger boards: the
-        # value-domain grid kernels.
-        self._vec = VecGame(1, device=dev) if self.state_space_size == 4 else None
-        if self._vec is not None:
-            self._d = torch.zeros(32, dtype=torch.int8, device=dev)
-            self._h = torch.zeros(32, dtype=torch.int8).pin_memory()
+        # 4x4: one r48_game_step1 launch per step (the move and every spawn outcome with its game
+        # over, k_game_step1), the board passed in the kernel arguments, one 520-byte result copied
+        # into a pinned host buffer: one launch, one copy, one stream synchronisation. The spawn
+        # draw stays on the global `random` (GameClient.py:121,125) and picks a candidate.
+        # Larger boards: the value-domain grid kernels.
+        self._small = self.state_space_size == 4
+        if self._small:
+            self._lib = _lib.load()
+            nb = int(self._lib.r48_game_step1_out_bytes())
+            self._dev = torch.device(dev)
+            self._d = torch.empty(nb, dtype=torch.uint8, device=dev)
+            self._h = torch.empty(nb, dtype=torch.uint8).pin_memory()
             self._hn = self._h.numpy()
-            check(self._vec._lib.r48_env_bind_boards(self._vec._env, ptr(self._d)))
-            self._vec.boards = self._d[:16].view(1, 16)
+            self._b = np.zeros(16, dtype=np.int8)
         self.reset()
 
     # ---------------------------------------------------------------- public (GameClient.py:33-51)
@@ -143,35 +146,29 @@ class Game:
 
     def step(self, action):
         code = action_code(action)
-        exps = [_exponent(v) for row in self.state_matrix for v in row] if self._vec is not None else [None]
+        exps = [_exponent(v) for row in self.state_matrix for v in row] if self._small else [None]
         if any(e is None for e in exps):
             # tiles outside 2^e: the value-domain kernels, composed like GameClient.py:45-51
             self.state_matrix, reward, changed = self.update_matrix(self.state_matrix, code)
             if changed:
                 self.state_matrix = Game.random_fill_grid(self.state_matrix)
             return self.state_matrix, reward, Game.has_game_over(self.state_matrix)
-        vec, d, h, hn = self._vec, self._d, self._h, self._hn
-        lib, st = vec._lib, torch.cuda.current_stream(vec.device)
-        base = d.data_ptr()
-        hn[:16] = exps
-        hn[16] = code
-        d[:17].copy_(h[:17], non_blocking=True)
-        check(lib.r48_env_move(vec._env, base + 16, 0, base + 20, base + 21, None, st.cuda_stream))
-        h[20:22].copy_(d[20:22], non_blocking=True)
+        b, hn = self._b, self._hn
+        b[:] = exps
+        st = torch.cuda.current_stream(self._dev)
+        check(self._lib.r48_game_step1(b.ctypes.data, code, self._d.data_ptr(), st.cuda_stream))
+        self._h.copy_(self._d, non_blocking=True)
         st.synchronize()
-        changed, n_blank = int(hn[20]), int(hn[21])
-        if changed:
-            hn[17] = random.randint(0, n_blank - 1)                 # GameClient.py:121
-            hn[18] = 0 if random.uniform(0, 1) > 0.1 else 1         # GameClient.py:125
-        hn[19] = changed                                           # unchanged: no spawn, only game over
-        d[17:20].copy_(h[17:20], non_blocking=True)
-        check(lib.r48_env_spawn(vec._env, base + 19, base + 17, base + 18, base + 22, st.cuda_stream))
-        h[:23].copy_(d[:23], non_blocking=True)
-        st.synchronize()
+        c = 0                                                      # unchanged: no spawn (GameClient.py:49)
+        if hn[512]:
+            r = random.randint(0, int(hn[513]) - 1)                # GameClient.py:121
+            c = 2 * r + (0 if random.uniform(0, 1) > 0.1 else 1)  # GameClient.py:125
+        over = (int(hn[516]) | int(hn[517]) << 8 | int(hn[518]) << 16 | int(hn[519]) << 24) >> c & 1
+        cand = hn[16 * c:16 * c + 16]
         for k in range(16):  # write back into the SAME lists (aliasing, GameClient.py:45)
-            e = int(hn[k])
+            e = int(cand[k])
             self.state_matrix[k // 4][k % 4] = (1 << e) if e else 0
-        return self.state_matrix, 0, bool(hn[22])
+        return self.state_matrix, 0, bool(over)
 
     # ---------------------------------------------------------------- static helpers (:55-269)
     @staticmethod

@@ -167,6 +167,41 @@ def to_exp_list(m):
     return [0 if v == 0 else int(v).bit_length() - 1 for r in m for v in r]
 
 
+def test_game_step1_candidates_equal_injected_draw_steps():
+    """r48_game_step1 (the drop-in Game.step's one launch): candidate 2r + f equals the injected-draw
+    step (rank r, tile 2 or 4) of the same board, and its game-over bit equals that step's done, for
+    every blank rank, on random boards incl. full ones (unchanged moves: every candidate is the
+    unchanged board) and every action."""
+    from rein48_amd import _lib
+    lib = _lib.load()
+    rng = np.random.default_rng(11)
+    boards = np.concatenate([rand_boards(rng, 60), rand_boards(rng, 20, emax=3, p_empty=0.0),
+                             rand_boards(rng, 20, p_empty=0.85)])
+    nb = int(lib.r48_game_step1_out_bytes())
+    out = torch.empty(nb, dtype=torch.uint8, device=DEV)
+    env = vec(32)
+    ranks = torch.arange(32, device=DEV, dtype=torch.int32).div(2, rounding_mode="floor").to(torch.uint8)
+    fours = (torch.arange(32, device=DEV) % 2).to(torch.uint8)
+    for i, b in enumerate(boards):
+        for a in range(4):
+            bb = np.ascontiguousarray(b)
+            _lib.check(lib.r48_game_step1(bb.ctypes.data, a, out.data_ptr(), torch.cuda.current_stream().cuda_stream))
+            h = out.cpu().numpy()
+            changed, n_blank = int(h[512]), int(h[513])
+            mask = int.from_bytes(h[516:520].tobytes(), "little")
+            env.boards.copy_(torch.from_numpy(np.repeat(b[None], 32, 0)))
+            _, _, done = env.step_with_draws(torch.full((32,), a, dtype=torch.int8, device=DEV), ranks, fours)
+            ref = env.boards.cpu().numpy()
+            assert changed == int(env.changed[0])
+            for c in range(32):
+                if changed and (c >> 1) >= n_blank:
+                    continue
+                assert np.array_equal(h[16 * c:16 * c + 16].view(np.int8), ref[c]), (i, a, c)
+                assert (mask >> c & 1) == int(done[c]), (i, a, c)
+            if changed:
+                assert n_blank == int((ref[0] == 0).sum()) + 1
+
+
 def test_drop_in_game_surface():
     from rein48_amd.game import Game
     g = Game()
