@@ -138,6 +138,12 @@ int r48_env_spawn(r48_env *env, const uint8_t *mask, const uint8_t *rank, const 
 int r48_game_step1(const int8_t *board, int32_t action, uint8_t *out, void *stream);
 int r48_game_step1_out_bytes(void);
 
+/* Pinned, device-mapped, coherent host memory (hipHostMalloc) for small results a kernel writes
+ * straight to the host (the drop-in Game's r48_game_step1 `out`): returns the host pointer and
+ * stores the device-side pointer in *device_ptr; NULL on failure. r48_host_free releases it. */
+void *r48_host_alloc(int64_t bytes, void **device_ptr);
+int r48_host_free(void *host_ptr);
+
 /* Random-policy rollout (README.md:19 "random-policy data generation on GPU"; the
  * main.py:36-42 loop batched): n_steps Philox-mode steps with R48_RANDOM_POLICY |
  * R48_AUTO_RESET, boards held in registers across steps. Per step t it writes

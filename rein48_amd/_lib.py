@@ -89,6 +89,8 @@ SIGNATURES = {
     "r48_env_clear_errors": (C.c_int, [_P, _P]),
     "r48_game_step1": (C.c_int, [_P, _I32, _P, _P]),
     "r48_game_step1_out_bytes": (C.c_int, []),
+    "r48_host_alloc": (C.c_void_p, [_I64, C.POINTER(C.c_void_p)]),
+    "r48_host_free": (C.c_int, [_P]),
     "r48_values_move": (C.c_int, [_P, _P, _I64, _P, _P, _P]),
     "r48_values_check": (C.c_int, [_P, _I64, _I32, _I32, _P, _P, _P]),
     "r48_values_move_grid": (C.c_int, [_P, _I64, _I32, _I32, _P, _P, _P]),

@@ -71,4 +71,25 @@ int r48_game_step1(const int8_t *board, int32_t action, uint8_t *out, void *stre
 
 int r48_game_step1_out_bytes(void) { return kStep1Out; }
 
+void *r48_host_alloc(int64_t bytes, void **device_ptr)
+{
+    void *h = nullptr;
+    if (bytes <= 0 || !device_ptr)
+        return nullptr;
+    if (hipHostMalloc(&h, (size_t)bytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+        return nullptr;
+    if (hipHostGetDevicePointer(device_ptr, h, 0) != hipSuccess) {
+        (void)hipHostFree(h);
+        return nullptr;
+    }
+    return h;
+}
+
+int r48_host_free(void *host_ptr)
+{
+    if (host_ptr && hipHostFree(host_ptr) != hipSuccess)
+        return fail(R48_EHIP, "hipHostFree failed");
+    return R48_OK;
+}
+
 }  // extern "C"

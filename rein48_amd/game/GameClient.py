@@ -27,7 +27,9 @@ drawn from the global `random` on the host, so it follows the reference's trajec
 (the reference's own tests use 4x1 / 1x4 matrices and the value 1).
 """
 import copy
+import ctypes
 import random
+import weakref
 
 import numpy as np
 import torch
@@ -121,18 +123,24 @@ class Game:
         self.state_space_size = 4 if table_matrix_size < 4 else table_matrix_size
         dev = _device()
         # 4x4: one r48_game_step1 launch per step (the move and every spawn outcome with its game
-        # over, k_game_step1), the board passed in the kernel arguments, one 520-byte result copied
-        # into a pinned host buffer: one launch, one copy, one stream synchronisation. The spawn
-        # draw stays on the global `random` (GameClient.py:121,125) and picks a candidate.
-        # Larger boards: the value-domain grid kernels.
+        # over, k_game_step1), the board passed in the kernel arguments and the 520-byte result
+        # written by the kernel straight into mapped, coherent host memory (r48_host_alloc): one
+        # launch and one stream synchronisation per step. The spawn draw stays on the global
+        # `random` (GameClient.py:121,125) and picks a candidate. Larger boards: the value-domain
+        # grid kernels.
         self._small = self.state_space_size == 4
         if self._small:
-            self._lib = _lib.load()
-            nb = int(self._lib.r48_game_step1_out_bytes())
+            lib = self._lib = _lib.load()
+            nb = int(lib.r48_game_step1_out_bytes())
             self._dev = torch.device(dev)
-            self._d = torch.empty(nb, dtype=torch.uint8, device=dev)
-            self._h = torch.empty(nb, dtype=torch.uint8).pin_memory()
-            self._hn = self._h.numpy()
+            dp = ctypes.c_void_p()
+            with torch.cuda.device(self._dev):
+                hp = lib.r48_host_alloc(nb, ctypes.byref(dp))
+            if not hp:
+                raise RuntimeError("r48_host_alloc failed: %s" % lib.r48_last_error().decode())
+            weakref.finalize(self, lib.r48_host_free, hp)
+            self._out = dp.value
+            self._hn = np.ctypeslib.as_array((ctypes.c_uint8 * nb).from_address(hp))
             self._b = np.zeros(16, dtype=np.int8)
         self.reset()
 
@@ -156,8 +164,7 @@ class Game:
         b, hn = self._b, self._hn
         b[:] = exps
         st = torch.cuda.current_stream(self._dev)
-        check(self._lib.r48_game_step1(b.ctypes.data, code, self._d.data_ptr(), st.cuda_stream))
-        self._h.copy_(self._d, non_blocking=True)
+        check(self._lib.r48_game_step1(b.ctypes.data, code, self._out, st.cuda_stream))
         st.synchronize()
         c = 0                                                      # unchanged: no spawn (GameClient.py:49)
         if hn[512]:
