@@ -245,14 +245,15 @@ int r48_cnn_policy_forward(const int8_t *boards, int64_t n, const void *wfrag, c
  * auto-reset; R48_MERGE_REWARD in flags for the merge reward). boards int8[n][16] (16-byte
  * aligned) are read at the start and hold the final boards at the end; traj_boards
  * int8[n_steps + 1][n][16] receives the pre-step board of every step and the final board;
- * actions int8[n_steps][n], done uint8[n_steps][n], reward int32[n_steps][n] (nullable), lengths
+ * actions int8[n_steps][n], done uint8[n_steps][n], reward float[n_steps][n] (nullable; the merge
+ * reward as fp32, exact below 2^24, 0 without R48_MERGE_REWARD), lengths
  * int32[n] (nullable): 1 + the first step that ended done, else n_steps (a3c.py:201); values
  * float[n_steps][n] (nullable): the critic value of every pre-step board, as r48_cnn_policy_forward's
  * `value` output (the reference loss's value pass, a3c.py:218-223, read from the rollout). Results
  * equal n_steps x (r48_cnn_policy_forward + r48_env_step) bit for bit; the caller advances the
  * env's step counter by n_steps (r48_env_set_counters). */
 int r48_cnn_rollout(int8_t *boards, int64_t n, int32_t n_steps, const void *wfrag, const float *bias, int32_t mode,
-                    int8_t *traj_boards, int8_t *actions, uint8_t *done, int32_t *reward, int32_t *lengths,
+                    int8_t *traj_boards, int8_t *actions, uint8_t *done, float *reward, int32_t *lengths,
                     float *values, uint64_t policy_seed, int64_t gid0, uint32_t sample_ctr, uint64_t env_seed, uint32_t env_step,
                     uint32_t flags, void *stream);
 

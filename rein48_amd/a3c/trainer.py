@@ -97,9 +97,10 @@ class A3CTrainer:
         fused = cfg.net == "cnn" and cfg.bf16 and cfg.fused_policy
         if fused:
             wfrag, bias = pack_cnn(self.net)   # weights are fixed for the whole rollout
-        if merge and getattr(self, "_rewards_i32", None) is None:
+        mega = fused and cfg.fused_rollout
+        if merge and not mega and getattr(self, "_rewards_i32", None) is None:
             self._rewards_i32 = torch.zeros((cfg.max_steps, cfg.n_boards), dtype=torch.int32, device=self.device)
-        if fused and cfg.fused_rollout:   # every step of every board in one persistent kernel
+        if mega:   # every step of every board in one persistent kernel (writes fp32 rewards itself)
             self._rollout_megakernel(wfrag, bias, merge)
         elif fused:   # per step: board -> CNN -> softmax -> Philox draw in one kernel, then the env kernel
             self._rollout_fused(wfrag, bias, merge)
@@ -113,7 +114,7 @@ class A3CTrainer:
                 # done (and the merge reward) land in the trajectory rows directly
                 env.step(act, merge_reward=merge, done_out=self.done[t],
                          reward_out=self._rewards_i32[t] if merge else None)
-        if merge:
+        if merge and not mega:
             self.rewards.copy_(self._rewards_i32)     # one int32 -> fp32 pass for the whole rollout
         # segment length: through the first done step, else max_steps (a3c.py:201)
         if fused and cfg.fused_rollout:                # the megakernel wrote boards[T] and the lengths
@@ -125,9 +126,15 @@ class A3CTrainer:
             notdone = (self.done.cumsum(0) == 0)
             self.lengths = (notdone.sum(0) + 1).clamp(max=cfg.max_steps).to(torch.int32)
             self.finished = self.done.bool().any(0)
-        t = torch.arange(cfg.max_steps, device=self.device).unsqueeze(1)
-        self.mask = t < self.lengths.unsqueeze(0)
-        return self.lengths
+        self._mask = None              # [T, n] valid-step mask, formed on first use (the fused update
+        return self.lengths            # reads the lengths instead)
+
+    @property
+    def mask(self):
+        if self._mask is None:
+            t = torch.arange(self.cfg.max_steps, device=self.device).unsqueeze(1)
+            self._mask = t < self.lengths.unsqueeze(0)
+        return self._mask
 
     def _rollout_fused(self, wfrag, bias, merge):
         """The fused rollout's T steps as two raw C-ABI calls each: r48_cnn_policy_forward (CNN,
@@ -174,7 +181,7 @@ class A3CTrainer:
             env.boards.data_ptr(), n, T, wfrag.data_ptr(), bias.data_ptr(),
             _lib.FEAT_EXPONENTS if cfg.features == "exponents" else _lib.FEAT_VALUES,
             self.boards.data_ptr(), self.actions.data_ptr(), self.done.data_ptr(),
-            self._rewards_i32.data_ptr() if merge else None, self._lengths.data_ptr(),
+            self.rewards.data_ptr() if merge else None, self._lengths.data_ptr(),
             None if values is None else values.data_ptr(), int(cfg.seed) & (2 ** 64 - 1), self.gid0,
             self.sample_ctr & 0xFFFFFFFF, int(env.seed) & (2 ** 64 - 1), step0,
             _lib.MERGE_REWARD if merge else 0, torch.cuda.current_stream(self.device).cuda_stream))

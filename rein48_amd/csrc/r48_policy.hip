@@ -223,7 +223,7 @@ __global__ __launch_bounds__(kThreads, kOccRoll) void k_cnn_rollout(int8_t *__re
                                                              const uint4 *__restrict__ wfrag,
                                                              const float *__restrict__ bias,
                                                              int8_t *__restrict__ traj, int8_t *__restrict__ actions,
-                                                             uint8_t *__restrict__ done, int32_t *__restrict__ reward,
+                                                             uint8_t *__restrict__ done, float *__restrict__ reward,
                                                              int32_t *__restrict__ lengths, float *__restrict__ values,
                                                              int64_t gid0, uint32_t pk0,
                                                              uint32_t pk1, uint32_t ctr0, uint32_t ek0, uint32_t ek1,
@@ -306,8 +306,8 @@ __global__ __launch_bounds__(kThreads, kOccRoll) void k_cnn_rollout(int8_t *__re
             if (liveE) {
                 actions[row0 + bE] = (int8_t)act;
                 done[row0 + bE] = (uint8_t)o.done;
-                if (reward)
-                    reward[row0 + bE] = REWARD ? (int32_t)o.reward : 0;
+                if (reward)   // merge reward as fp32 (exact: < 2^24), the update's input as is
+                    reward[row0 + bE] = REWARD ? (float)o.reward : 0.0f;
             }
         }
         const int64_t rowT = (int64_t)T * n;
@@ -363,7 +363,7 @@ int r48_cnn_policy_forward(const int8_t *boards, int64_t n, const void *wfrag, c
 }
 
 int r48_cnn_rollout(int8_t *boards, int64_t n, int32_t n_steps, const void *wfrag, const float *bias, int32_t mode,
-                    int8_t *traj_boards, int8_t *actions, uint8_t *done, int32_t *reward, int32_t *lengths,
+                    int8_t *traj_boards, int8_t *actions, uint8_t *done, float *reward, int32_t *lengths,
                     float *values, uint64_t policy_seed, int64_t gid0, uint32_t sample_ctr, uint64_t env_seed, uint32_t env_step,
                     uint32_t flags, void *stream)
 {
