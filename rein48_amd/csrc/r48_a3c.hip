@@ -146,6 +146,50 @@ __global__ __launch_bounds__(kBlock) void k_returns(const float *__restrict__ re
     }
 }
 
+// k_returns for n % 4 == 0 and 16-byte aligned slabs: a lane owns 4 consecutive boards and walks
+// every row t = T-1..0 with one 16-byte load and store (a wave moves 1 KiB per row, no divergence
+// on the per-board lengths); per board the same values and the same arithmetic as k_returns.
+template <bool DROP_LAST>
+__global__ __launch_bounds__(kBlock) void k_returns4(const float4 *__restrict__ rewards, const int4 *__restrict__ len,
+                                                     const float4 *__restrict__ bootstrap, int32_t T, int64_t n4,
+                                                     float gamma, float4 *__restrict__ out)
+{
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n4)
+        return;
+    const int4 l4 = len[i];
+    const int32_t L[4] = {min(max(l4.x, 0), T), min(max(l4.y, 0), T), min(max(l4.z, 0), T), min(max(l4.w, 0), T)};
+    const float4 b4 = bootstrap[i];
+    float g[4] = {b4.x, b4.y, b4.z, b4.w};
+    constexpr int kAhead = 4;
+    for (int32_t t0 = T - 1; t0 >= 0; t0 -= kAhead) {
+        float4 r[kAhead];
+#pragma unroll
+        for (int k = 0; k < kAhead; k++)
+            r[k] = t0 - k >= 0 ? rewards[(int64_t)(t0 - k) * n4 + i] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int k = 0; k < kAhead; k++) {
+            const int32_t t = t0 - k;
+            if (t < 0)
+                break;
+            const float rr[4] = {r[k].x, r[k].y, r[k].z, r[k].w};
+            float o[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                if (t >= L[j]) {
+                    o[j] = 0.0f;
+                } else if (DROP_LAST && t == L[j] - 1) {
+                    o[j] = g[j];
+                } else {
+                    g[j] = rr[j] + gamma * g[j];
+                    o[j] = g[j];
+                }
+            }
+            out[(int64_t)t * n4 + i] = make_float4(o[0], o[1], o[2], o[3]);
+        }
+    }
+}
+
 // tf.train.RMSPropOptimizer (TF1) ApplyRMSProp over one flat parameter buffer:
 //   ms  <- decay*ms + (1-decay)*g^2          (ms slot initialised to ONES by the caller)
 //   mom <- momentum*mom + lr*g/sqrt(ms + eps)
@@ -240,11 +284,12 @@ __global__ __launch_bounds__(kBlock) void k_row_weights(const int32_t *__restric
                                                         const float *__restrict__ td_sum, int32_t T, int64_t n,
                                                         float *__restrict__ wn, float *__restrict__ cm)
 {
-    const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (r >= (int64_t)T * n)
+    // grid (ceil(n / kBlock), T): row t = blockIdx.y, no 64-bit division per element
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n)
         return;
-    const int64_t i = r % n;
-    const int32_t t = (int32_t)(r / n);
+    const int32_t t = (int32_t)blockIdx.y;
+    const int64_t r = (int64_t)t * n + i;
     const float m = t < len[i] ? 1.0f : 0.0f, inv_n = 1.0f / (float)n, b = B[i];
     wn[r] = (m / b) * inv_n;
     if (cm)
@@ -312,7 +357,12 @@ int r48_discounted_returns(const float *rewards, const int32_t *lengths, const f
         return fail(R48_EINVAL, "NULL argument, T < 1 or n < 0");
     if (n == 0)
         return R48_OK;
-    if (drop_last)
+    if ((n & 3) == 0 && ((reinterpret_cast<uintptr_t>(rewards) | reinterpret_cast<uintptr_t>(lengths) |
+                          reinterpret_cast<uintptr_t>(bootstrap) | reinterpret_cast<uintptr_t>(out)) & 15u) == 0) {
+        auto k4 = drop_last ? k_returns4<true> : k_returns4<false>;
+        hipLaunchKernelGGL(k4, grid_for(n / 4), dim3(kBlock), 0, (hipStream_t)stream, (const float4 *)rewards,
+                           (const int4 *)lengths, (const float4 *)bootstrap, T, n / 4, gamma, (float4 *)out);
+    } else if (drop_last)
         hipLaunchKernelGGL(k_returns<true>, grid_for(n), dim3(kBlock), 0, (hipStream_t)stream, rewards, lengths,
                            bootstrap, T, n, gamma, out);
     else
@@ -347,7 +397,10 @@ int r48_a3c_row_weights(const int32_t *lengths, const float *B, const float *td_
         return fail(R48_EINVAL, "r48_a3c_row_weights: NULL argument (td_sum needed with cm), T < 1 or n < 0");
     if (n == 0)
         return R48_OK;
-    hipLaunchKernelGGL(k_row_weights, grid_for((int64_t)T * n), dim3(kBlock), 0, (hipStream_t)stream, lengths, B,
+    if (T > 65535)
+        return fail(R48_EINVAL, "T > 65535");
+    hipLaunchKernelGGL(k_row_weights, dim3((unsigned)((n + kBlock - 1) / kBlock), (unsigned)T), dim3(kBlock), 0,
+                       (hipStream_t)stream, lengths, B,
                        td_sum, T, n, wn, cm);
     return launched("k_row_weights");
 }

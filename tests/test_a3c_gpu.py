@@ -71,6 +71,28 @@ def test_discounted_returns_match_oracle(drop_last):
         assert (out[L:, i] == 0).all()
 
 
+@pytest.mark.parametrize("drop_last", [False, True])
+def test_discounted_returns_vector_path_equals_scalar_path(drop_last):
+    """r48_discounted_returns' 4-boards-per-lane path (n % 4 == 0, 16-byte aligned slabs) equals the
+    one-board-per-lane path bit for bit (the latter forced by 4-byte-offset views of the same data)."""
+    from rein48_amd.a3c import kernels as K
+    rng = np.random.default_rng(3)
+    T, n = 100, 4096
+    rewards = rng.normal(size=(T, n)).astype(np.float32)
+    lengths = rng.integers(0, T + 1, n).astype(np.int32)
+    boot = rng.normal(size=n).astype(np.float32)
+    out4 = K.discounted_returns(torch.from_numpy(rewards).to(DEV), torch.from_numpy(lengths).to(DEV),
+                                torch.from_numpy(boot).to(DEV), 0.9, drop_last=drop_last)
+
+    def offset(a, dtype):
+        buf = torch.zeros(a.size + 1, dtype=dtype, device=DEV)
+        buf[1:] = torch.from_numpy(a.ravel()).to(DEV)
+        return buf[1:].view(a.shape)
+    out1 = K.discounted_returns(offset(rewards, torch.float32), offset(lengths, torch.int32),
+                                offset(boot, torch.float32), 0.9, drop_last=drop_last)
+    assert torch.equal(out4, out1)
+
+
 def test_discounted_returns_match_reference_golden():
     """r48_discounted_returns (drop-last mode) vs the reference's own _get_target_value_list
     outputs (tests/golden/a3c_golden.json, made by executing a3c.py:246-256), all 48 cases in
