@@ -75,7 +75,7 @@ class A3CTrainer:
         self.rewards = torch.zeros((T, n), dtype=torch.float32, device=self.device)
         self.sample_ctr = 0
         self.updates = 0
-        self._rollout_v = None       # [T, n] V(boards[t]) from the last megakernel rollout, or None
+        self._rollout_v = None       # ([T + 1, n] V(boards[t]) slab of the last megakernel rollout, updates)
 
     # ------------------------------------------------------------------ helpers
     def _features(self, boards):
@@ -174,8 +174,8 @@ class A3CTrainer:
         # r48_cnn_policy_forward value pass it replaces, bit for bit)
         values = None
         if cfg.mode == "reference" and cfg.rollout_values:
-            if getattr(self, "_v_buf", None) is None:
-                self._v_buf = torch.empty((T, n), dtype=torch.float32, device=self.device)
+            if getattr(self, "_v_buf", None) is None:   # row T: V(boards[T]), filled by the update
+                self._v_buf = torch.empty((T + 1, n), dtype=torch.float32, device=self.device)
             values = self._v_buf
         _lib.check(_lib.load().r48_cnn_rollout(
             env.boards.data_ptr(), n, T, wfrag.data_ptr(), bias.data_ptr(),
@@ -213,14 +213,12 @@ class A3CTrainer:
             need_values = not (fused and cfg.fused_update and cfg.mode == "textbook")
             v_all = None
             rv = self._rollout_v
-            if need_values and rv is not None and rv[1] == self.updates:
-                # V(boards[t]) from the rollout; reference states are boards[1..T], so the rows shift
-                # by one and only V(boards[T]) (never a rollout input) takes a forward pass
-                v_all = torch.empty((T, n), dtype=torch.float32, device=self.device)
-                off = 1 if cfg.mode == "reference" else 0
-                v_all[0:T - off].copy_(rv[0][off:T])
-                if off:
-                    v_all[T - 1] = value(self.boards[T]).view(n)
+            if need_values and rv is not None and rv[1] == self.updates and cfg.mode == "reference":
+                # V(boards[t]) from the rollout (rows 0..T-1 of a [T + 1, n] slab); the reference
+                # states are boards[1..T], so V(boards[T]) -- never a rollout input -- takes one
+                # forward into row T and the values are the view of rows 1..T (no copy)
+                rv[0][T] = value(self.boards[T]).view(n)
+                v_all = rv[0][1:T + 1]
             elif need_values:
                 v_all = torch.empty((T, n), dtype=torch.float32, device=self.device)
                 for t0 in range(0, T, T if fused else cfg.update_chunk):

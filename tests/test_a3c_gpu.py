@@ -393,7 +393,7 @@ def test_rollout_values_replace_the_value_pass(n_boards):
             T = cfg.max_steps
             v = cnn_forward(tr.boards[0:T].reshape(-1, 16).contiguous(), wfrag, bias, exponents=False,
                             logits=False, value=True)[1].view(T, n_boards)
-            assert torch.equal(tr._rollout_v[0], v)
+            assert torch.equal(tr._rollout_v[0][:T], v)
         losses = tr.update()
         torch.cuda.synchronize()
         res.append((losses["actor_loss"], losses["critic_loss"], tr.flat.data.clone()))
