@@ -462,7 +462,18 @@ def run_extras_all_ranks(world, rank, items):
     return ex
 
 
+def hip_schedule_spin(local):
+    """hipSetDeviceFlags(hipDeviceScheduleSpin) on torch's own HIP runtime, before torch creates the
+    device context: synchronisations spin on the completion signal instead of sleeping until an
+    interrupt wakes the thread."""
+    import ctypes
+    hip = ctypes.CDLL(os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so"))
+    if hip.hipSetDevice(local) != 0 or hip.hipSetDeviceFlags(1) != 0:
+        print("bench.py: hipSetDeviceFlags(hipDeviceScheduleSpin) failed", file=sys.stderr)
+
+
 def main():
+    global SYNC_POLL, SETTLE_S
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=6000)
@@ -475,12 +486,15 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
-    ap.add_argument("--sync", choices=("poll", "block"), default="block",
-                    help="end of the timed region: spin on its last event, then synchronize (poll) or only "
-                         "synchronize (block)")
+    ap.add_argument("--settle", type=float, default=SETTLE_S,
+                    help="seconds of untimed stepping before each timed region (after the warm-up steps)")
+    ap.add_argument("--sync", choices=("poll", "block", "spin"), default="block",
+                    help="end of the timed region: spin on its last event, then synchronize (poll), only "
+                         "synchronize (block), or synchronize with the HIP runtime set to spin-wait "
+                         "(hipDeviceScheduleSpin) instead of sleeping (spin)")
     args = ap.parse_args()
-    global SYNC_POLL
     SYNC_POLL = args.sync == "poll"
+    SETTLE_S = args.settle
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(launch_ranks(args.gpus))
@@ -499,6 +513,8 @@ def main():
     ndev = torch.cuda.device_count()
     if backend != "nccl":
         local %= max(1, ndev)
+    if args.sync == "spin":
+        hip_schedule_spin(local)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
