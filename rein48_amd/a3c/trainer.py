@@ -76,6 +76,9 @@ class A3CTrainer:
         self.sample_ctr = 0
         self.updates = 0
         self._rollout_v = None       # ([T + 1, n] V(boards[t]) slab of the last megakernel rollout, updates)
+        self._mask = None            # [T, n] valid-step mask of the last rollout, formed on first use
+        # before the first rollout every step is valid (a full-length segment for every board)
+        self.lengths = torch.full((n,), T, dtype=torch.int32, device=self.device)
 
     # ------------------------------------------------------------------ helpers
     def _features(self, boards):

@@ -711,13 +711,9 @@ int fail(int code, const std::string &msg)
     return code;
 }
 
-int grid_size()
-{
-    int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) == hipSuccess)
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    return cus;
-}
+// one fixed persistent grid (the MI355X's 256 CUs), not a query of the current device, so the
+// per-wave record workspace (r48_cnn_train_workspace_floats) and the launch always agree
+constexpr int grid_size() { return 256; }
 
 }  // namespace
 

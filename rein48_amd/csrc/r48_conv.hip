@@ -78,13 +78,14 @@ int launched(const char *what)
     return R48_OK;
 }
 
-int cu_count()
-{
-    int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) == hipSuccess)
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    return cus;
-}
+// Persistent grids and their per-workgroup record buffers use ONE fixed workgroup count -- the
+// MI355X's 256 CUs -- not a query of the current device: the statistics / workspace sizes
+// (r48_conv_stats_floats, r48_conv_wgrad_workspace_floats, r48_q_head_workspace_floats) and the
+// launch grids then agree whatever device is current at allocation or call time, and a device with
+// fewer CUs (a compute partition) just runs the extra workgroups in a second wave.
+constexpr int kPersistentGroups = 256;
+
+constexpr int cu_count() { return kPersistentGroups; }
 
 // ---------------------------------------------------------------------------------- forward
 // x bf16 [boards][16][32 NC], wfrag (tap, O, c) fragments: lane l element j = W[16 O + (l & 15)]

@@ -317,8 +317,9 @@ __global__ __launch_bounds__(kBlock) void k_step(int8_t *boards, int64_t n, int6
 // traj_done ([n_steps][n], each nullable) -- one 2-byte store per plane per pair and step.
 template <bool RANDOM, bool AUTO_RESET, bool REWARD, int NP, bool TRAJ = false>
 // The read-ahead below needs ~62 VGPRs; waves_per_eu(8) holds the allocator to the 64 that keep the
-// 8 waves per SIMD the VALU issue bound needs.
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_step_n(int8_t *boards, int64_t n, int64_t gid0, uint32_t k0, uint32_t k1,
+// 8 waves per SIMD the VALU issue bound needs. The merge-reward variants need more than 64 (they
+// spilled 28-48 B per lane to scratch under the cap), so they keep the plain launch bounds.
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(REWARD ? 1 : 8, 8))) void k_step_n(int8_t *boards, int64_t n, int64_t gid0, uint32_t k0, uint32_t k1,
                                                    uint32_t step0, int32_t n_steps, int8_t *__restrict__ actions,
                                                    uint8_t *__restrict__ done, uint8_t *__restrict__ changed,
                                                    int32_t *__restrict__ reward, int32_t *__restrict__ score,
@@ -445,9 +446,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
             }
         }
         if (RANDOM) {   // the line form of the last action, or rows after a reset in the last step
+            // (without AUTO_RESET a done board is not reset: it stays in the line form of its action)
 #pragma unroll
             for (int j = 0; j < 2 * NP; j++)
-                ob[j] = r[j].done ? 0u : r[j].a << 6;
+                ob[j] = (AUTO_RESET && r[j].done) ? 0u : r[j].a << 6;
         }
 #pragma unroll
         for (int j = 0; j < NP; j++) {

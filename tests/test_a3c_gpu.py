@@ -246,14 +246,18 @@ def test_fused_cnn_policy_is_independent_of_tiling():
             assert torch.equal(f[lo:hi], q), (lo, hi)
 
 
-@pytest.mark.parametrize("exponents", [True, False])
+@pytest.mark.parametrize("exponents,T,n", [(True, 3, 10_007), (False, 3, 10_007),
+                                            (True, 4, 262_154)])   # 2^20 + 40 rows: >= 32 tiles per wave
 @pytest.mark.parametrize("mode", ["textbook", "reference"])
-def test_fused_cnn_update_gradients_match_torch(mode, exponents):
+def test_fused_cnn_update_gradients_match_torch(mode, exponents, T, n):
     """r48_cnn_train_grad (forward + loss + backward + weight gradients in one MFMA pass, rows
     moved to K through ds_read_b64_tr_b16 LDS images) vs PyTorch autograd of the trainer's own
     loss (losses.chunk_loss) on the same states. Per parameter tensor, error = max|g - g32| /
     max|g32| against the fp32 autograd gradient: within 1.5x (+2e-3) of PyTorch's own bf16
-    gradient error and below 5e-2. Actor/critic losses within 1e-2."""
+    gradient error and below 5e-2. Actor/critic losses within 1e-2. The kernel's grid is 1,024
+    waves of 32-row tiles: 30,021 rows is <= 1 tile per wave; 2^20 + 40 rows is the steady state
+    the bench runs (>= 32 tiles per wave: the AGPR gradient carried across tiles, the next tile's
+    rows prefetched, a partial last tile)."""
     from rein48_amd.a3c import kernels as K
     from rein48_amd.a3c.fused import cnn_train_grad
     from rein48_amd.a3c.losses import chunk_loss, segment_stats
@@ -264,7 +268,6 @@ def test_fused_cnn_update_gradients_match_torch(mode, exponents):
         for m in (net.conv1, net.conv2, net.heads):
             m.bias.uniform_(-0.3, 0.3)
     rng = np.random.default_rng(8)
-    T, n = 3, 10_007                                    # 30,021 rows: a partial last tile
     b = rng.integers(1, 10, size=(T, n, 16)).astype(np.int8)
     b[rng.random((T, n, 16)) < 0.4] = 0
     boards = torch.from_numpy(b).to(DEV)
@@ -348,6 +351,47 @@ def test_fused_rollout_trajectory_replays_through_the_env():
         assert torch.equal(env.boards, tr.boards[t + 1]), t
         assert torch.equal(done, tr.done[t]), t
         assert torch.equal(rew.float(), tr.rewards[t]), t
+
+
+@pytest.mark.parametrize("mode", ["textbook", "reference"])
+def test_rollout_megakernel_at_bench_size(mode):
+    """r48_cnn_rollout at the bench's size, 2^20 + 5 boards x 100 steps (8 tile pairs per wave and
+    a partial last pair; the small tests run <= 1 pair per wave): bit-identical to the per-step
+    rollout (policy kernel + env kernel per step) in boards, actions, done, rewards, lengths and
+    counters, and the whole trajectory replays through a fresh VecGame with the recorded actions."""
+    from rein48_amd import VecGame
+    from rein48_amd.a3c import A3CConfig, A3CTrainer
+    n, T = (1 << 20) + 5, 100
+    out = []
+    for mega in (True, False):
+        cfg = A3CConfig(n_boards=n, max_steps=T, mode=mode, net="cnn", bf16=True, features="exponents",
+                        seed=1234, fused_rollout=mega)
+        tr = A3CTrainer(cfg, device=DEV)
+        before = tr.env.counters
+        tr.rollout()
+        torch.cuda.synchronize()
+        out.append((tr.boards, tr.actions, tr.done, tr.rewards, tr.env.boards, tr.lengths, tr.finished))
+        counters = (tr.env.counters, tr.sample_ctr)
+        if mega:
+            mega_counters = counters
+        else:
+            assert counters == mega_counters
+        del tr
+    for a, b in zip(*out):
+        assert torch.equal(a, b)
+    boards, actions, done, rewards = out[0][:4]
+    del out
+    torch.cuda.empty_cache()
+    env = VecGame(n, device=DEV, seed=1234)
+    env.counters = before
+    env.reset()
+    assert torch.equal(env.boards, boards[0])
+    for t in range(T):
+        _, rew, d = env.step(actions[t], merge_reward=True)
+        assert torch.equal(env.boards, boards[t + 1]), t
+        assert torch.equal(d, done[t]), t
+        if mode == "textbook":
+            assert torch.equal(rew.float(), rewards[t]), t
 
 
 @pytest.mark.parametrize("n_boards", [5003, 1, 65])

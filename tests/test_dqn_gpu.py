@@ -503,6 +503,118 @@ def test_conv3x3_bn_grad_reduction_matches_fp64(B, with_add):
         assert bool((err <= 1e-5 * terms.abs().sum(0) + 1e-30).all()), float(err.max())
 
 
+# ---------------------------------------------------------------- steady-state sizes (the bench's)
+# The tests above run the conv kernels at <= 1 tile per wave and the wgrad ring at <= 3 steps per
+# workgroup. At the bench's 64K-board minibatch k_conv3x3 runs 2 tiles per wave (the cross-tile row
+# prefetch and the tile += stride loop) and k_conv_wgrad 32 128-row steps per workgroup (the 3-buffer
+# LDS-DMA ring wraps ~10 times). These run those sizes (and a ragged one) against fp64 references.
+def _shift_cells(x, dr, dc):
+    """x [B, 16, C] (cell = 4 r + c) -> x at cell (r + dr, c + dc), zero outside the grid."""
+    B, _, C = x.shape
+    g = x.view(B, 4, 4, C)
+    out = torch.zeros_like(g)
+    r0, r1 = max(0, -dr), min(4, 4 - dr)
+    c0, c1 = max(0, -dc), min(4, 4 - dc)
+    out[:, r0:r1, c0:c1] = g[:, r0 + dr:r1 + dr, c0 + dc:c1 + dc]
+    return out.view(B, 16, C)
+
+
+def _conv_fp64(x, w, bias=None):
+    """3x3 conv, padding 1, on [B, 16, Cin] -> [B, 16, 64] in float64 (9 shifted matmuls)."""
+    xd = x.double()
+    B = xd.shape[0]
+    y = torch.zeros(B * 16, w.shape[0], dtype=torch.float64, device=x.device)
+    wd = w.double()
+    for kr in range(3):
+        for kc in range(3):
+            xs = _shift_cells(xd, kr - 1, kc - 1).reshape(B * 16, -1)
+            y += xs @ wd[:, :, kr, kc].t()
+    if bias is not None:
+        y += bias.double()
+    return y.view(B, 16, -1)
+
+
+def _wgrad_fp64(gy, x):
+    """dW[o, c, kr, kc] = sum over boards and cells of gy[b, p, o] * x[b, p + (kr-1, kc-1), c]."""
+    B, _, C = x.shape
+    gd = gy.double().reshape(B * 16, -1)
+    xd = x.double()
+    dw = torch.zeros(gd.shape[1], C, 3, 3, dtype=torch.float64, device=x.device)
+    for kr in range(3):
+        for kc in range(3):
+            dw[:, :, kr, kc] = gd.t() @ _shift_cells(xd, kr - 1, kc - 1).reshape(B * 16, C)
+    return dw
+
+
+@pytest.mark.parametrize("B", [1 << 16, (1 << 16) + 5])
+def test_conv3x3_kernels_at_bench_size_match_fp64(B):
+    """k_conv3x3 forward, forward + BN statistics, data gradient + residual add, and k_conv_wgrad at
+    the bench's 64K-board minibatch (2 tiles per wave, 32 ring steps per workgroup) and a ragged
+    64K + 5, vs float64 on the same bf16 inputs: forward / data gradient within 1e-2 of the largest
+    value (bf16 output rounding), every element; the statistics within 1e-5 of the fp64 sums of the
+    written outputs; the weight gradient (fp32 out, summed over 2^20 rows) within 1e-4 of its largest
+    entry -- one lost or doubled 128-row ring step moves entries by ~1e-2 of that."""
+    from rein48_amd import _lib
+    from rein48_amd.dqn.conv import conv3x3, conv3x3_wgrad, pack_conv, pack_conv_dgrad
+    g = torch.Generator(device="cpu").manual_seed(B)
+    w = (torch.randn(64, 64, 3, 3, generator=g) * 0.1).to(DEV).to(torch.bfloat16).float()
+    bias = (torch.randn(64, generator=g) * 0.5 + 1.0).to(DEV)
+    x = torch.randn(B, 16, 64, generator=g).to(DEV).to(torch.bfloat16)
+    y_ref = _conv_fp64(x, w, bias)
+    st = torch.empty(int(_lib.load().r48_conv_stats_floats()), dtype=torch.float32, device=DEV)
+    y = conv3x3(x, pack_conv(w, 64), bias, stats=st)
+    assert _rel(y, y_ref) < 1e-2
+    assert torch.equal(y, conv3x3(x, pack_conv(w, 64), bias))
+    rec = st.view(-1, 2, 64).double().sum(0)
+    yd = y.reshape(-1, 64).double()
+    for got, want in ((rec[0], yd.sum(0)), (rec[1], (yd * yd).sum(0))):
+        assert float((got - want).abs().max()) <= 1e-5 * float(want.abs().max())
+    del y_ref, yd
+    gy = torch.randn(B, 16, 64, generator=g).to(DEV).to(torch.bfloat16)
+    add = torch.randn(B, 16, 64, generator=g).to(DEV).to(torch.bfloat16)
+    # data gradient = conv with the flipped, transposed taps
+    wt = w.flip(2, 3).transpose(0, 1).contiguous()
+    dx_ref = _conv_fp64(gy, wt) + add.double()
+    dx = conv3x3(gy, pack_conv_dgrad(w), add=add)
+    assert _rel(dx, dx_ref) < 1e-2
+    del dx_ref
+    dw_ref = _wgrad_fp64(gy, x)
+    dw = conv3x3_wgrad(gy, x)
+    assert _rel(dw, dw_ref) < 1e-4, _rel(dw, dw_ref)
+    assert torch.equal(conv3x3_wgrad(gy, x), dw)
+
+
+@pytest.mark.parametrize("B,with_add", [(1 << 16, True), ((1 << 16) + 5, False)])
+def test_conv3x3_bn_grad_at_bench_size_matches_fp64(B, with_add):
+    """r48_conv3x3_bn_grad at the bench's minibatch (2 tiles per wave, the cross-tile prefetch):
+    output == the plain data-gradient launch bit for bit, BN-backward records == the fp64 sums
+    within 1e-5 of the summed magnitudes (as test_conv3x3_bn_grad_reduction_matches_fp64)."""
+    import ctypes
+    from rein48_amd import _lib
+    from rein48_amd.dqn.conv import conv3x3, pack_conv_dgrad
+    g = torch.Generator(device="cpu").manual_seed(B + 3 * with_add)
+    frags = pack_conv_dgrad((torch.randn(64, 64, 3, 3, generator=g) * 0.1).to(DEV))
+    dy = torch.randn(B, 16, 64, generator=g).to(DEV).to(torch.bfloat16)
+    add = torch.randn(B, 16, 64, generator=g).to(DEV).to(torch.bfloat16) if with_add else None
+    bn_x = (torch.randn(B, 16, 64, generator=g) + 3.0).to(DEV).to(torch.bfloat16)
+    mask = torch.randint(0, 256, (B * 16, 8), generator=g, dtype=torch.uint8).to(DEV)
+    save = torch.cat([torch.randn(64, generator=g) + 3.0, torch.rand(64, generator=g) + 0.5]).to(DEV)
+    L = _lib.load()
+    part = torch.full((int(L.r48_conv_stats_floats()),), float("nan"), dtype=torch.float32, device=DEV)
+    out = torch.empty_like(dy)
+    _lib.check(L.r48_conv3x3_bn_grad(_lib.ptr(dy), B, _lib.ptr(frags), _lib.ptr(add), _lib.ptr(out),
+                                     _lib.ptr(bn_x), _lib.ptr(mask), _lib.ptr(save), _lib.ptr(part),
+                                     ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
+    assert torch.equal(out, conv3x3(dy, frags, add=add))
+    bits = ((mask.long().unsqueeze(-1) >> torch.arange(8, device=DEV)) & 1).reshape(B * 16, 64).bool()
+    gd = torch.where(bits, out.reshape(-1, 64).double(), torch.zeros((), dtype=torch.float64, device=DEV))
+    xd = bn_x.reshape(-1, 64).double() - save[:64].double()
+    rec = part.view(-1, 2, 64).double().sum(0)
+    for got, terms in ((rec[0], gd), (rec[1], gd * xd)):
+        err = (got - terms.sum(0)).abs()
+        assert bool((err <= 1e-5 * terms.abs().sum(0) + 1e-30).all()), float(err.max())
+
+
 def test_onehot32_exact():
     from rein48_amd.dqn.conv import board_onehot32
     b = np.random.default_rng(5).integers(0, 18, size=(3001, 16)).astype(np.int8)
@@ -542,7 +654,7 @@ def test_resnet_update_custom_conv_matches_structured_gemm():
         assert float((ga - gb).norm()) <= 5e-2 * float(gb.norm()) + 1e-6
 
 
-@pytest.mark.parametrize("B", [4096, 1000])
+@pytest.mark.parametrize("B", [4096, 1000, 1 << 16])      # 1 << 16: the bench's minibatch
 def test_resnet_train_step_matches_autograd(B):
     """train_step.ResNetTrainStep (explicit forward/backward: BN statistics summed in the conv
     epilogues, BN ReLU masks, the block-input gradient summed in the data-gradient conv's epilogue,

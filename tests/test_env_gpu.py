@@ -553,10 +553,10 @@ def test_input_validation():
         v.step(torch.zeros(8, dtype=torch.int8))  # host tensor
 
 
-def _step_n_vs_steps(n, off, K, flags, seed, rng, actions=None):
+def _step_n_vs_steps(n, off, K, flags, seed, rng, actions=None, emax=8, p_empty=0.5):
     """step_n(K) on one env vs K single-step launches (k_step) on a twin: every output plane,
     the boards, the counters and the bad-action counter must be identical."""
-    b0 = rand_boards(rng, n, emax=8)
+    b0 = rand_boards(rng, n, emax=emax, p_empty=p_empty)
     a, b = vec(n, seed=seed, offset=off), vec(n, seed=seed, offset=off)
     put(a, b0)
     put(b, b0)
@@ -584,6 +584,21 @@ def test_step_n_equals_repeated_steps(K, off):
     grid's partial last tile)."""
     rng = np.random.default_rng(K * 10 + off)
     _step_n_vs_steps(300_001, off, K, O.RANDOM_POLICY | O.AUTO_RESET | O.MERGE_REWARD, 77, rng)
+
+
+@pytest.mark.parametrize("flags", [O.RANDOM_POLICY, O.RANDOM_POLICY | O.MERGE_REWARD])
+@pytest.mark.parametrize("K", [1, 3, 20, 300])
+def test_step_n_random_policy_without_auto_reset(K, flags):
+    """Random policy WITHOUT auto-reset (VecGame.step_n's default): boards that end the call done
+    are not reset, so k_step_n must return them to rows from the line form of their last action
+    (not leave them transposed / reversed). Near-full boards (5 % blanks, exponents up to 12) so
+    that many boards are done after a few steps, with every last action; == K single steps."""
+    rng = np.random.default_rng(900 + K)
+    a, _ = _step_n_vs_steps(100_003, 0, K, flags, 31, rng, emax=12, p_empty=0.05)
+    done = host(a.done)
+    assert done.mean() > 0.2, done.mean()
+    acts = host(a.actions)[done != 0]
+    assert len(np.unique(acts)) == 4   # done boards whose last action was each of the four
 
 
 @pytest.mark.parametrize("flags", [0, O.AUTO_RESET | O.MERGE_REWARD])
