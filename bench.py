@@ -325,7 +325,8 @@ def _allreduce_label(world):
     return "%s all_reduce(SUM)/world" % ("RCCL (torch backend 'nccl')" if b == "nccl" else "torch backend '%s'" % b)
 
 
-def a3c_config3(dev, seed, n_boards, updates=3, world=1, mode="textbook", features="exponents", warmup=2):
+def a3c_config3(dev, seed, n_boards, updates=3, world=1, mode="textbook", features="exponents", warmup=2,
+                net="cnn", bf16=True):
     """BASELINE configs[2] (world 1: 2^20 boards + 2-layer CNN policy on 1 MI355X) and configs[3]
     (world > 1: 2^20 boards per GPU, 8M boards on 8 GPUs, one all-reduce of the flat fp32
     gradient per update): A3C rollout (MAX_STEP_NUM = 100 steps: fused CNN inference + softmax +
@@ -333,9 +334,10 @@ def a3c_config3(dev, seed, n_boards, updates=3, world=1, mode="textbook", featur
     all-reduce, TF1 RMSProp kernel). mode "reference" + features "values" is what a user of the
     reference gets (raw tile values in, a3c.py:37-39,139; post-step states, reward 0, dropped last
     reward and the literal [B,B,4]-broadcast actor loss, a3c.py:99-123,187-256); "textbook" +
-    "exponents" is the build's learning-oriented variant."""
+    "exponents" is the build's learning-oriented variant. net "mlp" + bf16 False is the reference's
+    own network (a3c.py:136-169, fp32) at the same size."""
     from rein48_amd.a3c import A3CConfig, A3CTrainer
-    cfg = A3CConfig(n_boards=n_boards, max_steps=100, mode=mode, net="cnn", bf16=True,
+    cfg = A3CConfig(n_boards=n_boards, max_steps=100, mode=mode, net=net, bf16=bf16,
                     features=features, seed=seed, update_chunk=10)
     tr = A3CTrainer(cfg, device=dev)
     for _ in range(warmup):                           # warm-up (allocator, kernels, first collective, clocks)
@@ -360,7 +362,9 @@ def a3c_config3(dev, seed, n_boards, updates=3, world=1, mode="textbook", featur
     board_steps = world * n_boards * cfg.max_steps  # every board is stepped every rollout step
     lab = _allreduce_label(world)
     return {"boards": world * n_boards, "boards_per_gpu": n_boards, "n_gpus": world,
-            "net": "cnn (conv2x2x32, conv2x2x64, heads 256->4/1), bf16", "mode": mode, "features": features,
+            "net": ("cnn (conv2x2x32, conv2x2x64, heads 256->4/1)" if net == "cnn" else
+                    "mlp (a3c.py:136-169: 16->64 ReLU6->4 ReLU softmax, 16->64 ReLU6->1)")
+                   + (", bf16" if bf16 else ", fp32"), "mode": mode, "features": features,
             "gradient_allreduce": ("%s of %d fp32 per update" % (lab, tr.flat.grad.numel())) if lab else None,
             "rollout_ms": r, "update_ms": u,
             "rollout_env_steps_per_s": board_steps / (r * 1e-3),
@@ -579,6 +583,9 @@ def main():
         for key, fn in (("a3c_config3", lambda: a3c_config3(dev, args.seed, n)),
                         ("a3c_config3_reference",
                          lambda: a3c_config3(dev, args.seed, n, mode="reference", features="values")),
+                        ("a3c_config3_reference_mlp",
+                         lambda: a3c_config3(dev, args.seed, n, mode="reference", features="values", net="mlp",
+                                             bf16=False)),
                         ("dqn_config5", lambda: dqn_config5(dev, args.seed, 1 << 21))):
             try:
                 ex[key] = fn()

@@ -10,7 +10,6 @@
 
 #include <cstdint>
 #include <cstdio>
-#include <cstdlib>
 #include <string>
 
 #include "../../include/rein48.h"
@@ -480,107 +479,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(REWARD ?
                 emit<RANDOM, REWARD>(r, i, boards, actions, done, changed, reward, score);
             }
         }
-    }
-}
-
-// ---------------------------------------------------------------- K steps, one board per lane
-// k_step_n1: the random-policy k_step_n with ONE board per lane, so a 2^20-board call is 16,384
-// waves -- twice the 8 x 1,024 resident slots. Waves finish at different times (the VALU arbiter
-// prefers the oldest wave of a SIMD), and with one round of waves the last ones run with too few
-// partners to fill the VALU; with two rounds a freed slot is refilled by a wave of the second, so
-// only the second round's (half as long) waves form the tail. Same draw contract: the two lanes of
-// a board pair still share ONE Philox call per pair-step. Every other step each lane computes one
-// Philox4x32-10 -- the even lane the pair's call for step t, the odd lane the call for step t + 1
-// -- and the two words the partner needs cross the lane pair in one DPP swap (pair_block_draws).
-__device__ __forceinline__ uint32_t swap_lane_pair(uint32_t v)
-{
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);   // quad_perm(1, 0, 3, 2)
-}
-
-// This board's draws for steps `step` (d0) and `step + 1` (d1); m = 0 on the even board of the pair,
-// ~0 on the odd one. All 64 lanes must be active (the DPP swap reads the partner lane).
-__device__ __forceinline__ void pair_block_draws(uint64_t q, uint32_t step, uint32_t m, uint32_t k0, uint32_t k1,
-                                                 Draw &d0, Draw &d1)
-{
-    uint32_t w[4];
-    philox_words(w, q, step + (m & 1u), r48::kStepTag, k0, k1);
-    // the even lane holds call(step) and gives its words 2, 3 (the odd board's step draws); the odd
-    // lane holds call(step + 1) and gives its words 0, 1 (the even board's step + 1 draws)
-    const uint32_t rx = swap_lane_pair(r48::bsel(m, w[0], w[2])), ry = swap_lane_pair(r48::bsel(m, w[1], w[3]));
-    d0 = Draw{r48::bsel(m, rx, w[0]), r48::bsel(m, ry, w[1])};
-    d1 = Draw{r48::bsel(m, w[2], rx), r48::bsel(m, w[3], ry)};
-}
-
-template <bool AUTO_RESET, bool REWARD>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(REWARD ? 1 : 8, 8))) void k_step_n1(
-    int8_t *boards, int64_t n, int64_t gid0, uint32_t k0, uint32_t k1, uint32_t step0, int32_t n_steps,
-    int8_t *__restrict__ actions, uint8_t *__restrict__ done, uint8_t *__restrict__ changed,
-    int32_t *__restrict__ reward, int32_t *__restrict__ score)
-{
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    const bool want_score = score != nullptr;
-    const int32_t last = n_steps - 1;
-    __shared__ __attribute__((aligned(16))) r48::Orient tab[16];
-    load_orient_table(tab);
-    if ((int64_t)(blockIdx.x + 1) * kBlock <= n && (gid0 & 1) == 0) {   // block-uniform
-        Board b = load_board(boards, i);
-        const uint64_t q = (uint64_t)(gid0 + i) >> 1;
-        const uint32_t m = 0u - (uint32_t)(threadIdx.x & 1);
-        Draw d0, d1;
-        pair_block_draws(q, step0, m, k0, k1, d0, d1);
-        r48::Orient s = orient_at(tab, (d0.x >> 26) & 0x30u);
-        LaneOut r;
-        // the priority phases of k_step_n, boundaries rounded to the two-step body
-        const int32_t q3 = n_steps <= 64 ? 5 : 6;
-        const int32_t ends[4] = {(n_steps >> 3) & ~1, ((n_steps * 3) >> 3) & ~1, ((n_steps * q3) >> 3) & ~1,
-                                 n_steps & ~1};
-        int32_t t = 0;
-#pragma nounroll
-        for (int ph = 0; ph < 4; ph++) {
-            switch (ph) {
-            case 0: __builtin_amdgcn_s_setprio(3); break;
-            case 1: __builtin_amdgcn_s_setprio(2); break;
-            case 2: __builtin_amdgcn_s_setprio(1); break;
-            default: __builtin_amdgcn_s_setprio(0); break;
-            }
-            for (const int32_t end = ends[ph]; t < end; t += 2) {
-                const uint32_t step = step0 + (uint32_t)t;
-                // step t (the next action, d1's, is known: its selector record reads under the move)
-                const uint32_t a1 = (d1.x >> 26) & 0x30u;
-                r48::Orient x = orient_at(tab, ((d0.x >> 24) & 0xC0u) + a1);
-                b = r48::reorient(b, s);
-                r = step_lane_pre<AUTO_RESET, REWARD>(b, x, a1, tab, d0, want_score && t == last);
-                s = x;
-                // step t + 1, with the next block's Philox under it
-                Draw n0, n1;
-                pair_block_draws(q, step + 2u, m, k0, k1, n0, n1);
-                const uint32_t a2 = (n0.x >> 26) & 0x30u;
-                x = orient_at(tab, ((d1.x >> 24) & 0xC0u) + a2);
-                b = r48::reorient(b, s);
-                r = step_lane_pre<AUTO_RESET, REWARD>(b, x, a2, tab, d1, want_score && t + 1 == last);
-                s = x;
-                d0 = n0;
-                d1 = n1;
-            }
-        }
-        if (n_steps & 1) {   // the odd last step
-            const uint32_t a1 = (d1.x >> 26) & 0x30u;
-            r48::Orient x = orient_at(tab, ((d0.x >> 24) & 0xC0u) + a1);
-            b = r48::reorient(b, s);
-            r = step_lane_pre<AUTO_RESET, REWARD>(b, x, a1, tab, d0, want_score);
-        }
-        // back to rows: from the line form of the last action, or rows after a reset in the last step
-        r.b = r48::reorient(b, orient_at(tab, (AUTO_RESET && r.done) ? 0u : r.a << 6));
-        emit<true, REWARD>(r, i, boards, actions, done, changed, reward, score);
-    } else if (i < n) {
-        Board b = load_board(boards, i);
-        LaneOut r;
-        for (int32_t t = 0; t < n_steps; t++) {
-            const Draw d = board_draw((uint64_t)(gid0 + i), step0 + (uint32_t)t, k0, k1);
-            r = step_lane<true, AUTO_RESET, REWARD, false>(b, 0u, d, want_score && t == last);
-            b = r.b;
-        }
-        emit<true, REWARD>(r, i, boards, actions, done, changed, reward, score);
     }
 }
 
@@ -1118,19 +1016,6 @@ void launch_steps(r48_env *env, int32_t n_steps, int8_t *actions, uint32_t flags
                            env->n, env->gid0, k0, k1, env->step_ctr, n_steps, actions, done, changed, reward, score,
                            env->err, (int8_t *)nullptr, (uint8_t *)nullptr);
     };
-    auto lane1 = [&](auto kern) {
-        hipLaunchKernelGGL(kern, grid_for(env->n), dim3(kBlock), 0, stream, env->boards, env->n, env->gid0, k0, k1,
-                           env->step_ctr, n_steps, actions, done, changed, reward, score);
-    };
-    static const int lane_boards = [] {
-        const char *v = getenv("R48_STEPN_LANE_BOARDS");
-        return v ? atoi(v) : 2;
-    }();
-    if (rnd && n_steps > 1 && lane_boards == 1) {
-        if (ar) rw ? lane1(k_step_n1<true, true>) : lane1(k_step_n1<true, false>);
-        else rw ? lane1(k_step_n1<false, true>) : lane1(k_step_n1<false, false>);
-        return;
-    }
 #define R48_GO(RN, AR, RW) \
     (n_steps == 1 ? one(k_step<RN, AR, RW>) : many(k_step_n<RN, AR, RW, kStepNP>))
     if (rnd) {

@@ -596,7 +596,7 @@ def test_step_n_random_policy_without_auto_reset(K, flags):
     rng = np.random.default_rng(900 + K)
     a, _ = _step_n_vs_steps(100_003, 0, K, flags, 31, rng, emax=12, p_empty=0.05)
     done = host(a.done)
-    assert done.mean() > 0.2, done.mean()
+    assert done.mean() > 0.1, done.mean()
     acts = host(a.actions)[done != 0]
     assert len(np.unique(acts)) == 4   # done boards whose last action was each of the four
 
