@@ -295,6 +295,23 @@ class A3CTrainer:
         self.rollout()
         return self.update()
 
+    def policy(self, seed=0x5A3C):
+        """The current policy as `policy(boards int8 [n, 16], t) -> actions int8 [n]` (choose_action,
+        a3c.py:89-93: a draw from the softmax; Philox keyed by (seed, board, t)) for
+        evaluate.play_episodes. Weights are packed once, at the call."""
+        cfg = self.cfg
+        exps = cfg.features == "exponents"
+        if cfg.net == "cnn" and cfg.bf16 and cfg.fused_policy:
+            wfrag, bias = pack_cnn(self.net)
+            return lambda boards, t: cnn_forward(boards, wfrag, bias, exponents=exps, logits=False, value=False,
+                                                 actions=True, seed=seed, ctr=t)[2]
+
+        def act(boards, t):
+            with torch.no_grad():
+                logits, _ = self._net(self._features(boards))
+            return K.sample_actions(logits.float().contiguous(), seed, t)[0]
+        return act
+
     def scores(self):
         """a3c.py:214 SCORE: tile sum of each segment's final state."""
         return self.env.score()

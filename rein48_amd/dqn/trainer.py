@@ -217,6 +217,20 @@ class DQNTrainer(DQNLearner):
         self.q_values(self.net, self.env.boards, out=self.q)
         return egreedy_actions(self.q, eps, self.cfg.seed, self.steps, gid0=gid0, out=self.actions)
 
+    def policy(self, eps=0.01, seed=0x5D09):
+        """The online net's epsilon-greedy policy as `policy(boards, t) -> actions` (Philox keyed by
+        (seed, board, t); a small eps keeps a greedy policy from repeating a move that changes
+        nothing) for evaluate.play_episodes."""
+        def act(boards, t):
+            with torch.no_grad():
+                if self.use_fused:
+                    from .fused import resnet_q_forward
+                    return resnet_q_forward(boards.contiguous(), self.packed(self.net), q=False, actions=True,
+                                            eps=eps, seed=seed, ctr=t)[1]
+                q = self.q_values(self.net, boards)
+                return egreedy_actions(q, eps, seed, t)
+        return act
+
     @torch.no_grad()
     def env_step(self):
         """act + step + store: one transition per board into the ring."""
