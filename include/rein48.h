@@ -257,6 +257,24 @@ int r48_cnn_rollout(int8_t *boards, int64_t n, int32_t n_steps, const void *wfra
                     float *values, uint64_t policy_seed, int64_t gid0, uint32_t sample_ctr, uint64_t env_seed, uint32_t env_step,
                     uint32_t flags, void *stream);
 
+/* The reference's own network, fused (rein48_amd/a3c/nets.py:ActorCriticMLP = a3c.py:136-169: actor
+ * 16 -> 64 ReLU6 -> 4 ReLU, critic 16 -> 64 ReLU6 -> 1, fp32) on the VALU, one board per lane.
+ * w: float[r48_mlp_weight_floats()] packed by rein48_amd/a3c/fused.py:pack_mlp (16-byte aligned).
+ * r48_mlp_policy_forward: boards int8[n][16] -> logits float[n][4] (post-ReLU, a3c.py:153) and
+ * value float[n] (each nullable) and, when actions != NULL, the choose_action draw of
+ * r48_sample_actions (same Philox contract) into actions int8[n]. mode: R48_FEAT_VALUES/EXPONENTS.
+ * Replaces NetworkTool.get_network_output + LocalAgent.choose_action (a3c.py:89-93,136-169). */
+int32_t r48_mlp_weight_floats(void);
+int r48_mlp_policy_forward(const int8_t *boards, int64_t n, const float *w, int32_t mode, float *logits,
+                           float *value, int8_t *actions, uint64_t seed, int64_t gid0, uint32_t ctr, void *stream);
+/* The whole A3C rollout with the MLP in ONE launch: arguments, outputs and counters exactly as
+ * r48_cnn_rollout, with the policy of r48_mlp_policy_forward; values (nullable) = the critic value of
+ * every pre-step board. Equals n_steps x (r48_mlp_policy_forward + r48_env_step) bit for bit. */
+int r48_mlp_rollout(int8_t *boards, int64_t n, int32_t n_steps, const float *w, int32_t mode, int8_t *traj_boards,
+                    int8_t *actions, uint8_t *done, float *reward, int32_t *lengths, float *values,
+                    uint64_t policy_seed, int64_t gid0, uint32_t sample_ctr, uint64_t env_seed, uint32_t env_step,
+                    uint32_t flags, void *stream);
+
 /* Fused A3C update for the CNN (configs 3-4; rein48_amd/a3c/losses.py restating a3c.py:99-123):
  * the gradient of (actor + critic) over `rows` training states w.r.t. every ActorCriticCNN
  * parameter, in one pass with no activation written to memory. boards int8[rows][16], actions

@@ -104,6 +104,10 @@ SIGNATURES = {
     "r48_cnn_rollout": (C.c_int, [_P, _I64, _I32, _P, _P, _I32, _P, _P, _P, _P, _P, _P, _U64, _I64, _U32, _U64,
                                   _U32, _U32, _P]),
     "r48_cnn_policy_forward": (C.c_int, [_P, _I64, _P, _P, _I32, _P, _P, _P, _P, _U64, _I64, _U32, _P]),
+    "r48_mlp_weight_floats": (_I32, []),
+    "r48_mlp_policy_forward": (C.c_int, [_P, _I64, _P, _I32, _P, _P, _P, _U64, _I64, _U32, _P]),
+    "r48_mlp_rollout": (C.c_int, [_P, _I64, _I32, _P, _I32, _P, _P, _P, _P, _P, _P, _U64, _I64, _U32, _U64, _U32,
+                                  _U32, _P]),
     "r48_last_error": (C.c_char_p, []),
     "r48_version": (C.c_char_p, []),
 }

@@ -156,3 +156,38 @@ def cnn_forward(boards, wfrag, bias, exponents=False, logits=True, value=True, a
                                              int(ctr) & 0xFFFFFFFF,
                                              C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)))
     return lg, v, a
+
+
+# ---------------------------------------------------------------- the reference MLP (r48_mlp.hip)
+@torch.no_grad()
+def pack_mlp(net, out=None):
+    """ActorCriticMLP -> fp32 weight blob [2504] for r48_mlp_*: a1^T [16][64] | a1.b | a2 [4][64] |
+    a2.b | c1^T [16][64] | c1.b | c2 [64] | c2.b | 3 pad (unit pairs adjacent for the packed FMAs)."""
+    dev = net.a1.weight.device
+    if out is None:
+        out = torch.zeros(int(_lib.load().r48_mlp_weight_floats()), dtype=torch.float32, device=dev)
+    parts = (net.a1.weight.t(), net.a1.bias, net.a2.weight, net.a2.bias, net.c1.weight.t(), net.c1.bias,
+             net.c2.weight, net.c2.bias)
+    off = 0
+    for p in parts:
+        k = p.numel()
+        out[off:off + k].copy_(p.reshape(-1))
+        off += k
+    return out
+
+
+def mlp_forward(boards, w, exponents=False, logits=True, value=True, actions=False, seed=0, ctr=0, gid0=0):
+    """Fused fp32 MLP inference over int8 boards [n, 16] (r48_mlp_policy_forward) -> (logits [n, 4]
+    post-ReLU, value [n], actions [n]) with the unrequested ones None."""
+    if not boards.is_cuda or boards.dtype != torch.int8 or not boards.is_contiguous():
+        raise ValueError("boards must be a contiguous int8 GPU tensor")
+    n = boards.numel() // 16
+    dev = boards.device
+    lg = torch.empty((n, 4), dtype=torch.float32, device=dev) if logits else None
+    v = torch.empty(n, dtype=torch.float32, device=dev) if value else None
+    a = torch.empty(n, dtype=torch.int8, device=dev) if actions else None
+    check(_lib.load().r48_mlp_policy_forward(ptr(boards), n, ptr(w), _lib.FEAT_EXPONENTS if exponents else _lib.FEAT_VALUES,
+                                             ptr(lg), ptr(v), ptr(a), int(seed) & (2 ** 64 - 1), int(gid0),
+                                             int(ctr) & 0xFFFFFFFF,
+                                             C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)))
+    return lg, v, a

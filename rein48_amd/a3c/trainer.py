@@ -100,10 +100,13 @@ class A3CTrainer:
         fused = cfg.net == "cnn" and cfg.bf16 and cfg.fused_policy
         if fused:
             wfrag, bias = pack_cnn(self.net)   # weights are fixed for the whole rollout
-        mega = fused and cfg.fused_rollout
+        mlp_mega = self._mlp_fused() and cfg.fused_rollout
+        mega = (fused and cfg.fused_rollout) or mlp_mega
         if merge and not mega and getattr(self, "_rewards_i32", None) is None:
             self._rewards_i32 = torch.zeros((cfg.max_steps, cfg.n_boards), dtype=torch.int32, device=self.device)
-        if mega:   # every step of every board in one persistent kernel (writes fp32 rewards itself)
+        if mlp_mega:   # the reference MLP: every step of every board in one launch (r48_mlp_rollout)
+            self._rollout_megakernel(None, None, merge, mlp=True)
+        elif mega:   # every step of every board in one persistent kernel (writes fp32 rewards itself)
             self._rollout_megakernel(wfrag, bias, merge)
         elif fused:   # per step: board -> CNN -> softmax -> Philox draw in one kernel, then the env kernel
             self._rollout_fused(wfrag, bias, merge)
@@ -120,7 +123,7 @@ class A3CTrainer:
         if merge and not mega:
             self.rewards.copy_(self._rewards_i32)     # one int32 -> fp32 pass for the whole rollout
         # segment length: through the first done step, else max_steps (a3c.py:201)
-        if fused and cfg.fused_rollout:                # the megakernel wrote boards[T] and the lengths
+        if mega:                                       # the megakernel wrote boards[T] and the lengths
             self.lengths = self._lengths
             last = (self.lengths.long() - 1).view(1, -1)
             self.finished = self.done.gather(0, last)[0].bool()
@@ -164,10 +167,21 @@ class A3CTrainer:
             _lib.check(lib.r48_env_step(env._env, at, flags, d0 + t * n, None,
                                         None if r0 is None else r0 + 4 * t * n, None, stream))
 
-    def _rollout_megakernel(self, wfrag, bias, merge):
-        """r48_cnn_rollout: the T policy + env steps of every board in one launch (boards stay in
-        registers; only the trajectory rows are written), bit-identical to _rollout_fused. The
-        env's step counter then advances by T like T r48_env_step calls."""
+    def _mlp_fused(self):
+        """The reference MLP in fp32 on the GPU runs its policy through r48_mlp.hip."""
+        cfg = self.cfg
+        return cfg.net == "mlp" and not cfg.bf16 and cfg.fused_policy and self.device.type == "cuda"
+
+    def _mlp_weights(self):
+        from .fused import pack_mlp
+        self._mlp_w = pack_mlp(self.net, out=getattr(self, "_mlp_w", None))
+        return self._mlp_w
+
+    def _rollout_megakernel(self, wfrag, bias, merge, mlp=False):
+        """r48_cnn_rollout (or, mlp=True, r48_mlp_rollout with the reference network): the T policy
+        + env steps of every board in one launch (boards stay in registers; only the trajectory
+        rows are written), bit-identical to the per-step kernels. The env's step counter then
+        advances by T like T r48_env_step calls."""
         cfg, env = self.cfg, self.env
         T, n = cfg.max_steps, cfg.n_boards
         step0, resets = env.counters
@@ -180,9 +194,15 @@ class A3CTrainer:
             if getattr(self, "_v_buf", None) is None:   # row T: V(boards[T]), filled by the update
                 self._v_buf = torch.empty((T + 1, n), dtype=torch.float32, device=self.device)
             values = self._v_buf
-        _lib.check(_lib.load().r48_cnn_rollout(
-            env.boards.data_ptr(), n, T, wfrag.data_ptr(), bias.data_ptr(),
-            _lib.FEAT_EXPONENTS if cfg.features == "exponents" else _lib.FEAT_VALUES,
+        lib = _lib.load()
+        mode = _lib.FEAT_EXPONENTS if cfg.features == "exponents" else _lib.FEAT_VALUES
+        if mlp:
+            call = lambda *rest: lib.r48_mlp_rollout(env.boards.data_ptr(), n, T, self._mlp_weights().data_ptr(),  # noqa: E731
+                                                     mode, *rest)
+        else:
+            call = lambda *rest: lib.r48_cnn_rollout(env.boards.data_ptr(), n, T, wfrag.data_ptr(),  # noqa: E731
+                                                     bias.data_ptr(), mode, *rest)
+        _lib.check(call(
             self.boards.data_ptr(), self.actions.data_ptr(), self.done.data_ptr(),
             self.rewards.data_ptr() if merge else None, self._lengths.data_ptr(),
             None if values is None else values.data_ptr(), int(cfg.seed) & (2 ** 64 - 1), self.gid0,
@@ -209,6 +229,11 @@ class A3CTrainer:
                 wfrag, bias = pack_cnn(self.net)
                 value = lambda b: cnn_forward(b.reshape(-1, 16), wfrag, bias, exponents=cfg.features == "exponents",
                                               logits=False, value=True)[1]
+            elif self._mlp_fused():   # the reference MLP: one fp32 VALU launch (r48_mlp_policy_forward)
+                from .fused import mlp_forward
+                w = self._mlp_weights()
+                value = lambda b: mlp_forward(b.reshape(-1, 16).contiguous(), w,  # noqa: E731
+                                              exponents=cfg.features == "exponents", logits=False, value=True)[1]
             else:
                 value = lambda b: self._net(self._features(b))[1]
             # the fused textbook update computes td = target - V(s) in-kernel and needs no
@@ -224,8 +249,9 @@ class A3CTrainer:
                 v_all = rv[0][1:T + 1]
             elif need_values:
                 v_all = torch.empty((T, n), dtype=torch.float32, device=self.device)
-                for t0 in range(0, T, T if fused else cfg.update_chunk):
-                    t1 = min(T, t0 + (T if fused else cfg.update_chunk))
+                ch = T if (fused or self._mlp_fused()) else cfg.update_chunk   # no activations kept
+                for t0 in range(0, T, ch):
+                    t1 = min(T, t0 + ch)
                     v_all[t0:t1] = value(states[t0:t1].contiguous()).view(t1 - t0, n)
             # last post-step state of each segment = boards[len]
             idx = self.lengths.long().view(1, n, 1).expand(1, n, 16)
@@ -305,6 +331,11 @@ class A3CTrainer:
             wfrag, bias = pack_cnn(self.net)
             return lambda boards, t: cnn_forward(boards, wfrag, bias, exponents=exps, logits=False, value=False,
                                                  actions=True, seed=seed, ctr=t)[2]
+        if self._mlp_fused():
+            from .fused import mlp_forward, pack_mlp
+            w = pack_mlp(self.net)
+            return lambda boards, t: mlp_forward(boards, w, exponents=exps, logits=False, value=False, actions=True,
+                                                 seed=seed, ctr=t)[2]
 
         def act(boards, t):
             with torch.no_grad():

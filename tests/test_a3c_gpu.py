@@ -470,3 +470,84 @@ def test_segment_stats_and_row_weights_match_tensor_forms():
     wn, cm = K.row_weights(lengths, got["B"], T, got["td_sum"])
     assert torch.equal(wn, m / got["B"][None, :] / n)
     assert torch.equal(cm, (got["td_sum"] / (4.0 * got["B"] * got["B"]))[None, :] * m / n)
+
+
+# ---------------------------------------------------------------- the reference MLP, fused (r48_mlp.hip)
+def _mlp_net(seed=3):
+    from rein48_amd.a3c.nets import ActorCriticMLP
+    torch.manual_seed(seed)
+    net = ActorCriticMLP().to(DEV)
+    with torch.no_grad():                     # nonzero biases (TF's are zero at init; training moves them)
+        for m in (net.a1, net.a2, net.c1, net.c2):
+            m.bias.uniform_(-0.5, 0.5)
+    return net
+
+
+@pytest.mark.parametrize("exponents", [False, True])
+def test_fused_mlp_forward_matches_torch_and_oracle(exponents):
+    """r48_mlp_policy_forward (fp32 VALU, one board per lane) vs the reference network in PyTorch fp32
+    and in the float64 oracle (oracle/a3c_ref.py, a3c.py:136-169): logits (post-ReLU) and value
+    within 2e-5 of the float64 values relative to their scale (fp32 sums in another order), and its
+    draw equals r48_sample_actions on its own logits bit for bit."""
+    from oracle import a3c_ref as R
+    from rein48_amd.a3c import kernels as K
+    from rein48_amd.a3c.fused import mlp_forward, pack_mlp
+    net = _mlp_net()
+    rng = np.random.default_rng(4)
+    n = 70_001
+    b = rng.integers(1, 12, size=(n, 16)).astype(np.int8)
+    b[rng.random((n, 16)) < 0.4] = 0
+    boards = torch.from_numpy(b).to(DEV)
+    w = pack_mlp(net)
+    lg, v, a = mlp_forward(boards, w, exponents=exponents, actions=True, seed=17, ctr=5, gid0=9)
+    x = K.board_features(boards, exponents=exponents)
+    with torch.no_grad():
+        tl, tv = net(x)
+    P, xd = net.reference_params(), x.double().cpu().numpy()
+    logits64 = np.maximum(R.relu6(xd @ P["a_w1"] + P["a_b1"]) @ P["a_w2"] + P["a_b2"], 0.0)   # a3c.py:150-154
+    _, v64 = R.net_forward(P, xd)
+    for got, t32, w64 in ((lg, tl, logits64), (v, tv, v64)):
+        w64 = torch.from_numpy(np.asarray(w64)).to(DEV).reshape(got.shape)
+        scale = float(w64.abs().max()) + 1.0
+        assert float((got.double() - w64).abs().max()) <= 2e-5 * scale
+        assert float((t32.double() - w64).abs().max()) <= 2e-5 * scale
+    act, _, _ = K.sample_actions(lg, 17, 5, gid0=9)
+    assert torch.equal(a, act)
+
+
+@pytest.mark.parametrize("mode,n", [("textbook", 5003), ("reference", 4099), ("textbook", (1 << 20) + 3)])
+def test_mlp_rollout_megakernel_equals_per_step_kernels(mode, n):
+    """r48_mlp_rollout (all T steps of every board in one launch) == T x (r48_mlp_policy_forward +
+    r48_env_step) bit for bit: trajectory boards, actions, done, merge rewards, values, lengths and
+    the final boards; also at the bench's 2^20 + 3 boards."""
+    from rein48_amd import VecGame
+    from rein48_amd.a3c import A3CConfig, A3CTrainer
+    from rein48_amd.a3c.fused import mlp_forward
+    T = 40
+    cfg = A3CConfig(n_boards=n, max_steps=T, mode=mode, net="mlp", bf16=False, features="values", seed=7)
+    tr = A3CTrainer(cfg, device=DEV)
+    with torch.no_grad():
+        for m in (tr.net.a1, tr.net.a2, tr.net.c1, tr.net.c2):
+            m.bias.uniform_(-0.5, 0.5)
+    before, ctr0 = tr.env.counters, tr.sample_ctr
+    tr.rollout()
+    w = tr._mlp_weights()
+    env = VecGame(n, device=DEV, seed=cfg.seed)
+    env.counters = before
+    env.reset()
+    merge = mode == "textbook"
+    assert torch.equal(env.boards, tr.boards[0])
+    for t in range(T):
+        _, v, a = mlp_forward(env.boards, w, logits=False, value=True, actions=True, seed=cfg.seed, ctr=ctr0 + t)
+        assert torch.equal(a, tr.actions[t]), t
+        if mode == "reference":
+            assert torch.equal(v, tr._rollout_v[0][t]), t
+        _, rew, d = env.step(a, merge_reward=merge)
+        assert torch.equal(env.boards, tr.boards[t + 1]), t
+        assert torch.equal(d, tr.done[t]), t
+        if merge:
+            assert torch.equal(rew.float(), tr.rewards[t]), t
+    first = torch.where(tr.done.bool().any(0), tr.done.float().argmax(0) + 1, torch.full_like(tr.lengths, T))
+    assert torch.equal(tr.lengths.long(), first.long())
+    out = tr.update()
+    assert all(np.isfinite(out[k]) for k in ("actor_loss", "critic_loss"))
