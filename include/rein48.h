@@ -275,6 +275,18 @@ int r48_mlp_rollout(int8_t *boards, int64_t n, int32_t n_steps, const float *w, 
                     uint64_t policy_seed, int64_t gid0, uint32_t sample_ctr, uint64_t env_seed, uint32_t env_step,
                     uint32_t flags, void *stream);
 
+/* Fused A3C update for the reference MLP (fp32; the per-row loss of r48_cnn_train_grad below, here
+ * through the logits' ReLU): arguments as r48_cnn_train_grad with the MLP weight blob w of
+ * r48_mlp_policy_forward; grad float[2504] (16-byte aligned) receives the gradient in FlatParams
+ * order (a1.w [64][16] | a1.b | a2.w [4][64] | a2.b | c1.w | c1.b | c2.w | c2.b = 2,501 floats),
+ * then the actor and critic losses. workspace: r48_mlp_train_workspace_floats() floats.
+ * Deterministic (fixed-order reduction). Replaces NetworkTool.get_loss_value + compute_gradients
+ * (a3c.py:99-123, 73-80). */
+int64_t r48_mlp_train_workspace_floats(void);
+int r48_mlp_train_grad(const int8_t *boards, int64_t rows, int64_t n_boards, const int8_t *actions,
+                       const float *targets, const float *wn, const float *cm, const float *counts, float beta,
+                       int32_t mode, const float *w, float *workspace, float *grad, void *stream);
+
 /* Fused A3C update for the CNN (configs 3-4; rein48_amd/a3c/losses.py restating a3c.py:99-123):
  * the gradient of (actor + critic) over `rows` training states w.r.t. every ActorCriticCNN
  * parameter, in one pass with no activation written to memory. boards int8[rows][16], actions

@@ -108,6 +108,8 @@ SIGNATURES = {
     "r48_mlp_policy_forward": (C.c_int, [_P, _I64, _P, _I32, _P, _P, _P, _U64, _I64, _U32, _P]),
     "r48_mlp_rollout": (C.c_int, [_P, _I64, _I32, _P, _I32, _P, _P, _P, _P, _P, _P, _U64, _I64, _U32, _U64, _U32,
                                   _U32, _P]),
+    "r48_mlp_train_workspace_floats": (_I64, []),
+    "r48_mlp_train_grad": (C.c_int, [_P, _I64, _I64, _P, _P, _P, _P, _P, C.c_float, _I32, _P, _P, _P, _P]),
     "r48_last_error": (C.c_char_p, []),
     "r48_version": (C.c_char_p, []),
 }

@@ -161,13 +161,15 @@ def cnn_forward(boards, wfrag, bias, exponents=False, logits=True, value=True, a
 # ---------------------------------------------------------------- the reference MLP (r48_mlp.hip)
 @torch.no_grad()
 def pack_mlp(net, out=None):
-    """ActorCriticMLP -> fp32 weight blob [2504] for r48_mlp_*: a1^T [16][64] | a1.b | a2 [4][64] |
-    a2.b | c1^T [16][64] | c1.b | c2 [64] | c2.b | 3 pad (unit pairs adjacent for the packed FMAs)."""
+    """ActorCriticMLP -> fp32 weight blob [2504] for r48_mlp_*, grouped by hidden-unit pair p (units
+    2p, 2p + 1): a1 [32][16 in][2] | a1.b | a2 [32][4 out][2] | a2.b | c1 [32][16 in][2] | c1.b |
+    c2 [64] | c2.b | 3 pad."""
     dev = net.a1.weight.device
     if out is None:
         out = torch.zeros(int(_lib.load().r48_mlp_weight_floats()), dtype=torch.float32, device=dev)
-    parts = (net.a1.weight.t(), net.a1.bias, net.a2.weight, net.a2.bias, net.c1.weight.t(), net.c1.bias,
-             net.c2.weight, net.c2.bias)
+    by_pair = lambda w: w.reshape(32, 2, -1).permute(0, 2, 1)                # [64, in] -> [32, in, 2]  # noqa: E731
+    parts = (by_pair(net.a1.weight), net.a1.bias, by_pair(net.a2.weight.t()), net.a2.bias, by_pair(net.c1.weight),
+             net.c1.bias, net.c2.weight, net.c2.bias)
     off = 0
     for p in parts:
         k = p.numel()
@@ -191,3 +193,30 @@ def mlp_forward(boards, w, exponents=False, logits=True, value=True, actions=Fal
                                              int(ctr) & 0xFFFFFFFF,
                                              C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)))
     return lg, v, a
+
+
+MLP_GRAD_FLOATS = 2501   # r48_mlp_train_grad's gradient (FlatParams order), then actor + critic loss
+
+
+def mlp_train_grad(net, boards, actions, targets, wn, cm=None, counts=None, beta=0.001, exponents=False,
+                   n_boards=None, w=None, workspace=None):
+    """r48_mlp_train_grad: the A3C loss gradient (losses.chunk_loss's per-row weights wn / cm /
+    counts, as cnn_train_grad) of every ActorCriticMLP parameter over `rows` training states in one
+    fp32 pass -> (flat gradient [2501] in parameters() order, actor loss, critic loss) as device
+    tensors (0-d for the losses)."""
+    rows = boards.numel() // 16
+    dev = boards.device
+    for t, name in ((boards, "boards"), (actions, "actions"), (targets, "targets"), (wn, "wn")):
+        if not t.is_cuda or not t.is_contiguous():
+            raise ValueError("%s must be a contiguous GPU tensor" % name)
+    if w is None:
+        w = pack_mlp(net)
+    L = _lib.load()
+    if workspace is None:
+        workspace = torch.empty(int(L.r48_mlp_train_workspace_floats()), dtype=torch.float32, device=dev)
+    out = torch.empty(2504, dtype=torch.float32, device=dev)
+    check(L.r48_mlp_train_grad(ptr(boards), rows, int(n_boards or rows), ptr(actions), ptr(targets), ptr(wn), ptr(cm),
+                               ptr(counts), float(beta), _lib.FEAT_EXPONENTS if exponents else _lib.FEAT_VALUES,
+                               ptr(w), ptr(workspace), ptr(out),
+                               C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)))
+    return out[:MLP_GRAD_FLOATS], out[MLP_GRAD_FLOATS], out[MLP_GRAD_FLOATS + 1]

@@ -238,7 +238,8 @@ class A3CTrainer:
                 value = lambda b: self._net(self._features(b))[1]
             # the fused textbook update computes td = target - V(s) in-kernel and needs no
             # per-segment td_sum, so only the reference loss (or the unfused path) pays this pass
-            need_values = not (fused and cfg.fused_update and cfg.mode == "textbook")
+            fused_upd = cfg.fused_update and (fused or self._mlp_fused())
+            need_values = not (fused_upd and cfg.mode == "textbook")
             v_all = None
             rv = self._rollout_v
             if need_values and rv is not None and rv[1] == self.updates and cfg.mode == "reference":
@@ -266,8 +267,9 @@ class A3CTrainer:
                 stats = segment_stats(v_all, targets, self.actions, self.mask)
             else:
                 stats = {"B": self.mask.float().sum(0).clamp(min=1.0)}
-        if fused and cfg.fused_update:
-            # pass 2 as ONE fused MFMA kernel over all T x n states (no activation hits HBM)
+        if fused_upd:
+            # pass 2 as ONE fused kernel over all T x n states (no activation hits HBM): MFMA for the
+            # CNN (r48_a3c_train.hip), fp32 VALU for the reference MLP (r48_mlp.hip)
             actor_total, critic_total = self._fused_gradient(states, targets, stats)
             self.flat.allreduce_grad(self.group)
             self.opt.step()
@@ -305,6 +307,17 @@ class A3CTrainer:
         wn, cm = K.row_weights(self.lengths, stats["B"].contiguous(), cfg.max_steps,
                                stats["td_sum"].contiguous() if ref else None)
         counts = stats["counts"].float().contiguous() if ref else None
+        if self._mlp_fused():
+            from .fused import mlp_train_grad
+            if getattr(self, "_mlp_ws", None) is None:
+                self._mlp_ws = torch.empty(int(_lib.load().r48_mlp_train_workspace_floats()), dtype=torch.float32,
+                                           device=self.device)
+            g, actor, critic = mlp_train_grad(
+                self.net, states.reshape(-1, 16), self.actions.reshape(-1), targets.reshape(-1).contiguous(),
+                wn.view(-1), None if cm is None else cm.view(-1), counts, beta=cfg.beta,
+                exponents=cfg.features == "exponents", n_boards=n, w=self._mlp_weights(), workspace=self._mlp_ws)
+            self.flat.grad.copy_(g)
+            return float(actor), float(critic)
         if getattr(self, "_train_ws", None) is None:
             self._train_ws = torch.empty(_lib_workspace_floats(), dtype=torch.float32, device=self.device)
         grads, actor, critic = cnn_train_grad(

@@ -15,9 +15,12 @@
 //                 GameClient.py:40-51, the r48_env_step Philox contract) -- and writes only the
 //                 trajectory rows; bit-identical to T x (k_mlp_forward + r48_env_step)
 //
-// Weight blob (rein48_amd/a3c/fused.py pack_mlp, 2,504 floats): a1^T [16][64] | a1.b [64] |
-// a2 [4][64] | a2.b [4] | c1^T [16][64] | c1.b [64] | c2 [64] | c2.b [1] | pad -- unit pairs
-// (j, j + 1) adjacent for every input, so one SGPR pair feeds one packed FMA.
+// Weight blob (rein48_amd/a3c/fused.py pack_mlp, 2,504 floats), grouped by hidden-unit PAIR p
+// (units 2p, 2p + 1): a1 [32 p][16 in][2] | a1.b [64] | a2 [32 p][4 out][2] | a2.b [4] |
+// c1 [32 p][16 in][2] | c1.b [64] | c2 [64] | c2.b [1] | pad -- one pair's weights are contiguous
+// (s_load_dwordx16 twice for its 32 layer-1 weights) and every SGPR pair feeds one packed FMA. The
+// pair loop is NOT unrolled: the scalar loads then stay next to their use instead of being
+// scheduled together (2,500 weights do not fit the SGPRs; they spilled into VGPR lanes).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -74,16 +77,16 @@ __device__ __forceinline__ void hidden_into(const float *__restrict__ w, int w1,
 #pragma unroll
     for (int k = 0; k < NO; k++)
         acc[k] = f32x2{0.0f, 0.0f};
-#pragma unroll
-    for (int j = 0; j < 64; j += 2) {
-        f32x2 a = pair_at(w, b1 + j);
+#pragma unroll 1
+    for (int p = 0; p < 32; p++) {
+        f32x2 a = pair_at(w, b1 + 2 * p);
 #pragma unroll
         for (int f = 0; f < 16; f++)
-            a = __builtin_elementwise_fma(pair_at(w, w1 + 64 * f + j), f32x2{x[f], x[f]}, a);
+            a = __builtin_elementwise_fma(pair_at(w, w1 + 32 * p + 2 * f), f32x2{x[f], x[f]}, a);
         const f32x2 h = f32x2{relu6(a.x), relu6(a.y)};
 #pragma unroll
         for (int k = 0; k < NO; k++)
-            acc[k] = __builtin_elementwise_fma(pair_at(w, w2 + 64 * k + j), h, acc[k]);
+            acc[k] = __builtin_elementwise_fma(pair_at(w, w2 + (NO == 1 ? 2 * p : 8 * p + 2 * k)), h, acc[k]);
     }
 }
 
@@ -194,6 +197,251 @@ __global__ __launch_bounds__(kBlock) void k_mlp_rollout(int8_t *__restrict__ boa
         lengths[i] = len;
 }
 
+// ---------------------------------------------------------------- fused update
+// k_mlp_train: the gradient of the A3C loss (rein48_amd/a3c/losses.py restating a3c.py:99-123,
+// textbook or the reference's broadcast actor loss; the per-row formulas of r48_a3c_train.hip's
+// k_cnn_train) w.r.t. all 2,501 parameters, fp32, in ONE pass over the training states.
+// A wave takes 64 rows per tile in two phases:
+//   phase 1, lane = row: the forward of mlp_forward (SGPR weights, packed FMAs), softmax / entropy
+//     / td, the row's output gradient dz (through the logits' ReLU) and dv; the row's inputs x and
+//     (dz, dv) go to the wave's LDS stash (24 floats per row)
+//   phase 2, lane = hidden unit l (actor unit l and critic unit l): for each of the 64 rows (LDS
+//     broadcast reads) recompute a_l, c_l (the same FMA sequence as phase 1, so the same values),
+//     then dh_l = [0 < a_l < 6] sum_k W2[k][l] dz_k, dhc_l = [0 < c_l < 6] wc2[l] dv, and
+//     accumulate the unit's gradient row in registers: dW1[l][:] += dh_l x, db1, dW2[:][l] += dz h_l,
+//     dWc1[l][:], dbc1, dwc2[l]
+// so the weight gradients (contractions over rows) never cross lanes. Per wave one record of the
+// flat gradient in FlatParams order (a1.w [64][16] | a1.b | a2.w [4][64] | a2.b | c1.w | c1.b |
+// c2.w | c2.b) + the two losses; k_mlp_reduce sums the records in a fixed order (deterministic).
+constexpr int kTrainWaves = 4;
+constexpr int kStash = 24;                 // x[16] | dz[4] | dv | pad
+constexpr int kRec = 2504;                 // 2,501 gradient floats + actor loss + critic loss + pad
+constexpr int kRecLossA = 2501, kRecLossC = 2502;
+// (the record's section offsets equal the blob's, kA1W .. kC2B; inside a1 / a2 / c1 the record has
+// the parameters' own [out][in] order)
+constexpr float kEntropyEps = 1e-5f;       // a3c.py:114
+constexpr float kLn2 = 0.69314718055994531f;
+
+__device__ __forceinline__ void wave_lds_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ float wave_sum(float v)
+{
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1)
+        v += __shfl_xor(v, m);
+    return v;
+}
+
+template <int MODE, bool REF>
+__global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_eu(3))) void k_mlp_train(
+    const int8_t *__restrict__ boards, int64_t rows, int64_t n_boards, const int8_t *__restrict__ actions,
+    const float *__restrict__ targets, const float *__restrict__ wn, const float *__restrict__ cm,
+    const float *__restrict__ counts, float beta, const float *__restrict__ w, float *__restrict__ partials)
+{
+    __shared__ float stash[kTrainWaves][64][kStash];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    float(*st)[kStash] = stash[wave];
+    // phase-2 weights of unit l = lane (actor and critic), and its gradient accumulators
+    float w1l[16], wc1l[16], w2l[4];
+    const int pl = 32 * (lane >> 1) + (lane & 1);      // unit l's place in its pair's layer-1 block
+#pragma unroll
+    for (int f = 0; f < 16; f++) {
+        w1l[f] = w[kA1W + pl + 2 * f];
+        wc1l[f] = w[kC1W + pl + 2 * f];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+        w2l[k] = w[kA2W + 8 * (lane >> 1) + 2 * k + (lane & 1)];
+    const float b1l = w[kA1B + lane], bc1l = w[kC1B + lane], wc2l = w[kC2W + lane];
+    float g1[16], gc1[16], g2[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int f = 0; f < 16; f++)
+        g1[f] = gc1[f] = 0.f;
+    float gb1 = 0.f, gbc1 = 0.f, gc2 = 0.f;
+    // per-row-lane sums (reduced over the wave at the end)
+    float gb2[4] = {0.f, 0.f, 0.f, 0.f}, gbc2 = 0.f, loss_a = 0.f, loss_c = 0.f;
+
+    const int64_t n_tiles = (rows + 63) / 64;
+    const int64_t stride = (int64_t)gridDim.x * kTrainWaves;
+    for (int64_t tile = (int64_t)blockIdx.x * kTrainWaves + wave; tile < n_tiles; tile += stride) {
+        // ---------------- phase 1: lane = row
+        const int64_t r = tile * 64 + lane;
+        const bool live = r < rows;
+        const int64_t rr = live ? r : rows - 1;      // padding lanes: a valid row with weight 0
+        float x[16], zr[4], v;
+        board_inputs<MODE>(load_board(boards, rr), x);
+        {
+            const float *wp = w;
+            f32x2 acc[4];
+            hidden_into<4>(wp, kA1W, kA1B, kA2W, x, acc);
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                zr[k] = wp[kA2B + k] + (acc[k].x + acc[k].y);      // pre-ReLU
+            f32x2 c[1];
+            hidden_into<1>(wp, kC1W, kC1B, kC2W, x, c);
+            v = wp[kC2B] + (c[0].x + c[0].y);
+        }
+        const float wt = live ? wn[rr] : 0.0f;
+        const float tgt = targets[rr];
+        const int a = actions[rr] & 3;
+        float z[4], p[4], gr[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            z[k] = fmaxf(zr[k], 0.0f);                            // the logits' ReLU (a3c.py:153)
+        const float m = fmaxf(fmaxf(z[0], z[1]), fmaxf(z[2], z[3]));
+        float se = 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            p[k] = __expf(z[k] - m);
+            se += p[k];
+        }
+        const float inv = __builtin_amdgcn_rcpf(se), lse = m + kLn2 * __builtin_amdgcn_logf(se);
+        float H = 0.f, gbar = 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            p[k] *= inv;
+            const float lq = kLn2 * __builtin_amdgcn_logf(p[k] + kEntropyEps);
+            H -= p[k] * lq;
+            gr[k] = -(lq + p[k] * __builtin_amdgcn_rcpf(p[k] + kEntropyEps));   // dH/dp_k
+            gbar += p[k] * gr[k];
+        }
+        const float td = tgt - v;
+        float dz[4];
+        if (REF) {   // reference: -beta wn H - cm sum_k c_k log p_k  (losses.py, a3c.py:110-116)
+            const float c = live ? cm[rr] : 0.0f;
+            const int64_t bidx = rows <= 0xFFFFFFFFll ? (int64_t)((uint32_t)rr % (uint32_t)n_boards) : rr % n_boards;
+            const float4 cnt = *reinterpret_cast<const float4 *>(counts + 4 * bidx);
+            const float ck[4] = {cnt.x, cnt.y, cnt.z, cnt.w}, C = cnt.x + cnt.y + cnt.z + cnt.w;
+            float sa = 0.f;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                dz[k] = -beta * wt * p[k] * (gr[k] - gbar) - c * (ck[k] - p[k] * C);
+                sa += ck[k] * (z[k] - lse);
+            }
+            loss_a += -beta * wt * H - c * sa;
+        } else {     // textbook: -wn (beta H + td log p[a]), td constant for the actor
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                dz[k] = -wt * (beta * p[k] * (gr[k] - gbar) + td * ((k == a ? 1.0f : 0.0f) - p[k]));
+            loss_a += -wt * (beta * H + td * (z[a] - lse));
+        }
+        const float dv = -2.0f * wt * td;                          // critic = wn td^2
+        loss_c += wt * td * td;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            dz[k] = zr[k] > 0.0f ? dz[k] : 0.0f;                   // through the logits' ReLU
+            gb2[k] += dz[k];
+        }
+        gbc2 += dv;
+        wave_lds_sync();   // the previous tile's phase 2 has read the stash
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            *reinterpret_cast<float4 *>(&st[lane][4 * q]) = make_float4(x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]);
+        *reinterpret_cast<float4 *>(&st[lane][16]) = make_float4(dz[0], dz[1], dz[2], dz[3]);
+        st[lane][20] = dv;
+        wave_lds_sync();
+        // ---------------- phase 2: lane = hidden unit
+#pragma unroll 1
+        for (int j = 0; j < 64; j++) {
+            float xr[16];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const float4 t4 = *reinterpret_cast<const float4 *>(&st[j][4 * q]);
+                xr[4 * q] = t4.x, xr[4 * q + 1] = t4.y, xr[4 * q + 2] = t4.z, xr[4 * q + 3] = t4.w;
+            }
+            const float4 dz4 = *reinterpret_cast<const float4 *>(&st[j][16]);
+            const float dvr = st[j][20];
+            float al = b1l, cl = bc1l;   // the FMA sequence of phase 1 (hidden_into), so the same values
+#pragma unroll
+            for (int f = 0; f < 16; f++) {
+                al = __builtin_fmaf(w1l[f], xr[f], al);
+                cl = __builtin_fmaf(wc1l[f], xr[f], cl);
+            }
+            const float hl = relu6(al), hcl = relu6(cl);
+            const float dh = (al > 0.0f && al < 6.0f) ? w2l[0] * dz4.x + w2l[1] * dz4.y + w2l[2] * dz4.z + w2l[3] * dz4.w
+                                                      : 0.0f;
+            const float dhc = (cl > 0.0f && cl < 6.0f) ? wc2l * dvr : 0.0f;
+#pragma unroll
+            for (int f = 0; f < 16; f++) {
+                g1[f] = __builtin_fmaf(dh, xr[f], g1[f]);
+                gc1[f] = __builtin_fmaf(dhc, xr[f], gc1[f]);
+            }
+            gb1 += dh;
+            gbc1 += dhc;
+            g2[0] = __builtin_fmaf(dz4.x, hl, g2[0]);
+            g2[1] = __builtin_fmaf(dz4.y, hl, g2[1]);
+            g2[2] = __builtin_fmaf(dz4.z, hl, g2[2]);
+            g2[3] = __builtin_fmaf(dz4.w, hl, g2[3]);
+            gc2 = __builtin_fmaf(dvr, hcl, gc2);
+        }
+    }
+    // ---------------- this wave's record (FlatParams order)
+    float *rec = partials + ((int64_t)blockIdx.x * kTrainWaves + wave) * kRec;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        *reinterpret_cast<float4 *>(rec + kA1W + 16 * lane + 4 * q) = make_float4(g1[4 * q], g1[4 * q + 1], g1[4 * q + 2], g1[4 * q + 3]);
+        *reinterpret_cast<float4 *>(rec + kC1W + 16 * lane + 4 * q) =
+            make_float4(gc1[4 * q], gc1[4 * q + 1], gc1[4 * q + 2], gc1[4 * q + 3]);
+    }
+    rec[kA1B + lane] = gb1;
+    rec[kC1B + lane] = gbc1;
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+        rec[kA2W + 64 * k + lane] = g2[k];
+    rec[kC2W + lane] = gc2;
+    const float s0 = wave_sum(gb2[0]), s1 = wave_sum(gb2[1]), s2 = wave_sum(gb2[2]), s3 = wave_sum(gb2[3]);
+    const float sc = wave_sum(gbc2), la = wave_sum(loss_a), lc = wave_sum(loss_c);
+    if (lane == 0) {
+        *reinterpret_cast<float4 *>(rec + kA2B) = make_float4(s0, s1, s2, s3);
+        rec[kC2B] = sc;
+        rec[kRecLossA] = la;
+        rec[kRecLossC] = lc;
+        rec[kRec - 1] = 0.0f;
+    }
+}
+
+// fixed-order sum of `n_rec` records of kRec floats into out[kRec]: pass 1 sums groups of kRedGroup
+// records (one thread per (group, float4)), pass 2 the group sums
+constexpr int kRedGroup = 64;
+
+__global__ __launch_bounds__(256) void k_mlp_reduce1(const float4 *__restrict__ rec, int n_rec, float4 *__restrict__ groups)
+{
+    constexpr int q = kRec / 4;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int n_grp = (n_rec + kRedGroup - 1) / kRedGroup;
+    if (i >= q * n_grp)
+        return;
+    const int g = i / q, e = i % q;
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int r = g * kRedGroup; r < n_rec && r < (g + 1) * kRedGroup; r++) {
+        const float4 v = rec[(int64_t)r * q + e];
+        s.x += v.x, s.y += v.y, s.z += v.z, s.w += v.w;
+    }
+    groups[(int64_t)g * q + e] = s;
+}
+
+__global__ __launch_bounds__(256) void k_mlp_reduce2(const float4 *__restrict__ groups, int n_grp, float4 *__restrict__ out)
+{
+    constexpr int q = kRec / 4;
+    const int e = blockIdx.x * 256 + threadIdx.x;
+    if (e >= q)
+        return;
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int g = 0; g < n_grp; g++) {
+        const float4 v = groups[(int64_t)g * q + e];
+        s.x += v.x, s.y += v.y, s.z += v.z, s.w += v.w;
+    }
+    out[e] = s;
+}
+
+constexpr int kTrainGroups = 1024;   // persistent grid: 4 workgroups of 4 waves per CU on 256 CUs
+
 int fail(int code, const std::string &msg)
 {
     r48::set_last_error(msg);
@@ -260,6 +508,42 @@ int r48_mlp_rollout(int8_t *boards, int64_t n, int32_t n_steps, const float *w, 
         R48_MLP_GO(R48_FEAT_EXPONENTS);
 #undef R48_MLP_GO
     return launched("k_mlp_rollout");
+}
+
+/* workspace floats of r48_mlp_train_grad: the per-wave records + the first reduction pass's groups */
+int64_t r48_mlp_train_workspace_floats(void)
+{
+    const int64_t recs = (int64_t)kTrainGroups * kTrainWaves;
+    return (recs + (recs + kRedGroup - 1) / kRedGroup) * kRec;
+}
+
+int r48_mlp_train_grad(const int8_t *boards, int64_t rows, int64_t n_boards, const int8_t *actions,
+                       const float *targets, const float *wn, const float *cm, const float *counts, float beta,
+                       int32_t mode, const float *w, float *workspace, float *grad, void *stream)
+{
+    if (!boards || !actions || !targets || !wn || !w || !workspace || !grad || rows < 1 || n_boards < 1 ||
+        (mode != R48_FEAT_VALUES && mode != R48_FEAT_EXPONENTS) || (cm && !counts))
+        return fail(R48_EINVAL, "r48_mlp_train_grad: NULL argument, rows/n_boards < 1, bad mode, or cm without counts");
+    if ((reinterpret_cast<uintptr_t>(boards) | reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(counts) |
+         reinterpret_cast<uintptr_t>(workspace) | reinterpret_cast<uintptr_t>(grad)) & 15u)
+        return fail(R48_EINVAL, "r48_mlp_train_grad: boards, w, counts, workspace and grad must be 16-byte aligned");
+    const int n_rec = kTrainGroups * kTrainWaves, n_grp = (n_rec + kRedGroup - 1) / kRedGroup;
+    hipStream_t s = (hipStream_t)stream;
+    auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(kTrainGroups), dim3(64 * kTrainWaves), 0, s, boards, rows, n_boards, actions,
+                           targets, wn, cm, counts, beta, w, workspace);
+    };
+    if (mode == R48_FEAT_VALUES)
+        cm ? go(k_mlp_train<R48_FEAT_VALUES, true>) : go(k_mlp_train<R48_FEAT_VALUES, false>);
+    else
+        cm ? go(k_mlp_train<R48_FEAT_EXPONENTS, true>) : go(k_mlp_train<R48_FEAT_EXPONENTS, false>);
+    float4 *groups = reinterpret_cast<float4 *>(workspace + (int64_t)n_rec * kRec);
+    constexpr int q = kRec / 4;
+    hipLaunchKernelGGL(k_mlp_reduce1, dim3((q * n_grp + 255) / 256), dim3(256), 0, s, (const float4 *)workspace, n_rec,
+                       groups);
+    hipLaunchKernelGGL(k_mlp_reduce2, dim3((q + 255) / 256), dim3(256), 0, s, (const float4 *)groups, n_grp,
+                       (float4 *)grad);
+    return launched("k_mlp_train");
 }
 
 }  // extern "C"

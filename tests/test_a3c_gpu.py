@@ -5,6 +5,8 @@ action given the same uniform, away from cdf ties), reverse discounted scan (bot
 TF1 RMSProp (fp32 vs f64). Trainer: one reference-mode update's losses equal the oracle's
 per-segment literal losses on the same trajectory; textbook/CNN/bf16 modes run and learn.
 """
+import copy
+
 import numpy as np
 import pytest
 import torch
@@ -551,3 +553,82 @@ def test_mlp_rollout_megakernel_equals_per_step_kernels(mode, n):
     assert torch.equal(tr.lengths.long(), first.long())
     out = tr.update()
     assert all(np.isfinite(out[k]) for k in ("actor_loss", "critic_loss"))
+
+
+@pytest.mark.parametrize("T,n", [(3, 10_007), (4, 262_154)])      # 30,021 rows; 2^20 + 40 rows (>= 4 tiles per wave)
+@pytest.mark.parametrize("mode", ["textbook", "reference"])
+def test_fused_mlp_update_gradients_match_torch(mode, T, n):
+    """r48_mlp_train_grad (fp32, one pass: forward + loss + backward, weight gradients accumulated per
+    hidden unit) vs PyTorch autograd of the trainer's own loss (losses.chunk_loss) on the reference
+    network in float64: per parameter tensor the max error relative to the tensor's scale is within
+    2x (+1e-5) of PyTorch's own fp32 autograd error; the losses agree to 1e-5."""
+    from rein48_amd.a3c import kernels as K
+    from rein48_amd.a3c.fused import mlp_train_grad
+    from rein48_amd.a3c.losses import chunk_loss, segment_stats
+    net = _mlp_net(11)
+    rng = np.random.default_rng(8)
+    b = rng.integers(1, 10, size=(T, n, 16)).astype(np.int8)
+    b[rng.random((T, n, 16)) < 0.4] = 0
+    boards = torch.from_numpy(b).to(DEV)
+    actions = torch.from_numpy(rng.integers(0, 4, size=(T, n)).astype(np.int8)).to(DEV)
+    targets = torch.from_numpy(rng.normal(scale=2.0, size=(T, n)).astype(np.float32)).to(DEV)
+    lengths = torch.from_numpy(rng.integers(1, T + 1, size=n)).to(DEV)
+    mask = (torch.arange(T, device=DEV)[:, None] < lengths[None, :])
+    x = K.board_features(boards.view(-1, 16), exponents=False)
+    with torch.no_grad():
+        _, v = net(x)
+    stats = segment_stats(v.view(T, n), targets, actions, mask)
+
+    def torch_grads(dt):
+        import torch.nn.functional as F
+        m = copy.deepcopy(net).to(dt)
+        xd = x.to(dt)
+        lg = F.relu(F.linear(F.relu6(F.linear(xd, m.a1.weight, m.a1.bias)), m.a2.weight, m.a2.bias))   # a3c.py:142-154
+        val = F.linear(F.relu6(F.linear(xd, m.c1.weight, m.c1.bias)), m.c2.weight, m.c2.bias)[:, 0]      # :157-166
+        st = {k: (t.to(dt) if t.is_floating_point() else t) for k, t in stats.items()}
+        a, c = chunk_loss(lg.to(dt).view(T, n, 4), val.to(dt).view(T, n), actions, targets.to(dt), mask, st, mode=mode)
+        (a + c).backward()
+        return [p.grad.detach().double() for p in m.parameters()], float(a), float(c)
+
+    g64, a64, c64 = torch_grads(torch.float64)
+    g32, _, _ = torch_grads(torch.float32)
+    m = mask.float()
+    wn = (m / stats["B"][None, :] / n).contiguous()
+    cm = counts = None
+    if mode == "reference":
+        cm = ((stats["td_sum"] / (4.0 * stats["B"] ** 2))[None, :] * m / n).contiguous()
+        counts = stats["counts"].float().contiguous()
+    gf, af, cf = mlp_train_grad(net, boards.view(-1, 16), actions.view(-1).contiguous(), targets.view(-1).contiguous(),
+                                wn.view(-1), None if cm is None else cm.view(-1), counts, n_boards=n)
+    off = 0
+    for (name, p), r64, r32 in zip(net.named_parameters(), g64, g32):
+        f = gf[off:off + p.numel()].double().view_as(r64)
+        off += p.numel()
+        scale = float(r64.abs().max()) + 1e-30
+        e_f, e_t = float((f - r64).abs().max()) / scale, float((r32 - r64).abs().max()) / scale
+        assert e_f <= 2.0 * e_t + 1e-5, (name, e_f, e_t)
+    np.testing.assert_allclose([float(af), float(cf)], [a64, c64], rtol=1e-5, atol=1e-9)
+    # deterministic (fixed-order reduction)
+    gf2, _, _ = mlp_train_grad(net, boards.view(-1, 16), actions.view(-1).contiguous(), targets.view(-1).contiguous(),
+                               wn.view(-1), None if cm is None else cm.view(-1), counts, n_boards=n)
+    assert torch.equal(gf, gf2)
+
+
+@pytest.mark.parametrize("mode", ["textbook", "reference"])
+def test_trainer_fused_mlp_update_matches_torch_update(mode):
+    """One A3C update of the reference MLP through r48_mlp_train_grad vs through PyTorch autograd on the
+    same rollout (fp32 both): the losses agree to 1e-4 and the parameters after the TF1 RMSProp step
+    to 1e-5 of their update size."""
+    from rein48_amd.a3c import A3CConfig, A3CTrainer
+    outs, deltas = [], []
+    for fused in (True, False):
+        cfg = A3CConfig(n_boards=4096, max_steps=30, mode=mode, net="mlp", bf16=False, features="values", seed=21,
+                        fused_update=fused)
+        tr = A3CTrainer(cfg, device=DEV)
+        p0 = tr.flat.data.clone()
+        tr.rollout()
+        outs.append(tr.update())
+        deltas.append(tr.flat.data - p0)
+    np.testing.assert_allclose([outs[0]["actor_loss"], outs[0]["critic_loss"]],
+                               [outs[1]["actor_loss"], outs[1]["critic_loss"]], rtol=1e-4, atol=1e-9)
+    assert float((deltas[0] - deltas[1]).abs().max()) <= 1e-2 * float(deltas[1].abs().max()) + 1e-12
