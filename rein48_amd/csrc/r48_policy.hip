@@ -218,6 +218,25 @@ __device__ __forceinline__ uint32_t sample_action(const float (&z)[4], uint64_t 
     return (p0 > u) ? 0u : (c1 > u) ? 1u : (c2 > u) ? 2u : 3u;
 }
 
+// The env step's draws (the k_step contract, r48_board.h step_draw) of a lane PAIR holding boards
+// 2q and 2q + 1 of one Philox call per pair-step: instead of both lanes computing the same call every
+// step, each computes one call every OTHER step -- the even lane the call for step s, the odd lane
+// the call for step s + 1 -- and the two words its partner needs cross the pair in one DPP swap.
+// m = 0 on the even board, ~0 on the odd one; every lane of the wave must be active. Returns this
+// board's (x, y) for steps s (d0) and s + 1 (d1), bit-identical to step_draw.
+__device__ __forceinline__ void pair_block_draws(uint64_t q, uint32_t step, uint32_t m, uint32_t k0, uint32_t k1,
+                                                 uint2 &d0, uint2 &d1)
+{
+    uint32_t w[4] = {(uint32_t)q, (uint32_t)(q >> 32), step + (m & 1u), r48::kStepTag};
+    r48::philox4x32_10(w, k0, k1);
+    auto swap = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false); };
+    // the even lane holds call(step) and gives words 2, 3 (its partner's step draws); the odd lane
+    // holds call(step + 1) and gives words 0, 1 (its partner's step + 1 draws)
+    const uint32_t rx = swap(r48::bsel(m, w[0], w[2])), ry = swap(r48::bsel(m, w[1], w[3]));
+    d0 = make_uint2(r48::bsel(m, rx, w[0]), r48::bsel(m, ry, w[1]));
+    d1 = make_uint2(r48::bsel(m, w[2], rx), r48::bsel(m, w[3], ry));
+}
+
 template <int MODE, bool REWARD>
 __global__ __launch_bounds__(kThreads, kOccRoll) void k_cnn_rollout(int8_t *__restrict__ boards, int64_t n, int32_t T,
                                                              const uint4 *__restrict__ wfrag,
@@ -257,8 +276,15 @@ __global__ __launch_bounds__(kThreads, kOccRoll) void k_cnn_rollout(int8_t *__re
         const bool liveE = h == 0 ? liveA : liveB;
         const uint64_t gE = h == 0 ? gA : gB;
         int32_t len = T;
+        // lanes col, col ^ 1 of a half hold boards 2q, 2q + 1 when gid0 is even (wave-uniform): they
+        // share the env draws (pair_block_draws); otherwise every lane draws for itself
+        const bool paired = (gid0 & 1) == 0;
+        const uint32_t pm = 0u - (uint32_t)(col & 1);
+        uint2 draw0 = make_uint2(0u, 0u), draw1 = draw0;
         for (int32_t t = 0; t < T; t++) {
             const int64_t row0 = (int64_t)t * n;
+            if (paired && (t & 1) == 0)
+                pair_block_draws(gE >> 1, step0 + (uint32_t)t, pm, ek0, ek1, draw0, draw1);
             if (liveA)
                 *reinterpret_cast<uint2 *>(traj + 16 * (row0 + bA) + 8 * h) = rawA;
             if (liveB)
@@ -287,7 +313,12 @@ __global__ __launch_bounds__(kThreads, kOccRoll) void k_cnn_rollout(int8_t *__re
             const uint2 recv = make_uint2((uint32_t)__shfl_xor((int)send.x, 32), (uint32_t)__shfl_xor((int)send.y, 32));
             r48::Board bd = h == 0 ? r48::Board{rawA.x, rawA.y, recv.x, recv.y} : r48::Board{recv.x, recv.y, rawB.x, rawB.y};
             uint32_t dx, dy;
-            r48::step_draw(gE, step0 + (uint32_t)t, ek0, ek1, dx, dy);
+            if (paired) {
+                dx = (t & 1) ? draw1.x : draw0.x;
+                dy = (t & 1) ? draw1.y : draw0.y;
+            } else {
+                r48::step_draw(gE, step0 + (uint32_t)t, ek0, ek1, dx, dy);
+            }
             const r48::StepOut o =
                 r48::step_board<REWARD, false, true>(bd, act, dy, (dx & 0x3FFFFFFFu) < r48::kFourThresh30);
             // return the halves: half 0 keeps A's rows 0-1, half 1 keeps B's rows 2-3, and each sends

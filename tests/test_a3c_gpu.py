@@ -632,3 +632,22 @@ def test_trainer_fused_mlp_update_matches_torch_update(mode):
     np.testing.assert_allclose([outs[0]["actor_loss"], outs[0]["critic_loss"]],
                                [outs[1]["actor_loss"], outs[1]["critic_loss"]], rtol=1e-4, atol=1e-9)
     assert float((deltas[0] - deltas[1]).abs().max()) <= 1e-2 * float(deltas[1].abs().max()) + 1e-12
+
+
+def test_rollout_megakernel_odd_board_offset():
+    """A rank whose global board ids start odd (gid0 = rank x n with n odd): board pairs straddle the
+    megakernel's lane pairs, so it must draw per lane instead of sharing one Philox call per pair --
+    still bit-identical to the per-step rollout with the same offset."""
+    from rein48_amd import VecGame
+    from rein48_amd.a3c import A3CConfig, A3CTrainer
+    out = []
+    for mega in (True, False):
+        cfg = A3CConfig(n_boards=4099, max_steps=25, mode="textbook", net="cnn", bf16=True, features="exponents",
+                        seed=77, fused_rollout=mega)
+        tr = A3CTrainer(cfg, device=DEV)
+        tr.gid0 = 4099 * 3                               # rank 3 of n = 4099: odd
+        tr.env = VecGame(cfg.n_boards, device=DEV, seed=cfg.seed, board_offset=tr.gid0)
+        tr.rollout()
+        out.append((tr.boards.clone(), tr.actions.clone(), tr.done.clone(), tr.rewards.clone(), tr.lengths.clone()))
+    for a, b in zip(*out):
+        assert torch.equal(a, b)

@@ -13,3 +13,4 @@ for mode, feat in (('reference', 'values'), ('textbook', 'exponents')):
 " > $O/a3c_mlp.json 2> $O/a3c_mlp.err; rc=$?; cat $O/a3c_mlp.json; tail -3 $O/a3c_mlp.err; [ $rc -eq 0 ] || exit $rc
 TEST_VAL=2 bash tools/gpurun/stepn_env_ab.sh R48_STEPN_FAIR r04_fair2 0 4 2 3 0 4 2 3
 bash tools/gpurun/kstep_nt_ab.sh r04_nt
+bash tools/gpurun/stepn_env_ab.sh HIP_FORCE_DEV_KERNARG r04_kernarg 0 1 0 1
