@@ -389,6 +389,15 @@ int r48_board_onehot32(const int8_t *boards, int64_t n, void *out, void *stream)
  * per-channel sum and sum of squares of the bf16 outputs, one record [S1 64][S2 64] per CU, for
  * r48_bn_forward_stats. All pointers 16-byte aligned. */
 int64_t r48_conv_stats_floats(void);
+/* The update's forward conv with the PREVIOUS layer's training-mode BN + ReLU folded into its operand
+ * load (rein48_amd/dqn/train_step.py): x bf16 [boards][16][64] is that BN's input (the previous conv's
+ * output); coef float[128] = (a[64], b[64]) from r48_bn_finish; residual (nullable) the block's identity
+ * input. The conv consumes z = relu(a x + b (+ residual)) -- the arithmetic and rounding of
+ * r48_bn_forward_stats' apply -- and also writes z into z_out and its ReLU mask (one byte per 8
+ * channels, bit k = z > 0) into mask_out; y and stats as r48_conv3x3 with stats (required). Replaces
+ * nets.py's BatchNorm + ReLU (+ identity) followed by the next conv (README.md:15-17). */
+int r48_conv3x3_bn_in(const void *x, int64_t boards, const void *wfrag, const float *bias, const float *coef,
+                      const void *residual, void *z_out, uint8_t *mask_out, void *y, float *stats, void *stream);
 /* A data-gradient conv (64 -> 64 channels, wfrag from pack_conv_dgrad; + add as r48_conv3x3) whose
  * output dx is the gradient reaching a training-mode BN + ReLU, with that BN's backward reduction
  * fused in the epilogue: bn_part (float[r48_conv_stats_floats()]) gets per-CU records [sum g 64]
@@ -470,6 +479,12 @@ int r48_bn_forward_stats(const float *part, int32_t nblk, const void *x, const v
                          const float *gamma, const float *beta, float *running_mean, float *running_var,
                          float momentum, float eps, int32_t relu, float *save, float *workspace, void *y, uint8_t *mask,
                          void *stream);
+/* The finish of r48_bn_forward_stats alone (no apply pass): from the nblk per-block sums `part` a
+ * producer wrote (r48_conv3x3 stats), the batch mean / invstd into save[2C], the apply coefficients
+ * (a = gamma invstd, b = beta - mean a) into coef[2C], and the running statistics (nullable). */
+int r48_bn_finish(const float *part, int32_t nblk, int64_t rows, int32_t C, const float *gamma, const float *beta,
+                  float *running_mean, float *running_var, float momentum, float eps, float *save, float *coef,
+                  void *stream);
 /* The backward (with ReLU mask) from sums a producer already reduced (r48_conv3x3_bn_grad: nblk
  * records of [sum g C][sum g (x - mean) C], g = dy . mask): finish + apply, as r48_bn_backward
  * without its reduction pass over dy and x. */

@@ -618,6 +618,19 @@ int r48_bn_forward_stats(const float *part, int32_t nblk, const void *x, const v
     }
 }
 
+int r48_bn_finish(const float *part, int32_t nblk, int64_t rows, int32_t C, const float *gamma, const float *beta,
+                  float *running_mean, float *running_var, float momentum, float eps, float *save, float *coef,
+                  void *stream)
+{
+    if (!part || nblk < 1 || rows < 1 || (C != 32 && C != 64 && C != 128) || !gamma || !beta || !save || !coef)
+        return fail(R48_EINVAL, "r48_bn_finish: null argument, rows < 1 or C not 32/64/128");
+    if ((running_mean == nullptr) != (running_var == nullptr))
+        return fail(R48_EINVAL, "r48_bn_finish: running_mean and running_var go together");
+    hipLaunchKernelGGL(k_bn_finish, dim3(C), dim3(kBlock), 0, (hipStream_t)stream, nullptr, part, nblk, C, rows, gamma,
+                       beta, running_mean, running_var, momentum, eps, save, coef);
+    return launched("k_bn_finish");
+}
+
 int r48_bn_backward_part(const float *part, int32_t nblk, const void *dy, const uint8_t *mask, const void *x,
                          int64_t rows, int32_t C, const float *gamma, const float *save, float *workspace, void *dx,
                          void *dresidual, float *dgamma, float *dbeta, void *stream)

@@ -112,7 +112,16 @@ constexpr int kOutPitch = 4 * 64 + 8;      // bf16 per board in the output-row s
 // [sum g (bn_x - mean) 64] with bn_x the BN's input (the forward conv output) and mean from its
 // save (r48_bn_backward's k_bn_bwd_reduce, without its second pass over y and bn_x).
 // Passes of PO row tiles: 2, or 1 with statistics to make room for their 16 accumulators.
-template <int NC, bool ADD, int SM>
+// IN (the forward's input is the PREVIOUS layer's training-mode BN + ReLU, folded into this conv's
+// operand load instead of a separate apply pass): x is that BN's input (the previous conv's output),
+// and each input row, once loaded, becomes z = relu(a x + b (+ res)) with the BN's per-channel
+// coefficients (coef: a[64] | b[64], r48_bn_finish) -- IN = 2 adds the block's identity input res.
+// z is what the MFMAs consume, and it is also written out (z_out, with its ReLU mask byte per 8
+// channels in m_out) for the backward: the weight gradient's input, the residual path, BN's
+// backward. Same arithmetic and bf16 rounding as k_bn_apply, so z equals the apply pass's output.
+// A row is transformed just before its first use (output row r - 1), one row-load after it was
+// issued, so the loads stay ahead of the MFMAs.
+template <int NC, bool ADD, int SM, int IN = 0>
 __global__ __launch_bounds__(64 * kConvWaves, 1) void k_conv3x3(const uint16_t *__restrict__ x, int64_t boards,
                                                                const uint4 *__restrict__ wfrag,
                                                                const float *__restrict__ bias,
@@ -120,7 +129,11 @@ __global__ __launch_bounds__(64 * kConvWaves, 1) void k_conv3x3(const uint16_t *
                                                                uint16_t *__restrict__ y, float *__restrict__ stats,
                                                                const uint16_t *__restrict__ bn_x,
                                                                const uint8_t *__restrict__ bn_mask,
-                                                               const float *__restrict__ bn_save)
+                                                               const float *__restrict__ bn_save,
+                                                               const float *__restrict__ coef = nullptr,
+                                                               const uint16_t *__restrict__ res = nullptr,
+                                                               uint16_t *__restrict__ z_out = nullptr,
+                                                               uint8_t *__restrict__ m_out = nullptr)
 {
     constexpr bool STATS = SM != 0;
     constexpr int PO = STATS ? 1 : 2;
@@ -131,12 +144,15 @@ __global__ __launch_bounds__(64 * kConvWaves, 1) void k_conv3x3(const uint16_t *
     __shared__ __attribute__((aligned(16))) uint16_t o_lds[kConvWaves][16 * kOutPitch];
     __shared__ float st_lds[STATS ? kConvWaves : 1][8][16];
     __shared__ __attribute__((aligned(16))) float mean_lds[SM == 2 ? kCout : 4];
+    __shared__ __attribute__((aligned(16))) float cf_lds[IN ? 2 * kCout : 4];
     for (int i = threadIdx.x; i < kFrags * 64; i += 64 * kConvWaves)
         w_lds[i] = wfrag[i];
     if (threadIdx.x < kCout)
         b_lds[threadIdx.x] = bias ? bias[threadIdx.x] : 0.0f;
     if (SM == 2 && threadIdx.x < kCout)
         mean_lds[threadIdx.x] = bn_save[threadIdx.x];
+    if (IN && threadIdx.x < 2 * kCout)
+        cf_lds[threadIdx.x] = coef[threadIdx.x];
     __syncthreads();
     const int lane = threadIdx.x & 63, n = lane & 15, g = lane >> 4;
     const int wave = threadIdx.x >> 6;
@@ -158,6 +174,48 @@ __global__ __launch_bounds__(64 * kConvWaves, 1) void k_conv3x3(const uint16_t *
             for (int c = 0; c < NC; c++)
                 xr[R][col][c] = *reinterpret_cast<const uint4 *>(src + col * kCin + 32 * c);
     };
+    // IN: the loaded row R of tile t becomes z = relu(a x + b (+ res)) in place; z and its mask go out
+    auto transform_row = [&](int64_t t, int R) {
+        const int64_t bz = t * 16 + n;
+        const int64_t bc = bz < boards ? bz : boards - 1;
+#pragma unroll
+        for (int c = 0; c < NC; c++) {
+            const int ch = 32 * c + 8 * g;
+            const float4 a0 = *reinterpret_cast<const float4 *>(cf_lds + ch), a1 = *reinterpret_cast<const float4 *>(cf_lds + ch + 4);
+            const float4 b0 = *reinterpret_cast<const float4 *>(cf_lds + kCout + ch),
+                         b1 = *reinterpret_cast<const float4 *>(cf_lds + kCout + ch + 4);
+            const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+            const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+            for (int col = 0; col < 4; col++) {
+                const int64_t o = (bc * 16 + 4 * R + col) * kCin + ch;
+                uint4 q = make_uint4(0u, 0u, 0u, 0u);
+                if (IN == 2)
+                    q = *reinterpret_cast<const uint4 *>(res + o);
+                const uint4 v = xr[R][col][c];
+                const uint32_t w4[4] = {v.x, v.y, v.z, v.w}, q4[4] = {q.x, q.y, q.z, q.w};
+                uint32_t pk[4], m = 0;
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    float lo = __builtin_fmaf(av[2 * k], __uint_as_float(w4[k] << 16), bv[2 * k]);
+                    float hi = __builtin_fmaf(av[2 * k + 1], __uint_as_float(w4[k] & 0xFFFF0000u), bv[2 * k + 1]);
+                    if (IN == 2) {
+                        lo += __uint_as_float(q4[k] << 16);
+                        hi += __uint_as_float(q4[k] & 0xFFFF0000u);
+                    }
+                    pk[k] = pack2(fmaxf(lo, 0.f), fmaxf(hi, 0.f));
+                    m |= ((pk[k] & 0x7FFFu) != 0 && !(pk[k] & 0x8000u) ? 1u : 0u) << (2 * k) |
+                         ((pk[k] & 0x7FFF0000u) != 0 && !(pk[k] & 0x80000000u) ? 1u : 0u) << (2 * k + 1);
+                }
+                const uint4 zv = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+                xr[R][col][c] = zv;
+                if (bz < boards) {
+                    *reinterpret_cast<uint4 *>(z_out + o) = zv;
+                    m_out[o >> 3] = (uint8_t)m;
+                }
+            }
+        }
+    };
     if (tile < n_tiles) {
         load_row(tile, 0);
         load_row(tile, 1);
@@ -173,6 +231,13 @@ __global__ __launch_bounds__(64 * kConvWaves, 1) void k_conv3x3(const uint16_t *
             // drain everything in flight
             load_row(r < 2 ? tile : (next < n_tiles ? next : tile), r < 2 ? r + 2 : r - 2);
             __builtin_amdgcn_sched_barrier(0);   // issue the row loads here, ahead of this row's MFMAs
+            if (IN) {   // rows first used by this output row: 0 and 1 at r = 0, then r + 1
+                if (r == 0)
+                    transform_row(tile, 0);
+                if (r < 3)
+                    transform_row(tile, r + 1);
+                __builtin_amdgcn_sched_barrier(0);
+            }
 #pragma unroll
             for (int oh = 0; oh < 4 / PO; oh++) {   // passes of PO row tiles
                 f32x4 acc[4][PO];                    // [output column][row tile PO oh + o]
@@ -905,6 +970,28 @@ int r48_conv3x3(const void *x, int64_t boards, int32_t cin, const void *wfrag, c
     else
         hipLaunchKernelGGL((k_conv3x3<1, false, 0>), g, blk, 0, s, xs, boards, wf, bias, a, ys, stats, nx, nm, ns);
     return launched("k_conv3x3");
+}
+
+int r48_conv3x3_bn_in(const void *x, int64_t boards, const void *wfrag, const float *bias, const float *coef,
+                      const void *residual, void *z_out, uint8_t *mask_out, void *y, float *stats, void *stream)
+{
+    if (!x || !wfrag || !coef || !z_out || !mask_out || !y || !stats || boards < 1)
+        return fail(R48_EINVAL, "r48_conv3x3_bn_in: NULL argument or boards < 1");
+    if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(wfrag) | reinterpret_cast<uintptr_t>(y) |
+         reinterpret_cast<uintptr_t>(bias) | reinterpret_cast<uintptr_t>(coef) | reinterpret_cast<uintptr_t>(residual) |
+         reinterpret_cast<uintptr_t>(z_out)) & 15u)
+        return fail(R48_EINVAL, "r48_conv3x3_bn_in: x, wfrag, bias, coef, residual, z_out and y must be 16-byte aligned");
+    const dim3 g(cu_count()), blk(64 * kConvWaves);
+    hipStream_t s = (hipStream_t)stream;
+    const uint16_t *xs = (const uint16_t *)x, *rs = (const uint16_t *)residual;
+    const uint4 *wf = (const uint4 *)wfrag;
+    if (residual)
+        hipLaunchKernelGGL((k_conv3x3<2, false, 1, 2>), g, blk, 0, s, xs, boards, wf, bias, nullptr, (uint16_t *)y, stats,
+                           nullptr, nullptr, nullptr, coef, rs, (uint16_t *)z_out, mask_out);
+    else
+        hipLaunchKernelGGL((k_conv3x3<2, false, 1, 1>), g, blk, 0, s, xs, boards, wf, bias, nullptr, (uint16_t *)y, stats,
+                           nullptr, nullptr, nullptr, coef, rs, (uint16_t *)z_out, mask_out);
+    return launched("k_conv3x3 (bn in)");
 }
 
 int r48_conv3x3_bn_grad(const void *dy, int64_t boards, const void *wfrag, const void *add, void *dx,

@@ -4,6 +4,10 @@ autograd's bookkeeping, and with the fusions it cannot express:
 
   * every conv of the forward sums its bf16 outputs per channel in its epilogue (r48_conv3x3
     `stats`), so BN's forward is finish + apply with no statistics pass over the activations;
+  * (fold_bn, the default) the apply of every BN but the last runs inside the NEXT conv's operand
+    load (r48_conv3x3_bn_in): that conv reads the previous conv's output, forms relu(a x + b
+    (+ identity)) per row as it loads it, and writes the result and its ReLU mask for the backward
+    -- no separate apply pass (read y, write z) and no re-read of z by the conv;
   * every BN+ReLU forward writes a ReLU mask (1 bit per activation, r48_bn_forward `mask`), and
     its backward reads the mask instead of the 16x larger BN output;
   * every data-gradient conv reduces the BN backward of the layer below in its epilogue
@@ -40,10 +44,11 @@ def supported(net):
 
 
 class ResNetTrainStep:
-    def __init__(self, net):
+    def __init__(self, net, fold_bn=True):
         if not supported(net):
             raise ValueError("ResNetTrainStep needs a bf16 CUDA ResNet10Q with 64 channels, 4 blocks and BN")
         self.net = net
+        self.fold_bn = fold_bn
         self._bufs = {}
 
     def _buffers(self, B, dev):
@@ -56,6 +61,7 @@ class ResNetTrainStep:
                 "z": [act() for _ in range(9)],                 # BN+ReLU outputs (next conv inputs)
                 "m": [torch.empty((B * 16, 8), dtype=torch.uint8, device=dev) for _ in range(9)],
                 "save": [torch.empty(128, dtype=torch.float32, device=dev) for _ in range(9)],
+                "coef": [torch.empty(128, dtype=torch.float32, device=dev) for _ in range(9)],
                 "g": [act() for _ in range(6)],                 # gradient scratch
                 "stem_dw": torch.empty((64, 32, 3, 3), dtype=torch.float32, device=dev),
                 "loss": torch.empty(2, dtype=torch.float32, device=dev),        # mean loss, mean Q(s, a)
@@ -74,6 +80,19 @@ class ResNetTrainStep:
                                      ptr(bn.bias), ptr(bn.running_mean), ptr(bn.running_var), float(mom),
                                      float(bn.eps), 1, ptr(save), ptr(_workspace(rows, 64, y.device)), ptr(z),
                                      ptr(mask), _stream(y)))
+
+    def _bn_finish(self, k, rows, save, coef, stats):
+        """BN k's finish only (batch statistics, apply coefficients, running statistics): its apply
+        runs in the next conv's operand load (r48_conv3x3_bn_in)."""
+        bn = self.net.bns[k]
+        mom = bn.momentum if bn.momentum is not None else 0.1
+        check(_lib.load().r48_bn_finish(ptr(stats), stats.numel() // 128, rows, 64, ptr(bn.weight), ptr(bn.bias),
+                                        ptr(bn.running_mean), ptr(bn.running_var), float(mom), float(bn.eps),
+                                        ptr(save), ptr(coef), _stream(stats)))
+
+    def _conv_bn_in(self, y_prev, coef, res, z_out, m_out, frags, bias, y, stats):
+        check(_lib.load().r48_conv3x3_bn_in(ptr(y_prev), y_prev.shape[0], ptr(frags), ptr(bias), ptr(coef), ptr(res),
+                                            ptr(z_out), ptr(m_out), ptr(y), ptr(stats), _stream(y_prev)))
 
     def _bn_backward_part(self, k, part, dz, mask, y, save, dy, dres=None):
         """BN k's backward from the reduction its gradient's producer fused (r48_conv3x3_bn_grad)."""
@@ -113,14 +132,27 @@ class ResNetTrainStep:
         torch._foreach_add_([m.num_batches_tracked for m in net.bns], 1)   # one launch for the 9 BNs
         st = buf["stats"]                                  # the conv epilogues' BN sums
         conv3x3(x, fwd[0], convs[0].bias, out=Y[0], stats=st)
-        self._bn_forward(0, Y[0], Z[0], M[0], S[0], st)
-        for b in range(4):
-            i1, i2 = 1 + 2 * b, 2 + 2 * b
-            h = Z[i1 - 1]
-            conv3x3(h, fwd[i1], convs[i1].bias, out=Y[i1], stats=st)
-            self._bn_forward(i1, Y[i1], Z[i1], M[i1], S[i1], st)
-            conv3x3(Z[i1], fwd[i2], convs[i2].bias, out=Y[i2], stats=st)
-            self._bn_forward(i2, Y[i2], Z[i2], M[i2], S[i2], st, residual=h)
+        if self.fold_bn:
+            # conv k applies BN k - 1 (+ the block's identity for k - 1 = 2, 4, 6) to its input rows
+            # and writes Z[k - 1], M[k - 1]; the last BN (into the head) is a plain finish + apply
+            CF = buf["coef"]
+            rows = B * 16
+            self._bn_finish(0, rows, S[0], CF[0], st)
+            for k in range(1, 9):
+                res = Z[k - 3] if (k - 1) % 2 == 0 and k - 1 >= 2 else None
+                self._conv_bn_in(Y[k - 1], CF[k - 1], res, Z[k - 1], M[k - 1], fwd[k], convs[k].bias, Y[k], st)
+                if k < 8:
+                    self._bn_finish(k, rows, S[k], CF[k], st)
+            self._bn_forward(8, Y[8], Z[8], M[8], S[8], st, residual=Z[6])
+        else:
+            self._bn_forward(0, Y[0], Z[0], M[0], S[0], st)
+            for b in range(4):
+                i1, i2 = 1 + 2 * b, 2 + 2 * b
+                h = Z[i1 - 1]
+                conv3x3(h, fwd[i1], convs[i1].bias, out=Y[i1], stats=st)
+                self._bn_forward(i1, Y[i1], Z[i1], M[i1], S[i1], st)
+                conv3x3(Z[i1], fwd[i2], convs[i2].bias, out=Y[i2], stats=st)
+                self._bn_forward(i2, Y[i2], Z[i2], M[i2], S[i2], st, residual=h)
         h = Z[8].view(B, 1024)
         q = q_head_forward(h, net.head.weight, net.head.bias)
         # ---- Huber loss of Q(x)[action] and its gradient (d loss / d q): one kernel + one finish

@@ -755,3 +755,51 @@ def test_fused_adam_matches_torch_adam():
         ref.step()
     torch.testing.assert_close(a.weight, b.weight, rtol=1e-6, atol=1e-7)
     torch.testing.assert_close(a.bias, b.bias, rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize("B", [4099, 1 << 16])
+def test_resnet_train_step_bn_fold_is_bit_identical(B):
+    """ResNetTrainStep with every BN apply but the last folded into the next conv's operand load
+    (r48_conv3x3_bn_in + r48_bn_finish) == the step with separate apply passes, bit for bit: the
+    folded load forms relu(a x + b (+ identity)) with k_bn_apply's arithmetic and rounding, so every
+    activation, ReLU mask, loss, gradient and running statistic is identical (ragged and bench-size
+    minibatches)."""
+    from rein48_amd.a3c.optim import FlatParams
+    from rein48_amd.dqn.conv import board_onehot32
+    from rein48_amd.dqn.nets import ResNet10Q
+    from rein48_amd.dqn.train_step import ResNetTrainStep
+    torch.manual_seed(B)
+    net = ResNet10Q(dtype=torch.bfloat16).to(DEV).train()
+    with torch.no_grad():
+        net.head.weight.normal_(std=0.05)
+        for m in net.bns:                                    # non-trivial affine parameters
+            m.weight.uniform_(0.5, 1.5)
+            m.bias.uniform_(-0.5, 0.5)
+    flat = FlatParams(net)
+    rng = np.random.default_rng(B + 1)
+    boards = torch.from_numpy(rng.integers(0, 14, size=(B, 16)).astype(np.int8)).to(DEV)
+    x = board_onehot32(boards).view(B, 512)
+    action = torch.from_numpy(rng.integers(0, 4, size=B).astype(np.int8)).to(DEV)
+    target = torch.from_numpy(rng.normal(size=B).astype(np.float32)).to(DEV)
+    stats0 = [(m.running_mean.clone(), m.running_var.clone()) for m in net.bns]
+    out = []
+    for fold in (True, False):
+        for m, (rm, rv) in zip(net.bns, stats0):
+            m.running_mean.copy_(rm)
+            m.running_var.copy_(rv)
+        flat.zero_grad()
+        step = ResNetTrainStep(net, fold_bn=fold)
+        loss, q_mean = step(x, action, target)
+        buf = next(iter(step._bufs.values()))
+        out.append((loss.clone(), q_mean.clone(), flat.grad.clone(),
+                    [torch.cat([m.running_mean, m.running_var]) for m in net.bns],
+                    [z.clone() for z in buf["z"]], [m.clone() for m in buf["m"]]))
+    (la, qa, ga, sa, za, ma), (lb, qb, gb, sb, zb, mb) = out
+    assert torch.equal(la, lb) and torch.equal(qa, qb)
+    for k, (u, v) in enumerate(zip(za, zb)):
+        assert torch.equal(u, v), ("z", k)
+    for k, (u, v) in enumerate(zip(ma, mb)):
+        assert torch.equal(u, v), ("mask", k)
+    for k, (u, v) in enumerate(zip(sa, sb)):
+        assert torch.equal(u, v), ("running stats", k)
+    assert torch.equal(ga, gb)
