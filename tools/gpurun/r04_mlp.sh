@@ -1,4 +1,5 @@
 #!/bin/bash
+bash tools/gpurun/r04_dqn.sh || exit 1
 # Round-4 session: the A3C GPU tests touched this round (fused reference MLP, rollout megakernels),
 # config-3-size A3C timings for the CNN and the reference MLP in both loss modes, then the k_step_n
 # fairness A/B, the non-temporal k_step A/B and the device-kernarg A/B.
@@ -16,6 +17,3 @@ for net, bf16, mode, feat in (('mlp', False, 'reference', 'values'), ('mlp', Fal
 import json, sys
 for l in sys.stdin:
     r = json.loads(l); print(r['net'][:3], r['mode'], 'rollout %.2f ms update %.2f ms train %.2f G/s' % (r['rollout_ms'], r['update_ms'], r['train_env_steps_per_s'] / 1e9))"; tail -3 $O/a3c.err; [ $rc -eq 0 ] || exit $rc
-TEST_VAL=2 bash tools/gpurun/stepn_env_ab.sh R48_STEPN_FAIR r04_fair2 0 4 2 3 0 4 2 3 || exit 1
-bash tools/gpurun/kstep_nt_ab.sh r04_nt || exit 1
-bash tools/gpurun/stepn_env_ab.sh HIP_FORCE_DEV_KERNARG r04_kernarg 0 1 0 1
