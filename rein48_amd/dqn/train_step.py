@@ -4,10 +4,13 @@ autograd's bookkeeping, and with the fusions it cannot express:
 
   * every conv of the forward sums its bf16 outputs per channel in its epilogue (r48_conv3x3
     `stats`), so BN's forward is finish + apply with no statistics pass over the activations;
-  * (fold_bn, the default) the apply of every BN but the last runs inside the NEXT conv's operand
+  * (fold_bn=True, opt-in) the apply of every BN but the last runs inside the NEXT conv's operand
     load (r48_conv3x3_bn_in): that conv reads the previous conv's output, forms relu(a x + b
     (+ identity)) per row as it loads it, and writes the result and its ReLU mask for the backward
-    -- no separate apply pass (read y, write z) and no re-read of z by the conv;
+    -- no separate apply pass and no re-read of z by the conv. Bit-identical, but measured 3 %
+    SLOWER at the 64K minibatch (3.88 vs 3.76 ms per forward + backward, profiles/r04/dqn/bnfold.txt:
+    the transform's VALU and the side-output stores sit on the conv's exposed load path), so the
+    default keeps the separate apply passes;
   * every BN+ReLU forward writes a ReLU mask (1 bit per activation, r48_bn_forward `mask`), and
     its backward reads the mask instead of the 16x larger BN output;
   * every data-gradient conv reduces the BN backward of the layer below in its epilogue
@@ -44,7 +47,7 @@ def supported(net):
 
 
 class ResNetTrainStep:
-    def __init__(self, net, fold_bn=True):
+    def __init__(self, net, fold_bn=False):
         if not supported(net):
             raise ValueError("ResNetTrainStep needs a bf16 CUDA ResNet10Q with 64 channels, 4 blocks and BN")
         self.net = net
