@@ -336,45 +336,23 @@ __global__ __launch_bounds__(kBlock) void k_step(int8_t *boards, int64_t n, int6
 // call, not per step.
 // TRAJ (r48_env_rollout): also every step's action and done into row t of traj_actions /
 // traj_done ([n_steps][n], each nullable) -- one 2-byte store per plane per pair and step.
-template <bool RANDOM, bool AUTO_RESET, bool REWARD, int NP, bool TRAJ = false, int FAIR = 0,
-          int BS = kBlock>
+template <bool RANDOM, bool AUTO_RESET, bool REWARD, int NP, bool TRAJ = false>
 // The read-ahead below needs ~62 VGPRs; waves_per_eu(8) holds the allocator to the 64 that keep the
 // 8 waves per SIMD the VALU issue bound needs. The merge-reward variants need more than 64 (they
 // spilled 28-48 B per lane to scratch under the cap), so they keep the plain launch bounds.
-__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(REWARD ? 1 : 8, 8))) void k_step_n(int8_t *boards, int64_t n, int64_t gid0, uint32_t k0, uint32_t k1,
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(REWARD ? 1 : 8, 8))) void k_step_n(int8_t *boards, int64_t n, int64_t gid0, uint32_t k0, uint32_t k1,
                                                    uint32_t step0, int32_t n_steps, int8_t *__restrict__ actions,
                                                    uint8_t *__restrict__ done, uint8_t *__restrict__ changed,
                                                    int32_t *__restrict__ reward, int32_t *__restrict__ score,
                                                    unsigned long long *err, int8_t *__restrict__ traj_actions = nullptr,
                                                    uint8_t *__restrict__ traj_done = nullptr)
 {
-    constexpr int64_t kTile = (int64_t)BS * 2 * NP;
+    constexpr int64_t kTile = (int64_t)kBlock * 2 * NP;
     const int64_t base = (int64_t)blockIdx.x * kTile + 2 * (int64_t)threadIdx.x;
     const bool want_score = score != nullptr;
     const int32_t last = n_steps - 1;
     __shared__ __attribute__((aligned(16))) r48::Orient tab[16];
-    // FAIR: each wave's step count, one byte per (SIMD, wave of this workgroup on it); see below
-    __shared__ __attribute__((aligned(8))) uint8_t prog[FAIR ? 4 : 1][8];
-    __shared__ uint32_t n_on_simd[FAIR ? 4 : 1];
-    __shared__ uint32_t front[FAIR ? 4 : 1];   // FAIR >= 2: the furthest step any wave of the SIMD reached
-    if (FAIR && threadIdx.x < 4) {
-        *reinterpret_cast<uint2 *>(prog[threadIdx.x]) = make_uint2(0u, 0u);
-        n_on_simd[threadIdx.x] = 0u;
-        front[threadIdx.x] = 0u;
-    }
     load_orient_table(tab);
-    uint32_t simd = 0, slot = 0, n_sib = 0;
-    if (FAIR) {   // register this wave with its SIMD: slot = its index among this workgroup's waves there
-        uint32_t hw;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-        simd = (hw >> 4) & 3u;
-        if ((threadIdx.x & 63) == 0)
-            slot = atomicAdd(&n_on_simd[simd], 1u);
-        slot = __builtin_amdgcn_readfirstlane(slot) & 7u;
-        __syncthreads();
-        n_sib = __builtin_amdgcn_readfirstlane(n_on_simd[simd]);
-        n_sib = n_sib < 8u ? n_sib : 8u;
-    }
     // trajectory rows whose pair addresses are not all 2-byte aligned (odd n or odd row pointers)
     // take byte stores inside the fast path, instead of sending the whole grid down the guarded one
     const bool traj_bytes = TRAJ && ((n | (int64_t)((uintptr_t)traj_actions | (uintptr_t)traj_done)) & 1) != 0;
@@ -385,7 +363,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(REWARD ? 1 :
         uint64_t q[NP];
 #pragma unroll
         for (int j = 0; j < NP; j++) {
-            const int64_t i = base + 2 * BS * j;
+            const int64_t i = base + 2 * kBlock * j;
             b[2 * j] = load_board(boards, i);
             b[2 * j + 1] = load_board(boards, i + 1);
             q[j] = (uint64_t)(gid0 + i) >> 1;
@@ -431,37 +409,16 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(REWARD ? 1 :
             sd[j] = orient_at(tab, (dd[j].x >> 26) & 0x30u);
         }
         int32_t t = 0;
-        // FAIR (instead of the phases): progress-balanced issue priority. Every step a wave posts
-        // its step count to its SIMD's byte slots in LDS, reads those of the other waves of its
-        // workgroup on the same SIMD, and sets its priority to 3 - (steps ahead of the slowest of
-        // them), so the leaders yield the VALU to the laggards all through the call instead of
-        // at three phase boundaries (the scalar unit does the arithmetic, beside the VALU).
-        if (FAIR)
-            __builtin_amdgcn_s_setprio(3);
 #pragma nounroll
-        for (int ph = 0; ph < (FAIR ? 1 : 4); ph++) {
-            if (!FAIR) {
-                switch (ph) {   // s_setprio takes an immediate
-                case 0: __builtin_amdgcn_s_setprio(3); break;
-                case 1: __builtin_amdgcn_s_setprio(2); break;
-                case 2: __builtin_amdgcn_s_setprio(1); break;
-                default: __builtin_amdgcn_s_setprio(0); break;
-                }
+        for (int ph = 0; ph < 4; ph++) {
+            switch (ph) {   // s_setprio takes an immediate
+            case 0: __builtin_amdgcn_s_setprio(3); break;
+            case 1: __builtin_amdgcn_s_setprio(2); break;
+            case 2: __builtin_amdgcn_s_setprio(1); break;
+            default: __builtin_amdgcn_s_setprio(0); break;
             }
-            for (const int32_t end = FAIR ? n_steps : ends[ph]; t < end; t++) {
+            for (const int32_t end = ends[ph]; t < end; t++) {
                 const uint32_t step = step0 + (uint32_t)t;
-                uint2 pv = make_uint2(0u, 0u);
-                uint32_t lead = 0u;
-                if (FAIR >= 2) {   // one LDS atomic: the SIMD's front before this wave's own step count
-                    if ((threadIdx.x & 63) == 0)
-                        lead = atomicMax(&front[simd], (uint32_t)t);
-                } else if (FAIR) {
-                    if ((threadIdx.x & 63) == 0)
-                        prog[simd][slot] = (uint8_t)t;
-                    asm volatile("" ::: "memory");   // re-read every step (the other waves write it)
-                    const unsigned long long v = *reinterpret_cast<const unsigned long long *>(prog[simd]);
-                    pv = make_uint2((uint32_t)v, (uint32_t)(v >> 32));
-                }
                 const bool sc = want_score && t == last;
 #pragma unroll
                 for (int j = 0; j < NP; j++) {
@@ -487,7 +444,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(REWARD ? 1 :
                     de[j] = ne;
                     dd[j] = nd;
                     if (TRAJ) {
-                        const int64_t at = (int64_t)t * n + base + 2 * BS * j;
+                        const int64_t at = (int64_t)t * n + base + 2 * kBlock * j;
                         if (traj_bytes) {   // wave-uniform
                             if (traj_actions) {
                                 traj_actions[at] = (int8_t)r[2 * j].a;
@@ -507,36 +464,6 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(REWARD ? 1 :
                         }
                     }
                 }
-                if (FAIR >= 2) {   // steps behind the SIMD's leader -> priority
-                    const int32_t behind = (int32_t)__builtin_amdgcn_readfirstlane(lead) - t;
-                    if (FAIR == 2) {
-                        if (behind <= 0)
-                            __builtin_amdgcn_s_setprio(0);
-                        else if (behind == 1)
-                            __builtin_amdgcn_s_setprio(1);
-                        else if (behind == 2)
-                            __builtin_amdgcn_s_setprio(2);
-                        else
-                            __builtin_amdgcn_s_setprio(3);
-                    } else {
-                        asm volatile("" ::"s"(behind));   // FAIR 3: the bookkeeping without the priority
-                    }
-                } else if (FAIR) {   // steps ahead of the slowest sibling (bytes: counts modulo 256)
-                    const uint32_t lo = __builtin_amdgcn_readfirstlane(pv.x), hi = __builtin_amdgcn_readfirstlane(pv.y);
-                    int32_t ahead = 0;
-#pragma unroll
-                    for (uint32_t k = 0; k < 8; k++) {
-                        const uint32_t b8 = ((k < 4 ? lo : hi) >> (8 * (k & 3))) & 0xFFu;
-                        const int32_t d = (int32_t)(int8_t)(uint8_t)((uint32_t)t - b8);
-                        ahead = (k < n_sib && d > ahead) ? d : ahead;
-                    }
-                    switch (ahead) {
-                    case 0: __builtin_amdgcn_s_setprio(3); break;
-                    case 1: __builtin_amdgcn_s_setprio(2); break;
-                    case 2: __builtin_amdgcn_s_setprio(1); break;
-                    default: __builtin_amdgcn_s_setprio(0); break;
-                    }
-                }
             }
         }
         if (RANDOM) {   // the line form of the last action, or rows after a reset in the last step
@@ -549,12 +476,12 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(REWARD ? 1 :
         for (int j = 0; j < NP; j++) {
             r[2 * j].b = r48::reorient(b[2 * j], orient_at(tab, ob[2 * j]));   // back to rows
             r[2 * j + 1].b = r48::reorient(b[2 * j + 1], orient_at(tab, ob[2 * j + 1]));
-            emit_pair<RANDOM, REWARD>(r[2 * j], r[2 * j + 1], base + 2 * BS * j, boards, actions, done, changed,
+            emit_pair<RANDOM, REWARD>(r[2 * j], r[2 * j + 1], base + 2 * kBlock * j, boards, actions, done, changed,
                                       reward, score);
         }
     } else {
         for (int j = 0; j < 2 * NP; j++) {
-            const int64_t i = base + 2 * BS * (j >> 1) + (j & 1);
+            const int64_t i = base + 2 * kBlock * (j >> 1) + (j & 1);
             if (i < n) {
                 const uint32_t a = RANDOM ? 0u : (uint32_t)(uint8_t)actions[i];
                 if (!RANDOM)
@@ -1104,26 +1031,6 @@ void launch_steps(r48_env *env, int32_t n_steps, int8_t *actions, uint32_t flags
                            env->n, env->gid0, k0, k1, env->step_ctr, actions, done, changed, reward, score,
                            env->err);
     };
-    static const int fair = [] {
-        const char *v = getenv("R48_STEPN_FAIR");
-        return v ? atoi(v) : 0;
-    }();
-    if (fair && rnd && n_steps > 1) {
-        constexpr int kFairBlock = 1024;
-        auto go = [&](auto kern) {
-            const int64_t tile = (int64_t)kFairBlock * 2 * kStepNP;
-            hipLaunchKernelGGL(kern, dim3((unsigned)((env->n + tile - 1) / tile)), dim3(kFairBlock), 0, stream,
-                               env->boards, env->n, env->gid0, k0, k1, env->step_ctr, n_steps, actions, done, changed,
-                               reward, score, env->err, (int8_t *)nullptr, (uint8_t *)nullptr);
-        };
-        if (ar && !rw) {
-            if (fair == 1) go(k_step_n<true, true, false, kStepNP, false, 1, kFairBlock>);
-            else if (fair == 2) go(k_step_n<true, true, false, kStepNP, false, 2, kFairBlock>);
-            else if (fair == 3) go(k_step_n<true, true, false, kStepNP, false, 3, kFairBlock>);
-            else go(k_step_n<true, true, false, kStepNP, false, 0, kFairBlock>);
-            return;
-        }
-    }
     auto many = [&](auto kern) {
         const int64_t tile = (int64_t)kBlock * 2 * kStepNP;
         hipLaunchKernelGGL(kern, dim3((unsigned)((env->n + tile - 1) / tile)), dim3(kBlock), 0, stream, env->boards,

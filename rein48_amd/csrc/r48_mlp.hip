@@ -222,9 +222,13 @@ constexpr int kRecLossA = 2501, kRecLossC = 2502;
 constexpr float kEntropyEps = 1e-5f;       // a3c.py:114
 constexpr float kLn2 = 0.69314718055994531f;
 
+// the wave's LDS stash is written by one phase and read by the other: every outstanding LDS
+// operation completes (s_waitcnt lgkmcnt(0)) before the next phase's first access, and the
+// compiler moves no LDS access across the point
 __device__ __forceinline__ void wave_lds_sync()
 {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
