@@ -213,8 +213,14 @@ __global__ __launch_bounds__(kBlock) void k_mlp_rollout(int8_t *__restrict__ boa
 // so the weight gradients (contractions over rows) never cross lanes. Per wave one record of the
 // flat gradient in FlatParams order (a1.w [64][16] | a1.b | a2.w [4][64] | a2.b | c1.w | c1.b |
 // c2.w | c2.b) + the two losses; k_mlp_reduce sums the records in a fixed order (deterministic).
+// The ReLU derivatives of the update are decisions at 0 (and 6, ReLU6): an fp32 pre-activation within
+// its rounding error of the boundary may land on the other side than the exact value, and with raw
+// tile values as inputs (up to 2^17) a flipped hidden-unit mask moves a weight-gradient entry by a
+// whole row's term (dh x). So the update decides them on exact-enough values: a hidden pre-activation
+// (phase 2) or a logit (phase 1) whose fp32 value lies within the fp32 error bound of its boundary is
+// recomputed in fp64 (rare: a divergent branch taken by ~1e-5 of the units / logits).
 constexpr int kTrainWaves = 4;
-constexpr int kStash = 24;                 // x[16] | dz[4] | dv | pad
+constexpr int kStash = 28;                 // x[16] | dz[4] | dv | max x | dz before the logits' ReLU [4] | pad
 constexpr int kRec = 2504;                 // 2,501 gradient floats + actor loss + critic loss + pad
 constexpr int kRecLossA = 2501, kRecLossC = 2502;
 // (the record's section offsets equal the blob's, kA1W .. kC2B; inside a1 / a2 / c1 the record has
@@ -242,7 +248,7 @@ __device__ __forceinline__ float wave_sum(float v)
 }
 
 template <int MODE, bool REF>
-__global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_eu(3))) void k_mlp_train(
+__global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_eu(2))) void k_mlp_train(
     const int8_t *__restrict__ boards, int64_t rows, int64_t n_boards, const int8_t *__restrict__ actions,
     const float *__restrict__ targets, const float *__restrict__ wn, const float *__restrict__ cm,
     const float *__restrict__ counts, float beta, const float *__restrict__ w, float *__restrict__ partials)
@@ -263,6 +269,17 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
     for (int k = 0; k < 4; k++)
         w2l[k] = w[kA2W + 8 * (lane >> 1) + 2 * k + (lane & 1)];
     const float b1l = w[kA1B + lane], bc1l = w[kC1B + lane], wc2l = w[kC2W + lane];
+    // fp32 error bound of the unit's pre-activation: 16 roundings of partial sums below
+    // |b| + sum |w| max x, i.e. < 2^-20 (|b| + sum |w| max x); 2x margin
+    float s1l = 0.f, sc1l = 0.f;
+#pragma unroll
+    for (int f = 0; f < 16; f++) {
+        s1l += fabsf(w1l[f]);
+        sc1l += fabsf(wc1l[f]);
+    }
+    s1l *= 0x1p-19f;
+    sc1l *= 0x1p-19f;
+    const float e1l = fabsf(b1l) * 0x1p-19f, ec1l = fabsf(bc1l) * 0x1p-19f;
     float g1[16], gc1[16], g2[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int f = 0; f < 16; f++)
@@ -270,6 +287,25 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
     float gb1 = 0.f, gbc1 = 0.f, gc2 = 0.f;
     // per-row-lane sums (reduced over the wave at the end)
     float gb2[4] = {0.f, 0.f, 0.f, 0.f}, gbc2 = 0.f, loss_a = 0.f, loss_c = 0.f;
+    // fp32 error bound of a pre-ReLU logit: its own sum (64 products of |h| <= 6 in parity halves:
+    // < 2^-18 (|b2| + 6 sum |W2[k][:]|)) plus the hidden units' errors carried through W2 (each
+    // < 2^-20 (|b1| + sum |W1[j][:]| max x), see s1l below); 2x-4x margins
+    float zedge[4], zcarry[4], hb = 0.f, hw = 0.f;
+    for (int j = 0; j < 64; j++) {
+        float sw = 0.f;
+        for (int f = 0; f < 16; f++)
+            sw += fabsf(w[kA1W + 32 * (j >> 1) + 2 * f + (j & 1)]);
+        hw = fmaxf(hw, sw);
+        hb = fmaxf(hb, fabsf(w[kA1B + j]));
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        float sa = 0.f;
+        for (int j = 0; j < 64; j++)
+            sa += fabsf(w[kA2W + 8 * (j >> 1) + 2 * k + (j & 1)]);
+        zedge[k] = (fabsf(w[kA2B + k]) + 6.0f * sa) * 0x1p-16f;
+        zcarry[k] = sa * 0x1p-19f;
+    }
 
     const int64_t n_tiles = (rows + 63) / 64;
     const int64_t stride = (int64_t)gridDim.x * kTrainWaves;
@@ -280,6 +316,7 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
         const int64_t rr = live ? r : rows - 1;      // padding lanes: a valid row with weight 0
         float x[16], zr[4], v;
         board_inputs<MODE>(load_board(boards, rr), x);
+        float xmax;
         {
             const float *wp = w;
             f32x2 acc[4];
@@ -290,6 +327,9 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
             f32x2 c[1];
             hidden_into<1>(wp, kC1W, kC1B, kC2W, x, c);
             v = wp[kC2B] + (c[0].x + c[0].y);
+            xmax = fmaxf(fmaxf(fmaxf(fmaxf(x[0], x[1]), fmaxf(x[2], x[3])), fmaxf(fmaxf(x[4], x[5]), fmaxf(x[6], x[7]))),
+                                     fmaxf(fmaxf(fmaxf(x[8], x[9]), fmaxf(x[10], x[11])), fmaxf(fmaxf(x[12], x[13]), fmaxf(x[14], x[15]))));
+
         }
         const float wt = live ? wn[rr] : 0.0f;
         const float tgt = targets[rr];
@@ -337,19 +377,60 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
         }
         const float dv = -2.0f * wt * td;                          // critic = wn td^2
         loss_c += wt * td * td;
+        // through the logits' ReLU; a logit within its fp32 error bound of 0 is decided on its exact
+        // value by the whole wave at the start of phase 2 (rows flagged in `near_rows`)
+        bool near = false;
+        float dzm[4];
 #pragma unroll
         for (int k = 0; k < 4; k++) {
-            dz[k] = zr[k] > 0.0f ? dz[k] : 0.0f;                   // through the logits' ReLU
-            gb2[k] += dz[k];
+            near |= fabsf(zr[k]) < zedge[k] + zcarry[k] * (hb + hw * xmax);
+            dzm[k] = zr[k] > 0.0f ? dz[k] : 0.0f;
         }
+        if (!near) {
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                gb2[k] += dzm[k];
+        }
+        const uint64_t near_rows = __ballot(near);
         gbc2 += dv;
         wave_lds_sync();   // the previous tile's phase 2 has read the stash
 #pragma unroll
         for (int q = 0; q < 4; q++)
             *reinterpret_cast<float4 *>(&st[lane][4 * q]) = make_float4(x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]);
-        *reinterpret_cast<float4 *>(&st[lane][16]) = make_float4(dz[0], dz[1], dz[2], dz[3]);
+        *reinterpret_cast<float4 *>(&st[lane][16]) = make_float4(dzm[0], dzm[1], dzm[2], dzm[3]);
         st[lane][20] = dv;
+        st[lane][21] = xmax;
+        if (near_rows)
+            *reinterpret_cast<float4 *>(&st[lane][24]) = make_float4(dz[0], dz[1], dz[2], dz[3]);
         wave_lds_sync();
+        // exact logits of the flagged rows, lane = hidden unit: its fp64 pre-activation, times W2,
+        // summed over the wave; lane 0 writes the row's dz through the exact ReLU decision
+        for (uint64_t m = near_rows; m; m &= m - 1) {
+            const int j = __builtin_ctzll(m);
+            double ad = b1l;
+#pragma unroll
+            for (int f = 0; f < 16; f++)
+                ad = __builtin_fma((double)w1l[f], (double)st[j][f], ad);
+            const double hd = ad < 0.0 ? 0.0 : (ad > 6.0 ? 6.0 : ad);
+            double t[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                t[k] = (double)w2l[k] * hd;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1)
+                    t[k] += __shfl_xor(t[k], o);
+            }
+            if (lane == 0) {
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const float d = (double)w[kA2B + k] + t[k] > 0.0 ? st[j][24 + k] : 0.0f;
+                    st[j][16 + k] = d;
+                    gb2[k] += d;
+                }
+            }
+        }
+        if (near_rows)
+            wave_lds_sync();
         // ---------------- phase 2: lane = hidden unit
 #pragma unroll 1
         for (int j = 0; j < 64; j++) {
@@ -367,10 +448,28 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
                 al = __builtin_fmaf(w1l[f], xr[f], al);
                 cl = __builtin_fmaf(wc1l[f], xr[f], cl);
             }
+            // the ReLU6 decisions on exact-enough values: within the fp32 error bound of 0 or 6
+            // (16 roundings of partial sums below sum |w| max x) the pre-activation is redone in fp64
+            const float xm = st[j][21];
+            bool ma = al > 0.0f && al < 6.0f, mc = cl > 0.0f && cl < 6.0f;
+            if (fminf(fabsf(al), fabsf(al - 6.0f)) < __builtin_fmaf(s1l, xm, e1l) ||
+                fminf(fabsf(cl), fabsf(cl - 6.0f)) < __builtin_fmaf(sc1l, xm, ec1l)) {
+                double ad = b1l, cd = bc1l;
+#pragma unroll
+                for (int f = 0; f < 16; f++) {
+                    // converted here, behind an opaque copy: hoisted out of the row loop, 32 fp64
+                    // weight copies would stay live and spill
+                    float wa = w1l[f], wc = wc1l[f];
+                    asm volatile("" : "+v"(wa), "+v"(wc));
+                    ad = __builtin_fma((double)wa, (double)xr[f], ad);
+                    cd = __builtin_fma((double)wc, (double)xr[f], cd);
+                }
+                ma = ad > 0.0 && ad < 6.0;
+                mc = cd > 0.0 && cd < 6.0;
+            }
             const float hl = relu6(al), hcl = relu6(cl);
-            const float dh = (al > 0.0f && al < 6.0f) ? w2l[0] * dz4.x + w2l[1] * dz4.y + w2l[2] * dz4.z + w2l[3] * dz4.w
-                                                      : 0.0f;
-            const float dhc = (cl > 0.0f && cl < 6.0f) ? wc2l * dvr : 0.0f;
+            const float dh = ma ? w2l[0] * dz4.x + w2l[1] * dz4.y + w2l[2] * dz4.z + w2l[3] * dz4.w : 0.0f;
+            const float dhc = mc ? wc2l * dvr : 0.0f;
 #pragma unroll
             for (int f = 0; f < 16; f++) {
                 g1[f] = __builtin_fmaf(dh, xr[f], g1[f]);
