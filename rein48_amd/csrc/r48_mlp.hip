@@ -79,10 +79,13 @@ __device__ __forceinline__ void hidden_into(const float *__restrict__ w, int w1,
         acc[k] = f32x2{0.0f, 0.0f};
 #pragma unroll 1
     for (int p = 0; p < 32; p++) {
-        f32x2 a = pair_at(w, b1 + 2 * p);
+        // four independent FMA chains over inputs f = q mod 4 (the bias starts chain 0), summed in a
+        // fixed order: a 16-long dependent chain per pair left the VALU waiting on its latency
+        f32x2 c4[4] = {pair_at(w, b1 + 2 * p), f32x2{0.0f, 0.0f}, f32x2{0.0f, 0.0f}, f32x2{0.0f, 0.0f}};
 #pragma unroll
         for (int f = 0; f < 16; f++)
-            a = __builtin_elementwise_fma(pair_at(w, w1 + 32 * p + 2 * f), f32x2{x[f], x[f]}, a);
+            c4[f & 3] = __builtin_elementwise_fma(pair_at(w, w1 + 32 * p + 2 * f), f32x2{x[f], x[f]}, c4[f & 3]);
+        const f32x2 a = (c4[0] + c4[1]) + (c4[2] + c4[3]);
         const f32x2 h = f32x2{relu6(a.x), relu6(a.y)};
 #pragma unroll
         for (int k = 0; k < NO; k++)
@@ -442,12 +445,14 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
             }
             const float4 dz4 = *reinterpret_cast<const float4 *>(&st[j][16]);
             const float dvr = st[j][20];
-            float al = b1l, cl = bc1l;   // the FMA sequence of phase 1 (hidden_into), so the same values
+            // the four-chain FMA order of phase 1 (hidden_into), so the same values
+            float ca[4] = {b1l, 0.f, 0.f, 0.f}, cc[4] = {bc1l, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int f = 0; f < 16; f++) {
-                al = __builtin_fmaf(w1l[f], xr[f], al);
-                cl = __builtin_fmaf(wc1l[f], xr[f], cl);
+                ca[f & 3] = __builtin_fmaf(w1l[f], xr[f], ca[f & 3]);
+                cc[f & 3] = __builtin_fmaf(wc1l[f], xr[f], cc[f & 3]);
             }
+            const float al = (ca[0] + ca[1]) + (ca[2] + ca[3]), cl = (cc[0] + cc[1]) + (cc[2] + cc[3]);
             // the ReLU6 decisions on exact-enough values: within the fp32 error bound of 0 or 6
             // (16 roundings of partial sums below sum |w| max x) the pre-activation is redone in fp64
             const float xm = st[j][21];
