@@ -250,6 +250,29 @@ __device__ __forceinline__ float wave_sum(float v)
     return v;
 }
 
+// phase 2's (a_l, c_l) of one stashed row (its inputs returned as pairs (x_2i, x_2i+1)), in the
+// four-chain FMA order of phase 1 (hidden_into: chain q takes the inputs f = q mod 4 in order, the
+// bias starts chain 0), so the same values: chains (0, 1) are the pair p*, chains (2, 3) the pair q*
+__device__ __forceinline__ f32x2 unit_preacts(const float (&row)[kStash], const f32x2 (&wa)[8], const f32x2 (&wc)[8],
+                                              f32x2 bl, f32x2 (&xp)[8])
+{
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const float4 t4 = *reinterpret_cast<const float4 *>(&row[4 * q]);
+        xp[2 * q] = f32x2{t4.x, t4.y};
+        xp[2 * q + 1] = f32x2{t4.z, t4.w};
+    }
+    f32x2 pa = f32x2{bl.x, 0.f}, qa = f32x2{0.f, 0.f}, pc = f32x2{bl.y, 0.f}, qc = f32x2{0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < 8; i += 2) {
+        pa = __builtin_elementwise_fma(wa[i], xp[i], pa);
+        pc = __builtin_elementwise_fma(wc[i], xp[i], pc);
+        qa = __builtin_elementwise_fma(wa[i + 1], xp[i + 1], qa);
+        qc = __builtin_elementwise_fma(wc[i + 1], xp[i + 1], qc);
+    }
+    return f32x2{(pa.x + pa.y) + (qa.x + qa.y), (pc.x + pc.y) + (qc.x + qc.y)};
+}
+
 template <int MODE, bool REF>
 __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_eu(2))) void k_mlp_train(
     const int8_t *__restrict__ boards, int64_t rows, int64_t n_boards, const int8_t *__restrict__ actions,
@@ -260,39 +283,40 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     float(*st)[kStash] = stash[wave];
-    // phase-2 weights of unit l = lane (actor and critic), and its gradient accumulators
-    float w1l[16], wc1l[16], w2l[4];
+    // phase-2 weights of unit l = lane in input pairs (2i, 2i + 1) -- every phase-2 FMA is a
+    // v_pk_fma_f32 over two inputs, whose values the LDS reads deliver as aligned pairs -- and its
+    // gradient accumulators
+    f32x2 wa[8], wc[8], w2l[2];
     const int pl = 32 * (lane >> 1) + (lane & 1);      // unit l's place in its pair's layer-1 block
 #pragma unroll
-    for (int f = 0; f < 16; f++) {
-        w1l[f] = w[kA1W + pl + 2 * f];
-        wc1l[f] = w[kC1W + pl + 2 * f];
+    for (int i = 0; i < 8; i++) {
+        wa[i] = f32x2{w[kA1W + pl + 4 * i], w[kA1W + pl + 4 * i + 2]};
+        wc[i] = f32x2{w[kC1W + pl + 4 * i], w[kC1W + pl + 4 * i + 2]};
     }
 #pragma unroll
-    for (int k = 0; k < 4; k++)
-        w2l[k] = w[kA2W + 8 * (lane >> 1) + 2 * k + (lane & 1)];
-    const float b1l = w[kA1B + lane], bc1l = w[kC1B + lane], wc2l = w[kC2W + lane];
+    for (int k = 0; k < 2; k++)
+        w2l[k] = f32x2{w[kA2W + 8 * (lane >> 1) + 4 * k + (lane & 1)], w[kA2W + 8 * (lane >> 1) + 4 * k + 2 + (lane & 1)]};
+    const float wc2l = w[kC2W + lane];
+    const f32x2 bl = f32x2{w[kA1B + lane], w[kC1B + lane]};
     // fp32 error bound of the unit's pre-activation: 16 roundings of partial sums below
-    // |b| + sum |w| max x, i.e. < 2^-20 (|b| + sum |w| max x); 2x margin
-    float s1l = 0.f, sc1l = 0.f;
+    // |b| + sum |w| max x, i.e. < 2^-20 (|b| + sum |w| max x); 2x margin, + 2^-21 for the rounding
+    // of the decision's own al - 3 (phase 2)
+    f32x2 sl = f32x2{0.f, 0.f};
 #pragma unroll
-    for (int f = 0; f < 16; f++) {
-        s1l += fabsf(w1l[f]);
-        sc1l += fabsf(wc1l[f]);
-    }
-    s1l *= 0x1p-19f;
-    sc1l *= 0x1p-19f;
-    const float e1l = fabsf(b1l) * 0x1p-19f, ec1l = fabsf(bc1l) * 0x1p-19f;
-    float g1[16], gc1[16], g2[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < 8; i++)
+        sl += f32x2{fabsf(wa[i].x) + fabsf(wa[i].y), fabsf(wc[i].x) + fabsf(wc[i].y)};
+    sl *= 0x1p-19f;
+    const f32x2 el = f32x2{fmaf(fabsf(bl.x), 0x1p-19f, 0x1p-21f), fmaf(fabsf(bl.y), 0x1p-19f, 0x1p-21f)};
+    f32x2 ga[8], gc[8], gbl = f32x2{0.f, 0.f}, g2l[2] = {f32x2{0.f, 0.f}, f32x2{0.f, 0.f}};
 #pragma unroll
-    for (int f = 0; f < 16; f++)
-        g1[f] = gc1[f] = 0.f;
-    float gb1 = 0.f, gbc1 = 0.f, gc2 = 0.f;
+    for (int i = 0; i < 8; i++)
+        ga[i] = gc[i] = f32x2{0.f, 0.f};
+    float gc2 = 0.f;
     // per-row-lane sums (reduced over the wave at the end)
     float gb2[4] = {0.f, 0.f, 0.f, 0.f}, gbc2 = 0.f, loss_a = 0.f, loss_c = 0.f;
     // fp32 error bound of a pre-ReLU logit: its own sum (64 products of |h| <= 6 in parity halves:
     // < 2^-18 (|b2| + 6 sum |W2[k][:]|)) plus the hidden units' errors carried through W2 (each
-    // < 2^-20 (|b1| + sum |W1[j][:]| max x), see s1l below); 2x-4x margins
+    // < 2^-20 (|b1| + sum |W1[j][:]| max x), see sl above); 2x-4x margins
     float zedge[4], zcarry[4], hb = 0.f, hw = 0.f;
     for (int j = 0; j < 64; j++) {
         float sw = 0.f;
@@ -410,15 +434,18 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
         // summed over the wave; lane 0 writes the row's dz through the exact ReLU decision
         for (uint64_t m = near_rows; m; m &= m - 1) {
             const int j = __builtin_ctzll(m);
-            double ad = b1l;
+            double ad = bl.x;
 #pragma unroll
-            for (int f = 0; f < 16; f++)
-                ad = __builtin_fma((double)w1l[f], (double)st[j][f], ad);
+            for (int i = 0; i < 8; i++) {
+                ad = __builtin_fma((double)wa[i].x, (double)st[j][2 * i], ad);
+                ad = __builtin_fma((double)wa[i].y, (double)st[j][2 * i + 1], ad);
+            }
             const double hd = ad < 0.0 ? 0.0 : (ad > 6.0 ? 6.0 : ad);
+            const double w2d[4] = {w2l[0].x, w2l[0].y, w2l[1].x, w2l[1].y};
             double t[4];
 #pragma unroll
             for (int k = 0; k < 4; k++) {
-                t[k] = (double)w2l[k] * hd;
+                t[k] = w2d[k] * hd;
 #pragma unroll
                 for (int o = 1; o < 64; o <<= 1)
                     t[k] += __shfl_xor(t[k], o);
@@ -435,73 +462,85 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
         if (near_rows)
             wave_lds_sync();
         // ---------------- phase 2: lane = hidden unit
+        // the ReLU6 decisions 0 < a < 6, i.e. |a - 3| < 3, are taken on the fp32 values; a row whose
+        // pre-activation lies within the fp32 error bound of 0 or 6 (min(|a|, |a - 6|) = ||a - 3| - 3|)
+        // is flagged, and after the row loop its decision is redone in fp64 and, where it differs,
+        // the row's term is moved (no branch in the row loop)
+        uint32_t flagged[2] = {0u, 0u};
 #pragma unroll 1
-        for (int j = 0; j < 64; j++) {
-            float xr[16];
+        for (int half = 0; half < 2; half++) {
+            uint32_t fl = 0u;
+#pragma unroll 2
+            for (int jj = 0; jj < 32; jj++) {
+                const int j = 32 * half + jj;
+                f32x2 xp[8];
+                const f32x2 ac = unit_preacts(st[j], wa, wc, bl, xp);
+                const float4 dz4 = *reinterpret_cast<const float4 *>(&st[j][16]);
+                const f32x2 dvm = *reinterpret_cast<const f32x2 *>(&st[j][20]);   // dv | max x
+                const f32x2 d = ac - f32x2{3.0f, 3.0f};
+                const f32x2 bound = __builtin_elementwise_fma(sl, f32x2{dvm.y, dvm.y}, el);
+                const int edge = (int)(fabsf(fabsf(d.x) - 3.0f) < bound.x) | (int)(fabsf(fabsf(d.y) - 3.0f) < bound.y);
+                fl = edge ? fl | (1u << jj) : fl;
+                const float hl = __builtin_amdgcn_fmed3f(ac.x, 0.0f, 6.0f), hcl = __builtin_amdgcn_fmed3f(ac.y, 0.0f, 6.0f);
+                const f32x2 sdh = w2l[0] * f32x2{dz4.x, dz4.y} + w2l[1] * f32x2{dz4.z, dz4.w};
+                const float dha = fabsf(d.x) < 3.0f ? sdh.x + sdh.y : 0.0f;
+                const float dhc = fabsf(d.y) < 3.0f ? wc2l * dvm.x : 0.0f;
 #pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const float4 t4 = *reinterpret_cast<const float4 *>(&st[j][4 * q]);
-                xr[4 * q] = t4.x, xr[4 * q + 1] = t4.y, xr[4 * q + 2] = t4.z, xr[4 * q + 3] = t4.w;
+                for (int i = 0; i < 8; i++) {
+                    ga[i] = __builtin_elementwise_fma(f32x2{dha, dha}, xp[i], ga[i]);
+                    gc[i] = __builtin_elementwise_fma(f32x2{dhc, dhc}, xp[i], gc[i]);
+                }
+                gbl += f32x2{dha, dhc};
+                g2l[0] = __builtin_elementwise_fma(f32x2{dz4.x, dz4.y}, f32x2{hl, hl}, g2l[0]);
+                g2l[1] = __builtin_elementwise_fma(f32x2{dz4.z, dz4.w}, f32x2{hl, hl}, g2l[1]);
+                gc2 = __builtin_fmaf(dvm.x, hcl, gc2);
             }
+            flagged[half] = fl;
+        }
+        // the flagged rows of this lane's unit (~1e-5 of the decisions; lanes diverge here)
+        for (uint64_t m = ((uint64_t)flagged[1] << 32) | flagged[0]; m; m &= m - 1) {
+            const int j = __builtin_ctzll(m);
+            f32x2 xp[8];
+            const f32x2 ac = unit_preacts(st[j], wa, wc, bl, xp);
             const float4 dz4 = *reinterpret_cast<const float4 *>(&st[j][16]);
             const float dvr = st[j][20];
-            // the four-chain FMA order of phase 1 (hidden_into), so the same values
-            float ca[4] = {b1l, 0.f, 0.f, 0.f}, cc[4] = {bc1l, 0.f, 0.f, 0.f};
+            double ad = bl.x, cd = bl.y;
 #pragma unroll
-            for (int f = 0; f < 16; f++) {
-                ca[f & 3] = __builtin_fmaf(w1l[f], xr[f], ca[f & 3]);
-                cc[f & 3] = __builtin_fmaf(wc1l[f], xr[f], cc[f & 3]);
+            for (int i = 0; i < 8; i++) {
+                ad = __builtin_fma((double)wa[i].x, (double)xp[i].x, ad);
+                ad = __builtin_fma((double)wa[i].y, (double)xp[i].y, ad);
+                cd = __builtin_fma((double)wc[i].x, (double)xp[i].x, cd);
+                cd = __builtin_fma((double)wc[i].y, (double)xp[i].y, cd);
             }
-            const float al = (ca[0] + ca[1]) + (ca[2] + ca[3]), cl = (cc[0] + cc[1]) + (cc[2] + cc[3]);
-            // the ReLU6 decisions on exact-enough values: within the fp32 error bound of 0 or 6
-            // (16 roundings of partial sums below sum |w| max x) the pre-activation is redone in fp64
-            const float xm = st[j][21];
-            bool ma = al > 0.0f && al < 6.0f, mc = cl > 0.0f && cl < 6.0f;
-            if (fminf(fabsf(al), fabsf(al - 6.0f)) < __builtin_fmaf(s1l, xm, e1l) ||
-                fminf(fabsf(cl), fabsf(cl - 6.0f)) < __builtin_fmaf(sc1l, xm, ec1l)) {
-                double ad = b1l, cd = bc1l;
+            const bool ma = ad > 0.0 && ad < 6.0, mc = cd > 0.0 && cd < 6.0;
+            const bool ma32 = fabsf(ac.x - 3.0f) < 3.0f, mc32 = fabsf(ac.y - 3.0f) < 3.0f;
+            const f32x2 sdh = w2l[0] * f32x2{dz4.x, dz4.y} + w2l[1] * f32x2{dz4.z, dz4.w};
+            // + the row's term where the exact decision is "on", - where the fp32 one was
+            const float dha = ma == ma32 ? 0.0f : (ma ? sdh.x + sdh.y : -(sdh.x + sdh.y));
+            const float dhc = mc == mc32 ? 0.0f : (mc ? wc2l * dvr : -(wc2l * dvr));
 #pragma unroll
-                for (int f = 0; f < 16; f++) {
-                    // converted here, behind an opaque copy: hoisted out of the row loop, 32 fp64
-                    // weight copies would stay live and spill
-                    float wa = w1l[f], wc = wc1l[f];
-                    asm volatile("" : "+v"(wa), "+v"(wc));
-                    ad = __builtin_fma((double)wa, (double)xr[f], ad);
-                    cd = __builtin_fma((double)wc, (double)xr[f], cd);
-                }
-                ma = ad > 0.0 && ad < 6.0;
-                mc = cd > 0.0 && cd < 6.0;
+            for (int i = 0; i < 8; i++) {
+                ga[i] = __builtin_elementwise_fma(f32x2{dha, dha}, xp[i], ga[i]);
+                gc[i] = __builtin_elementwise_fma(f32x2{dhc, dhc}, xp[i], gc[i]);
             }
-            const float hl = relu6(al), hcl = relu6(cl);
-            const float dh = ma ? w2l[0] * dz4.x + w2l[1] * dz4.y + w2l[2] * dz4.z + w2l[3] * dz4.w : 0.0f;
-            const float dhc = mc ? wc2l * dvr : 0.0f;
-#pragma unroll
-            for (int f = 0; f < 16; f++) {
-                g1[f] = __builtin_fmaf(dh, xr[f], g1[f]);
-                gc1[f] = __builtin_fmaf(dhc, xr[f], gc1[f]);
-            }
-            gb1 += dh;
-            gbc1 += dhc;
-            g2[0] = __builtin_fmaf(dz4.x, hl, g2[0]);
-            g2[1] = __builtin_fmaf(dz4.y, hl, g2[1]);
-            g2[2] = __builtin_fmaf(dz4.z, hl, g2[2]);
-            g2[3] = __builtin_fmaf(dz4.w, hl, g2[3]);
-            gc2 = __builtin_fmaf(dvr, hcl, gc2);
+            gbl += f32x2{dha, dhc};
         }
     }
     // ---------------- this wave's record (FlatParams order)
     float *rec = partials + ((int64_t)blockIdx.x * kTrainWaves + wave) * kRec;
 #pragma unroll
     for (int q = 0; q < 4; q++) {
-        *reinterpret_cast<float4 *>(rec + kA1W + 16 * lane + 4 * q) = make_float4(g1[4 * q], g1[4 * q + 1], g1[4 * q + 2], g1[4 * q + 3]);
+        *reinterpret_cast<float4 *>(rec + kA1W + 16 * lane + 4 * q) =
+            make_float4(ga[2 * q].x, ga[2 * q].y, ga[2 * q + 1].x, ga[2 * q + 1].y);
         *reinterpret_cast<float4 *>(rec + kC1W + 16 * lane + 4 * q) =
-            make_float4(gc1[4 * q], gc1[4 * q + 1], gc1[4 * q + 2], gc1[4 * q + 3]);
+            make_float4(gc[2 * q].x, gc[2 * q].y, gc[2 * q + 1].x, gc[2 * q + 1].y);
     }
-    rec[kA1B + lane] = gb1;
-    rec[kC1B + lane] = gbc1;
-#pragma unroll
-    for (int k = 0; k < 4; k++)
-        rec[kA2W + 64 * k + lane] = g2[k];
+    rec[kA1B + lane] = gbl.x;
+    rec[kC1B + lane] = gbl.y;
+    rec[kA2W + lane] = g2l[0].x;
+    rec[kA2W + 64 + lane] = g2l[0].y;
+    rec[kA2W + 128 + lane] = g2l[1].x;
+    rec[kA2W + 192 + lane] = g2l[1].y;
     rec[kC2W + lane] = gc2;
     const float s0 = wave_sum(gb2[0]), s1 = wave_sum(gb2[1]), s2 = wave_sum(gb2[2]), s3 = wave_sum(gb2[3]);
     const float sc = wave_sum(gbc2), la = wave_sum(loss_a), lc = wave_sum(loss_c);
