@@ -10,7 +10,6 @@
 
 #include <cstdint>
 #include <cstdio>
-#include <cstdlib>
 #include <string>
 
 #include "../../include/rein48.h"
@@ -257,8 +256,7 @@ __device__ __forceinline__ bool planes_aligned(const void *actions, const void *
 // bytes; a wave's pairs are one contiguous 2 KiB) and ONE Philox call serves both boards. Full,
 // pair-aligned tiles take a straight-line path; the grid's partial last tile and envs whose
 // global board ids start odd (pairs straddling the tile) take the guarded per-board path.
-// NT: non-temporal board loads and stores (streaming past the caches; A/B of the 2^26-board HBM point)
-template <bool RANDOM, bool AUTO_RESET, bool REWARD, bool NT = false>
+template <bool RANDOM, bool AUTO_RESET, bool REWARD>
 __global__ __launch_bounds__(kBlock) void k_step(int8_t *boards, int64_t n, int64_t gid0, uint32_t k0, uint32_t k1,
                                                  uint32_t step, int8_t *__restrict__ actions,
                                                  uint8_t *__restrict__ done, uint8_t *__restrict__ changed,
@@ -272,16 +270,7 @@ __global__ __launch_bounds__(kBlock) void k_step(int8_t *boards, int64_t n, int6
     load_orient_table(tab);
     if ((int64_t)(blockIdx.x + 1) * kTile <= n && (gid0 & 1) == 0 &&
         planes_aligned(actions, done, changed, reward, score)) {
-        Board be, bo;
-        if (NT) {
-            const u32x4 ve = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(boards + 16 * i));
-            const u32x4 vo = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(boards + 16 * i + 16));
-            be = Board{ve.x, ve.y, ve.z, ve.w};
-            bo = Board{vo.x, vo.y, vo.z, vo.w};
-        } else {
-            be = load_board(boards, i);
-            bo = load_board(boards, i + 1);
-        }
+        Board be = load_board(boards, i), bo = load_board(boards, i + 1);
         uint32_t ae = 0, ao = 0;
         if (!RANDOM) {
             const uint16_t a2 = *reinterpret_cast<const uint16_t *>(actions + i);
@@ -299,17 +288,7 @@ __global__ __launch_bounds__(kBlock) void k_step(int8_t *boards, int64_t n, int6
         LaneOut ro = step_lane_lines<RANDOM, AUTO_RESET, REWARD>(bo, obo, tab, ao, dd, want_score);
         re.b = r48::reorient(be, orient_at(tab, obe));
         ro.b = r48::reorient(bo, orient_at(tab, obo));
-        if (NT && RANDOM && !REWARD && !changed && !reward && !score) {   // the bench's planes
-            __builtin_nontemporal_store(u32x4{re.b.w0, re.b.w1, re.b.w2, re.b.w3}, reinterpret_cast<u32x4 *>(boards + 16 * i));
-            __builtin_nontemporal_store(u32x4{ro.b.w0, ro.b.w1, ro.b.w2, ro.b.w3},
-                                        reinterpret_cast<u32x4 *>(boards + 16 * i + 16));
-            if (actions)
-                __builtin_nontemporal_store((uint16_t)((re.a & 0xffu) | (ro.a << 8)), reinterpret_cast<uint16_t *>(actions + i));
-            if (done)
-                __builtin_nontemporal_store((uint16_t)(re.done | (ro.done << 8)), reinterpret_cast<uint16_t *>(done + i));
-        } else {
-            emit_pair<RANDOM, REWARD>(re, ro, i, boards, actions, done, changed, reward, score);
-        }
+        emit_pair<RANDOM, REWARD>(re, ro, i, boards, actions, done, changed, reward, score);
     } else {
         for (int j = 0; j < 2; j++) {
             if (i + j < n) {
@@ -1037,14 +1016,6 @@ void launch_steps(r48_env *env, int32_t n_steps, int8_t *actions, uint32_t flags
                            env->n, env->gid0, k0, k1, env->step_ctr, n_steps, actions, done, changed, reward, score,
                            env->err, (int8_t *)nullptr, (uint8_t *)nullptr);
     };
-    static const bool nt = [] {
-        const char *v = getenv("R48_STEP_NT");
-        return v && atoi(v) != 0;
-    }();
-    if (nt && n_steps == 1 && rnd && ar && !rw) {
-        one(k_step<true, true, false, true>);
-        return;
-    }
 #define R48_GO(RN, AR, RW) \
     (n_steps == 1 ? one(k_step<RN, AR, RW>) : many(k_step_n<RN, AR, RW, kStepNP>))
     if (rnd) {
