@@ -41,10 +41,12 @@ extern "C" {
 
 /* Version of the Philox-mode draw contract (which Philox words decide action, spawn and reset;
  * DESIGN.md section 7, restated in oracle/r48_oracle.c). A seed replays the same trajectories
- * only under the same version: version 2 (round 2) counts the spawn rank over the blanks in the
- * line order of the action, version 1 counted them row-major. The injected-draw path
- * (r48_env_step_with_draws) is the reference's row-major rule under every version. */
-#define R48_DRAW_CONTRACT 2
+ * only under the same version: version 3 (round 4) draws the step words from Philox4x32-7
+ * (resets keep Philox4x32-10), version 2 (round 2) drew them from Philox4x32-10 and counts the
+ * spawn rank over the blanks in the line order of the action, version 1 counted them row-major.
+ * The injected-draw path (r48_env_step_with_draws) is the reference's row-major rule under every
+ * version. */
+#define R48_DRAW_CONTRACT 3
 
 typedef struct r48_env r48_env;
 

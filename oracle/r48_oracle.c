@@ -363,27 +363,30 @@ ORC_API int orc_pyrand_episode(orc_mt *s, int max_steps, int8_t *start, int32_t 
 }
 
 /* ------------------------------------------------------------------------------------
- * Philox4x32-10 (Salmon et al., SC'11) -- the production RNG of the HIP kernel. Only the
+ * Philox4x32 (Salmon et al., SC'11) -- the production RNG of the HIP kernel. Only the
  * build defines how its words are used (the reference has no counter-based RNG); this is
- * the specification the kernel must match bit-for-bit (contract version 2
+ * the specification the kernel must match bit-for-bit (contract version 3
  * = R48_DRAW_CONTRACT in include/rein48.h):
  *   key = {seed lo, seed hi}
- *   step:  boards with global ids 2q and 2q+1 share ctr = {q lo, q hi, step, 0x2048}; the even
+ *   step:  Philox4x32-7; boards with global ids 2q and 2q+1 share ctr = {q lo, q hi, step, 0x2048}; the even
  *          board takes (x, y) = (w0, w1), the odd one (w2, w3). Per board: action x >> 30 in
  *          random-policy mode; spawn a 4 iff (x & 0x3FFFFFFF) < 0x06666666; spawn rank
  *          mulhi(y, n_blank) with the blanks counted in LINE order of the action
  *          (orc_spawn_lines); auto-reset tile: cell y >> 28 (row-major), a 4 iff
  *          (y & 0x0FFFFFFF) < 0x0199999A (y is free then: a step that ends done spawned into
  *          its last blank, mulhi(y, 1) = 0, or spawned nothing).
- *          Contract version 1 (round 1) counted the spawn rank in row-major order: seeds saved
- *          under it do not replay under version 2.
- *   reset: ctr = {gid lo, gid hi, reset_ctr, 0x5E7} -> cell w0 >> 28, four iff w1 < 0x1999999A
+ *          Contract version 1 (round 1) counted the spawn rank in row-major order, version 2
+ *          (rounds 2-3) drew the step words from Philox4x32-10: seeds saved under either do not
+ *          replay under version 3.
+ *   reset: Philox4x32-10, ctr = {gid lo, gid hi, reset_ctr, 0x5E7} -> cell w0 >> 28, four iff w1 < 0x1999999A
  * ---------------------------------------------------------------------------------- */
-ORC_API void orc_philox4x32_10(const uint32_t ctr_in[4], const uint32_t key_in[2], uint32_t out[4])
+/* Philox4x32 with `rounds` rounds (Salmon et al., SC'11): 10 is Random123's default (pinned by its
+ * KAT vectors, tests/test_oracle_pinned.py), the env step's draws use 7 (contract version 3) */
+ORC_API void orc_philox4x32_r(const uint32_t ctr_in[4], const uint32_t key_in[2], uint32_t out[4], int rounds)
 {
     uint32_t c0 = ctr_in[0], c1 = ctr_in[1], c2 = ctr_in[2], c3 = ctr_in[3];
     uint32_t k0 = key_in[0], k1 = key_in[1];
-    for (int r = 0; r < 10; r++) {
+    for (int r = 0; r < rounds; r++) {
         uint64_t p0 = (uint64_t)0xD2511F53u * c0;
         uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
         uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
@@ -397,6 +400,11 @@ ORC_API void orc_philox4x32_10(const uint32_t ctr_in[4], const uint32_t key_in[2
     out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
 }
 
+ORC_API void orc_philox4x32_10(const uint32_t ctr_in[4], const uint32_t key_in[2], uint32_t out[4])
+{
+    orc_philox4x32_r(ctr_in, key_in, out, 10);
+}
+
 #define ORC_FLAG_AUTO_RESET 1u
 #define ORC_FLAG_RANDOM_POLICY 2u
 #define ORC_FLAG_MERGE_REWARD 4u
@@ -407,7 +415,7 @@ static inline uint32_t mulhi32(uint32_t a, uint32_t b)
 }
 
 /* Batched step in the kernel's Philox mode (r48_env_step; draw contract in DESIGN.md section 7):
- * boards with global ids 2q and 2q+1 share Philox4x32-10({q lo, q hi, step, 0x2048}); the even
+ * boards with global ids 2q and 2q+1 share Philox4x32-7({q lo, q hi, step, 0x2048}); the even
  * board takes (x, y) = (w0, w1), the odd one (w2, w3). action = x >> 30, spawn a 4 iff
  * (x & 0x3FFFFFFF) < 0x06666666, blank rank = mulhi(y, n_blank) with the blanks in line order
  * (orc_spawn_lines), auto-reset cell = y >> 28 (row-major) with
@@ -424,7 +432,7 @@ ORC_API int64_t orc_step_philox(int8_t *boards, int64_t n, uint64_t seed, int64_
         /* boards 2q and 2q+1 share one Philox call; the even one takes (w0, w1), the odd one (w2, w3) */
         uint64_t gid = (uint64_t)(board_offset + i), q = gid >> 1;
         uint32_t ctr[4] = {(uint32_t)q, (uint32_t)(q >> 32), step, 0x2048u}, w[4];
-        orc_philox4x32_10(ctr, key, w);
+        orc_philox4x32_r(ctr, key, w, 7);
         const uint32_t x = w[2 * (gid & 1)], y = w[2 * (gid & 1) + 1];
         int a;
         if (flags & ORC_FLAG_RANDOM_POLICY) {

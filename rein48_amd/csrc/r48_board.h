@@ -324,13 +324,14 @@ R48_HD uint32_t xor3_uniform(uint32_t a, uint32_t b, uint32_t k)
 #endif
 }
 
-// ---- Philox4x32-10 (Salmon, Moraes, Dror, Shaw, SC'11) -----------------------------
+// ---- Philox4x32-R (Salmon, Moraes, Dror, Shaw, SC'11) -----------------------------
 // Round 0 stays in C so the compiler can move its wave-uniform counter words to the SALU;
-// rounds 1-9 fold each round's two XORs into one v_bitop3_b32.
-R48_HD void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1)
+// rounds 1.. fold each round's two XORs into one v_bitop3_b32.
+template <int ROUNDS>
+R48_HD void philox4x32_r(uint32_t c[4], uint32_t k0, uint32_t k1)
 {
     R48_UNROLL
-    for (int i = 0; i < 10; i++) {
+    for (int i = 0; i < ROUNDS; i++) {
         const uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
         const uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
         uint32_t n0, n2;
@@ -356,8 +357,14 @@ R48_HD void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1)
     }
 }
 
+R48_HD void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) { philox4x32_r<10>(c, k0, k1); }
+
 // Draw-word contract (DESIGN.md "Philox mode"; restated in oracle/r48_oracle.c)
 static constexpr uint32_t kStepTag = 0x2048u;
+// the env step's draws use Philox4x32-7, the fewest rounds the Philox authors found to pass
+// BigCrush (draw contract version 3, round 4: the step's Philox was ~1/6 of the env kernels' VALU
+// issue); every other draw (reset, fill, sampling, replay) keeps the default 10 rounds
+static constexpr int kStepRounds = 7;
 static constexpr uint32_t kResetTag = 0x5E7u;
 static constexpr uint32_t kFillTag = 0xF111u;   // synthetic start boards (r48_env_fill_random)
 static constexpr uint32_t kFourThresh = 0x1999999Au;     // P(4) = 0.1   (GameClient.py:125)
@@ -365,13 +372,13 @@ static constexpr uint32_t kFourThresh30 = 0x06666666u;   // same on 30 bits (P =
 static constexpr uint32_t kFourThresh28 = 0x0199999Au;   // same on 28 bits
 
 // The env step's draw words of board `gid` at step `step` (the k_step contract of r48_env.hip,
-// DESIGN.md section 7): boards 2q, 2q + 1 share Philox4x32-10(key, {q lo, q hi, step, kStepTag});
+// DESIGN.md section 7): boards 2q, 2q + 1 share Philox4x32-7(key, {q lo, q hi, step, kStepTag});
 // the even board takes (x, y) = (w0, w1), the odd one (w2, w3).
 R48_HD void step_draw(uint64_t gid, uint32_t step, uint32_t k0, uint32_t k1, uint32_t &x, uint32_t &y)
 {
     const uint64_t q = gid >> 1;
     uint32_t w[4] = {(uint32_t)q, (uint32_t)(q >> 32), step, kStepTag};
-    philox4x32_10(w, k0, k1);
+    philox4x32_r<kStepRounds>(w, k0, k1);
     x = (gid & 1u) ? w[2] : w[0];
     y = (gid & 1u) ? w[3] : w[1];
 }

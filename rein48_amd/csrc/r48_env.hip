@@ -57,7 +57,7 @@ __device__ __forceinline__ void count_bad(bool bad, unsigned long long *err, uns
 
 // ---------------------------------------------------------------- Philox-mode step
 // Draw contract (oracle/r48_oracle.c orc_step_philox): boards 2q and 2q+1
-// (global ids) share one Philox4x32-10(key = seed, counter = {q lo, q hi, step, kStepTag});
+// (global ids) share one Philox4x32-7(key = seed, counter = {q lo, q hi, step, kStepTag});
 // board 2q takes (x, y) = (w0, w1), board 2q+1 takes (w2, w3). Per board: action = x >> 30
 // (random policy), spawn tile 4 iff (x & 0x3FFFFFFF) < kFourThresh30, blank rank =
 // mulhi(y, n_blank); auto-reset cell = y >> 28, 4 iff (y & 0x0FFFFFFF) < kFourThresh28. A board
@@ -70,8 +70,8 @@ struct Draw {
 __device__ __forceinline__ void pair_draws(uint64_t q, uint32_t step, uint32_t k0, uint32_t k1, Draw &even,
                                            Draw &odd)
 {
-    uint32_t w[4];
-    philox_words(w, q, step, r48::kStepTag, k0, k1);
+    uint32_t w[4] = {(uint32_t)q, (uint32_t)(q >> 32), step, r48::kStepTag};
+    r48::philox4x32_r<r48::kStepRounds>(w, k0, k1);
     even = Draw{w[0], w[1]};
     odd = Draw{w[2], w[3]};
 }

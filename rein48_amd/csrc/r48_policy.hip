@@ -228,7 +228,7 @@ __device__ __forceinline__ void pair_block_draws(uint64_t q, uint32_t step, uint
                                                  uint2 &d0, uint2 &d1)
 {
     uint32_t w[4] = {(uint32_t)q, (uint32_t)(q >> 32), step + (m & 1u), r48::kStepTag};
-    r48::philox4x32_10(w, k0, k1);
+    r48::philox4x32_r<r48::kStepRounds>(w, k0, k1);
     auto swap = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false); };
     // the even lane holds call(step) and gives words 2, 3 (its partner's step draws); the odd lane
     // holds call(step + 1) and gives words 0, 1 (its partner's step + 1 draws)

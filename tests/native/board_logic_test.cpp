@@ -143,11 +143,11 @@ int main()
         for (uint32_t step = 7; step < 10; step++) {
             orc_step_philox(ob, n, seed, off, step, 1u | 2u, act, done, chg, rw, sc);
             for (int i = 0; i < n; i++) {
-                // pair contract: boards 2q, 2q+1 share one Philox call; even takes (w0, w1), odd (w2, w3)
-                const uint64_t gid = (uint64_t)(off + i), q = gid >> 1;
-                uint32_t w[4] = {(uint32_t)q, (uint32_t)(q >> 32), step, r48::kStepTag};
-                r48::philox4x32_10(w, (uint32_t)seed, (uint32_t)(seed >> 32));
-                const uint32_t x = w[2 * (gid & 1)], y = w[2 * (gid & 1) + 1];
+                // pair contract (r48::step_draw): boards 2q, 2q+1 share one Philox4x32-7 call; even
+                // takes (w0, w1), odd (w2, w3)
+                const uint64_t gid = (uint64_t)(off + i);
+                uint32_t x, y;
+                r48::step_draw(gid, step, (uint32_t)seed, (uint32_t)(seed >> 32), x, y);
                 const uint32_t a = x >> 30;
                 CHECK((int8_t)a == act[i], "philox action i=%d", i);
                 Board r = load(boards + 16 * i);
@@ -200,11 +200,11 @@ int main()
         for (int i = 0; i < n; i++) {
             Board L = load(boards + 16 * i);
             uint32_t o = 0;
-            const uint64_t gid = (uint64_t)(off + i), q = gid >> 1;
+            const uint64_t gid = (uint64_t)(off + i);
             for (uint32_t step = 0; step < (uint32_t)steps; step++) {
-                uint32_t w[4] = {(uint32_t)q, (uint32_t)(q >> 32), 100 + step, r48::kStepTag};
-                r48::philox4x32_10(w, (uint32_t)seed, (uint32_t)(seed >> 32));
-                const uint32_t x = w[2 * (gid & 1)], y = w[2 * (gid & 1) + 1], a = x >> 30;
+                uint32_t x, y;
+                r48::step_draw(gid, 100 + step, (uint32_t)seed, (uint32_t)(seed >> 32), x, y);
+                const uint32_t a = x >> 30;
                 L = r48::reorient(L, r48::kOrient[4 * o + a]);
                 o = a;
                 const r48::StepOut s = r48::step_lines<false, true>(L, a, y, (x & 0x3FFFFFFFu) < r48::kFourThresh30);
