@@ -548,7 +548,7 @@ def main():
         "vs_baseline": None,
         "dtype": "int8",
         "data": "synthetic: start boards with each cell empty w.p. 1/2 else exponent ~U{1..7} (Philox, "
-                "r48_env_fill_random), in-kernel uniform random policy and spawns from Philox4x32-10, "
+                "r48_env_fill_random), in-kernel uniform random policy and spawns from Philox4x32-7 (draw contract 3), "
                 "auto-reset on game over",
         "config": {"workload": "BASELINE configs[1]: 2^20 4x4 int8 boards per GPU, random policy, env-only",
                    "boards_per_gpu": n, "global_boards": n * world,

@@ -3,7 +3,7 @@
 // Hot path: Game.step (nevertiree/Rein48 game/GameClient.py:40-51) over millions of
 // int8[16] boards in lockstep. One board per lane: a 16-B global_load_dwordx4 per lane
 // (1 KiB contiguous per wave), the step on four VGPRs (r48_board.h), a 16-B store back.
-// Spawn draws come from a per-lane Philox4x32-10 keyed by (seed, global board id) with
+// Spawn draws come from a per-lane Philox4x32-7 keyed by (seed, global board id) with
 // the step counter -- no RNG state lives in HBM. HBM traffic per board-step (random policy):
 // 16 B board in + 16 B board out + 1 B action out + 1 B done out = 34 B.
 #include <hip/hip_runtime.h>

@@ -5,7 +5,7 @@ N int8[16] boards in HBM (row-major cells, exponent e = tile 2^e, 0 empty) and a
 of them per call through librein48.so's gfx950 kernels. Boards, actions and flags are torch
 tensors on the env's GPU; every call is asynchronous on torch's current stream.
 
-Spawn randomness (GameClient.py:121,125) comes from a per-lane Philox4x32-10 keyed by
+Spawn randomness (GameClient.py:121,125) comes from a per-lane Philox4x32-7 keyed by
 (seed, global board id): a VecGame sharded across ranks with board_offset = rank * N is
 bit-identical to one unsharded VecGame.
 """
