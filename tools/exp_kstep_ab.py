@@ -1,8 +1,9 @@
 """GPU experiment: k_step (one step per launch, boards through HBM) at 2^26 boards -- the HBM-honest
-point -- for the launch option the environment selects (e.g. R48_STEP_NT=1); median device time
-per launch over 3 rounds of 30 back-to-back launches after a settle, and a digest of the boards.
+point -- of one library build (default: the product library; a variant from tools/build_variant.sh
+to A/B); median device time per launch over 3 rounds of 30 back-to-back launches after a settle,
+and a digest of the boards.
 
-    R48_STEP_NT=1 python tools/exp_kstep_ab.py"""
+    python tools/exp_kstep_ab.py [lib.so]"""
 import os
 import sys
 import time
@@ -10,7 +11,10 @@ import time
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from rein48_amd import VecGame  # noqa: E402
+from rein48_amd import VecGame, _lib  # noqa: E402
+
+if len(sys.argv) > 1:
+    _lib.LIB_PATH, _lib._lib = sys.argv[1], None
 
 dev = "cuda:0"
 n = 1 << 26
@@ -33,5 +37,5 @@ for _ in range(3):
 ms = sorted(per)[1]
 digest = int((env.boards.view(torch.int32).long() * 2654435761).sum()) & 0xFFFFFFFF
 print("%s k_step 2^26: %.1f us/launch = %.0f GB/s (34 B/board) = %.3f of 8 TB/s | rounds %s | digest %08x"
-      % ({k: v for k, v in os.environ.items() if k.startswith("R48_")}, ms * 1e3, n * 34 / (ms * 1e-3) / 1e9,
+      % (os.path.basename(_lib.LIB_PATH), ms * 1e3, n * 34 / (ms * 1e-3) / 1e9,
          n * 34 / (ms * 1e-3) / 8e12, ["%.1f" % (p * 1e3) for p in per], digest), flush=True)
