@@ -242,6 +242,11 @@ __device__ __forceinline__ void wave_lds_sync()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+__device__ __forceinline__ float uniform(float v)
+{
+    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
+}
+
 __device__ __forceinline__ float wave_sum(float v)
 {
 #pragma unroll
@@ -317,6 +322,7 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
     // fp32 error bound of a pre-ReLU logit: its own sum (64 products of |h| <= 6 in parity halves:
     // < 2^-18 (|b2| + 6 sum |W2[k][:]|)) plus the hidden units' errors carried through W2 (each
     // < 2^-20 (|b1| + sum |W1[j][:]| max x), see sl above); 2x-4x margins
+    // (wave-uniform: kept in SGPRs)
     float zedge[4], zcarry[4], hb = 0.f, hw = 0.f;
     for (int j = 0; j < 64; j++) {
         float sw = 0.f;
@@ -330,9 +336,11 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
         float sa = 0.f;
         for (int j = 0; j < 64; j++)
             sa += fabsf(w[kA2W + 8 * (j >> 1) + 2 * k + (j & 1)]);
-        zedge[k] = (fabsf(w[kA2B + k]) + 6.0f * sa) * 0x1p-16f;
-        zcarry[k] = sa * 0x1p-19f;
+        zedge[k] = uniform((fabsf(w[kA2B + k]) + 6.0f * sa) * 0x1p-16f);
+        zcarry[k] = uniform(sa * 0x1p-19f);
     }
+    hb = uniform(hb);
+    hw = uniform(hw);
 
     const int64_t n_tiles = (rows + 63) / 64;
     const int64_t stride = (int64_t)gridDim.x * kTrainWaves;
@@ -343,7 +351,14 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
         const int64_t rr = live ? r : rows - 1;      // padding lanes: a valid row with weight 0
         float x[16], zr[4], v;
         board_inputs<MODE>(load_board(boards, rr), x);
-        float xmax;
+        const float xmax = fmaxf(fmaxf(fmaxf(fmaxf(x[0], x[1]), fmaxf(x[2], x[3])), fmaxf(fmaxf(x[4], x[5]), fmaxf(x[6], x[7]))),
+                                 fmaxf(fmaxf(fmaxf(x[8], x[9]), fmaxf(x[10], x[11])), fmaxf(fmaxf(x[12], x[13]), fmaxf(x[14], x[15]))));
+        // the row's inputs go to the stash at once (they are dead after the forward)
+        wave_lds_sync();   // the previous tile's phase 2 has read the stash
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            *reinterpret_cast<float4 *>(&st[lane][4 * q]) = make_float4(x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]);
+        st[lane][21] = xmax;
         {
             const float *wp = w;
             f32x2 acc[4];
@@ -354,9 +369,6 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
             f32x2 c[1];
             hidden_into<1>(wp, kC1W, kC1B, kC2W, x, c);
             v = wp[kC2B] + (c[0].x + c[0].y);
-            xmax = fmaxf(fmaxf(fmaxf(fmaxf(x[0], x[1]), fmaxf(x[2], x[3])), fmaxf(fmaxf(x[4], x[5]), fmaxf(x[6], x[7]))),
-                                     fmaxf(fmaxf(fmaxf(x[8], x[9]), fmaxf(x[10], x[11])), fmaxf(fmaxf(x[12], x[13]), fmaxf(x[14], x[15]))));
-
         }
         const float wt = live ? wn[rr] : 0.0f;
         const float tgt = targets[rr];
@@ -420,13 +432,8 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
         }
         const uint64_t near_rows = __ballot(near);
         gbc2 += dv;
-        wave_lds_sync();   // the previous tile's phase 2 has read the stash
-#pragma unroll
-        for (int q = 0; q < 4; q++)
-            *reinterpret_cast<float4 *>(&st[lane][4 * q]) = make_float4(x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]);
         *reinterpret_cast<float4 *>(&st[lane][16]) = make_float4(dzm[0], dzm[1], dzm[2], dzm[3]);
         st[lane][20] = dv;
-        st[lane][21] = xmax;
         if (near_rows)
             *reinterpret_cast<float4 *>(&st[lane][24]) = make_float4(dz[0], dz[1], dz[2], dz[3]);
         wave_lds_sync();
