@@ -130,6 +130,7 @@ def _load_profile(name):
 
 SETTLE_S = 0.3   # minimum untimed stepping before a timed region: GPU clocks ramp over ~20 ms+
 SYNC_POLL = False  # --sync: poll the region's last HIP event before the closing synchronize
+CLOSE_DEVICE = False  # --close device: t1 after torch.cuda.synchronize() instead of the last event's wait
 
 
 def _now():
@@ -181,7 +182,10 @@ def timed_steps(env, plan, W, chunk, world, dev):
         last = ev[-1][1]
         while not last.query():
             pass
-    ev[-1][1].synchronize()          # the region's last event: every step of every call is done
+    if CLOSE_DEVICE:
+        torch.cuda.synchronize(dev)      # the device is idle: every step of every call is done
+    else:
+        ev[-1][1].synchronize()          # the region's last event: every step of every call is done
     t1 = _now()
     torch.cuda.synchronize(dev)
     skew = 0.0
@@ -477,7 +481,7 @@ def hip_schedule_spin(local):
 
 
 def main():
-    global SYNC_POLL, SETTLE_S
+    global SYNC_POLL, SETTLE_S, CLOSE_DEVICE
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=6000)
@@ -496,8 +500,12 @@ def main():
                     help="end of the timed region: spin on its last event, then synchronize (poll), only "
                          "synchronize (block), or synchronize with the HIP runtime set to spin-wait "
                          "(hipDeviceScheduleSpin) instead of sleeping (spin)")
+    ap.add_argument("--close", choices=("event", "device"), default="event",
+                    help="end of the timed region: wait on the region's last HIP event (event) or on the "
+                         "device (torch.cuda.synchronize) before t1")
     args = ap.parse_args()
     SYNC_POLL = args.sync == "poll"
+    CLOSE_DEVICE = args.close == "device"
     SETTLE_S = args.settle
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
