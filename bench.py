@@ -130,6 +130,7 @@ def _load_profile(name):
 
 SETTLE_S = 0.3   # minimum untimed stepping before a timed region: GPU clocks ramp over ~20 ms+
 SYNC_POLL = False  # --sync: poll the region's last HIP event before the closing synchronize
+DRY_PASSES = 3  # --dry-passes: untimed passes through the region's exact host path before t0
 CLOSE_DEVICE = False  # --close device: t1 after torch.cuda.synchronize() instead of the last event's wait
 
 
@@ -154,15 +155,17 @@ def timed_steps(env, plan, W, chunk, world, dev):
         torch.cuda.synchronize(dev)
     s = torch.cuda.current_stream(dev)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in plan]
-    # one untimed pass through the region's exact host path (event records, the calls, the closing
+    # untimed passes through the region's exact host path (event records, the calls, the closing
     # event wait): torch creates the HIP events at their first record, which does not belong in the
-    # region (a first-pass host effect beyond that was not measurable: tools/show_bench20.py runs)
-    for (a, b), c in zip(ev, plan):
-        a.record(s)
-        env.step_n(c, auto_reset=True)
-        b.record(s)
-    ev[-1][1].synchronize()
-    torch.cuda.synchronize(dev)
+    # region, and the first pass of that host path in a process runs slower than later ones (launch
+    # path 7.4 vs ~5 us, tools/exp_first_region.py; profiles/r04/env/first_region_probe.txt)
+    for _ in range(max(1, DRY_PASSES)):
+        for (a, b), c in zip(ev, plan):
+            a.record(s)
+            env.step_n(c, auto_reset=True)
+            b.record(s)
+        ev[-1][1].synchronize()
+        torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
         torch.cuda.synchronize(dev)          # the barrier's own device work done before t0
@@ -170,12 +173,18 @@ def timed_steps(env, plan, W, chunk, world, dev):
     # device time it brackets is the launch's own plus the launch latency (conservative), and its
     # host-side cost does not delay the launch (tools/exp_sync.py: ~1-3 us of a ~95 us region)
     ev[0][0].record(s)
-    t0 = _now()
-    for k, ((a, b), c) in enumerate(zip(ev, plan)):
-        if k:
-            a.record(s)
-        env.step_n(c, auto_reset=True)
-        b.record(s)
+    if len(plan) == 1:   # the driver's region: one call
+        last = ev[0][1]
+        t0 = _now()
+        env.step_n(plan[0], auto_reset=True)
+        last.record(s)
+    else:
+        t0 = _now()
+        for k, ((a, b), c) in enumerate(zip(ev, plan)):
+            if k:
+                a.record(s)
+            env.step_n(c, auto_reset=True)
+            b.record(s)
     if SYNC_POLL:
         # spin on the last event instead of sleeping in the driver's blocking wait: a ~80 us
         # region otherwise measures the wake-up jitter of the waiting thread
@@ -481,7 +490,7 @@ def hip_schedule_spin(local):
 
 
 def main():
-    global SYNC_POLL, SETTLE_S, CLOSE_DEVICE
+    global SYNC_POLL, SETTLE_S, CLOSE_DEVICE, DRY_PASSES
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=6000)
@@ -503,8 +512,11 @@ def main():
     ap.add_argument("--close", choices=("event", "device"), default="event",
                     help="end of the timed region: wait on the region's last HIP event (event) or on the "
                          "device (torch.cuda.synchronize) before t1")
+    ap.add_argument("--dry-passes", type=int, default=DRY_PASSES,
+                    help="untimed passes through the timed region's exact host path before t0")
     args = ap.parse_args()
     SYNC_POLL = args.sync == "poll"
+    DRY_PASSES = args.dry_passes
     CLOSE_DEVICE = args.close == "device"
     SETTLE_S = args.settle
 

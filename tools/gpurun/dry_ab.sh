@@ -1,0 +1,9 @@
+#!/bin/bash
+# bench.py --steps 20: untimed passes of the region's host path before t0, 1 (round 3) vs 3, processes
+# alternated; prints value, wall / device time and repeat_5 of each run.
+set -o pipefail
+O=gpurun_out/dry_ab; mkdir -p $O
+for i in 1 2 3 4; do for d in 1 3; do
+  timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-extras --dry-passes $d > $O/b_${d}_$i.json 2>> $O/err.txt || exit 1
+  python -c "import json; r=json.load(open('$O/b_${d}_$i.json')); print('dry $d', '%.1f G' % (r['value']/1e9), 'wall %.1f us dev %.1f us' % (r['roofline']['wall_ms_timed']*1e3, r['roofline']['device_ms_timed']*1e3), 'repeat_5', [round(v/1e9) for v in r['repeat_5']['values']])" | tee -a $O/ab.txt
+done; done

@@ -1,0 +1,8 @@
+#!/bin/bash
+# bench.py --steps 20: settle (untimed stepping before the region) 0.3 s vs 1.5 s, processes alternated.
+set -o pipefail
+O=gpurun_out/settle_ab; mkdir -p $O
+for i in 1 2 3 4; do for d in ${SETTLES:-0.3 1.5}; do
+  timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-extras --settle $d > $O/b_${d}_$i.json 2>> $O/err.txt || exit 1
+  python -c "import json; r=json.load(open('$O/b_${d}_$i.json')); print('settle $d', '%.1f G' % (r['value']/1e9), 'wall %.1f us dev %.1f us' % (r['roofline']['wall_ms_timed']*1e3, r['roofline']['device_ms_timed']*1e3), 'repeat_5', [round(v/1e9) for v in r['repeat_5']['values']])" | tee -a $O/ab.txt
+done; done
