@@ -93,6 +93,33 @@ __device__ __forceinline__ void hidden_into(const float *__restrict__ w, int w1,
     }
 }
 
+// hidden_into for the actor (4 outputs) and the critic (1 output) in ONE pair loop: two independent
+// FMA chains per trip under one round of scalar loads (the update's forward, where the latency of the
+// loads is exposed at two waves per SIMD)
+__device__ __forceinline__ void hidden_both(const float *__restrict__ w, const float (&x)[16], f32x2 (&acc)[4], f32x2 &cv)
+{
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+        acc[k] = f32x2{0.0f, 0.0f};
+    cv = f32x2{0.0f, 0.0f};
+#pragma unroll 1
+    for (int p = 0; p < 32; p++) {
+        f32x2 ca[4] = {pair_at(w, kA1B + 2 * p), f32x2{0.0f, 0.0f}, f32x2{0.0f, 0.0f}, f32x2{0.0f, 0.0f}};
+        f32x2 cc[4] = {pair_at(w, kC1B + 2 * p), f32x2{0.0f, 0.0f}, f32x2{0.0f, 0.0f}, f32x2{0.0f, 0.0f}};
+#pragma unroll
+        for (int f = 0; f < 16; f++) {
+            ca[f & 3] = __builtin_elementwise_fma(pair_at(w, kA1W + 32 * p + 2 * f), f32x2{x[f], x[f]}, ca[f & 3]);
+            cc[f & 3] = __builtin_elementwise_fma(pair_at(w, kC1W + 32 * p + 2 * f), f32x2{x[f], x[f]}, cc[f & 3]);
+        }
+        const f32x2 a = (ca[0] + ca[1]) + (ca[2] + ca[3]), c = (cc[0] + cc[1]) + (cc[2] + cc[3]);
+        const f32x2 h = f32x2{relu6(a.x), relu6(a.y)}, hc = f32x2{relu6(c.x), relu6(c.y)};
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            acc[k] = __builtin_elementwise_fma(pair_at(w, kA2W + 8 * p + 2 * k), h, acc[k]);
+        cv = __builtin_elementwise_fma(pair_at(w, kC2W + 2 * p), hc, cv);
+    }
+}
+
 // logits z (post-ReLU) and, when VALUE, the critic's value of one board's inputs
 template <bool VALUE>
 __device__ __forceinline__ void mlp_forward(const float *__restrict__ w, const float (&x)[16], float (&z)[4], float &v)
@@ -361,14 +388,12 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
         st[lane][21] = xmax;
         {
             const float *wp = w;
-            f32x2 acc[4];
-            hidden_into<4>(wp, kA1W, kA1B, kA2W, x, acc);
+            f32x2 acc[4], c;
+            hidden_both(wp, x, acc, c);
 #pragma unroll
             for (int k = 0; k < 4; k++)
                 zr[k] = wp[kA2B + k] + (acc[k].x + acc[k].y);      // pre-ReLU
-            f32x2 c[1];
-            hidden_into<1>(wp, kC1W, kC1B, kC2W, x, c);
-            v = wp[kC2B] + (c[0].x + c[0].y);
+            v = wp[kC2B] + (c.x + c.y);
         }
         const float wt = live ? wn[rr] : 0.0f;
         const float tgt = targets[rr];

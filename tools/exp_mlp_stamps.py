@@ -25,7 +25,7 @@ net = ActorCriticMLP().to(dev)
 w = pack_mlp(net)
 L = _lib.load()
 ws = torch.empty(int(L.r48_mlp_train_workspace_floats()), dtype=torch.float32, device=dev)
-names = ["inputs", "actor fwd", "critic fwd", "loss", "stash+fix", "phase 2"]
+names = ["inputs", "forward", "-", "loss", "stash+fix", "phase 2"]
 n_rec = 1024 * 4
 for rep in range(3):
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -2,7 +2,7 @@
 tile loop: writes build/var/r48_mlp_stamp.hip, whose kernel stores, per wave, the cycles spent in
 each phase (summed over its tiles) over the first 16 words of its gradient record (so that build's
 gradients are wrong: timing only). The product source holds no diagnostic code.
-Phases: 0 inputs, 1 actor forward, 2 critic forward, 3 loss, 4 stash + exact logits, 5 phase 2.
+Phases: 0 inputs, 1 forward (actor and critic), 3 loss, 4 stash + exact logits, 5 phase 2.
 
     python tools/stamp_mlp.py && tools/build_variant.sh build/var/r48_mlp_stamp.hip r48_mlp build/lib_mlp_stamp.so
     python tools/exp_mlp_stamps.py build/lib_mlp_stamp.so      (on the GPU)"""
@@ -14,9 +14,8 @@ SRC = os.path.join(ROOT, "rein48_amd", "csrc", "r48_mlp.hip")
 OUT = os.path.join(ROOT, "build", "var", "r48_mlp_stamp.hip")
 
 MARKS = [
-    ("            hidden_into<4>(wp, kA1W, kA1B, kA2W, x, acc);", 0),
-    ("            hidden_into<1>(wp, kC1W, kC1B, kC2W, x, c);", 1),
-    ("        const float wt = live ? wn[rr] : 0.0f;", 2),
+    ("            hidden_both(wp, x, acc, c);", 0),
+    ("        const float wt = live ? wn[rr] : 0.0f;", 1),
     ("        wave_lds_sync();   // the previous tile's phase 2 has read the stash", 3),
     ("        // ---------------- phase 2: lane = hidden unit", 4),
     ("    }\n    // ---------------- this wave's record", 5),
