@@ -17,8 +17,6 @@ FLAGS_r48_policy ?=
 # the cell-grouped ResNet kernel keeps its 16 x 4 live accumulators in VGPRs (the epilogue reads
 # them without v_accvgpr_read) and the block input in AGPRs
 FLAGS_r48_resnet ?= -mllvm -amdgpu-mfma-vgpr-form=1
-# the MLP update: no SLP packing of its scalar f32 adds / FMAs (packed f32 VALU issues at half rate)
-FLAGS_r48_mlp ?= -fno-slp-vectorize
 
 $(LIBDIR)/librein48.so: $(OBJ)
 	@mkdir -p $(LIBDIR)

@@ -231,43 +231,36 @@ __global__ __launch_bounds__(kBlock) void k_mlp_rollout(int8_t *__restrict__ boa
 // k_mlp_train: the gradient of the A3C loss (rein48_amd/a3c/losses.py restating a3c.py:99-123,
 // textbook or the reference's broadcast actor loss; the per-row formulas of r48_a3c_train.hip's
 // k_cnn_train) w.r.t. all 2,501 parameters, fp32, in ONE pass over the training states.
-// The two 16 -> 64 layers are the bulk of the work (4,096 of ~5,000 FMAs per row: the forward and the
-// dW1 contraction of both networks) and run on the fp32 MFMA (v_mfma_f32_16x16x4_f32: bit-for-bit
-// a k-ordered fmaf chain, at the f32 peak beside the VALU); the rest is VALU. A wave takes 16 rows
-// per tile in ONE orientation, rows in registers and hidden units on the lanes:
-//   layer 1   pre-activation P[r][u] = b1[u] + sum_f x[r][f] W1[u][f] (one fmaf chain over f = 0..15):
-//             A = x (16 rows x 4 inputs per k-step, lane j + 16g holds x[r0 + j][4s + g]), B = W1^T
-//             (lane j + 16g: W1[16ub + j][4s + g], constant); D lane j + 16g, register i = row
-//             4g + i, unit 16ub + j.  2 nets x 4 unit blocks x 4 k-steps = 32 MFMAs per tile
-//   ReLU6     mask / h elementwise in that layout (exact decisions near 0 and 6, below)
-//   layer 2   logits and value of row 4g + i: each lane sums its 4 units, the 16 lanes of the row
-//             group add up with a DPP rotation butterfly (every lane gets the bitwise same sum)
-//   loss      per row (every lane of the group, counted once): softmax, entropy, td -> dz, dv
-//   dh        [mask] W2^T dz / [mask] wc2 dv, elementwise; db1, dW2, dwc2 in per-lane partials
-//   dW1       += x^T dh on the MFMA: A = x^T (lane j + 16g, k-step i: x[r0 + 4g + i][j]), B = dh (the
-//             layer-1 layout IS the B layout of a k = rows contraction), C = dW1^T (f x units, 4
-//             accumulators per net and unit block, in AGPRs).  32 MFMAs per tile
-// Per wave one record of the flat gradient in FlatParams order (a1.w [64][16] | a1.b | a2.w [4][64] |
-// a2.b | c1.w | c1.b | c2.w | c2.b) + the two losses; k_mlp_reduce sums the records in a fixed order
-// (deterministic).
-// The ReLU derivatives are decisions at 0 (and 6, ReLU6): an fp32 pre-activation within its rounding
-// error of the boundary may land on the other side than the exact value, and with raw tile values as
-// inputs (up to 2^17) a flipped hidden-unit mask moves a weight-gradient entry by a whole row's term
-// (dh x). So the update decides them on exact-enough values: a hidden pre-activation or a logit whose
-// fp32 value lies within its fp32 error bound of the boundary is recomputed in fp64 (rare: a branch
-// taken by ~1e-5 of the units, ~1e-3 of the rows' logits).
+// A wave takes 64 rows per tile in two phases:
+//   phase 1, lane = row: the forward of mlp_forward (SGPR weights, packed FMAs), softmax / entropy
+//     / td, the row's output gradient dz (through the logits' ReLU) and dv; the row's inputs x and
+//     (dz, dv) go to the wave's LDS stash (24 floats per row)
+//   phase 2, lane = hidden unit l (actor unit l and critic unit l): for each of the 64 rows (LDS
+//     broadcast reads) recompute a_l, c_l (the same FMA sequence as phase 1, so the same values),
+//     then dh_l = [0 < a_l < 6] sum_k W2[k][l] dz_k, dhc_l = [0 < c_l < 6] wc2[l] dv, and
+//     accumulate the unit's gradient row in registers: dW1[l][:] += dh_l x, db1, dW2[:][l] += dz h_l,
+//     dWc1[l][:], dbc1, dwc2[l]
+// so the weight gradients (contractions over rows) never cross lanes. Per wave one record of the
+// flat gradient in FlatParams order (a1.w [64][16] | a1.b | a2.w [4][64] | a2.b | c1.w | c1.b |
+// c2.w | c2.b) + the two losses; k_mlp_reduce sums the records in a fixed order (deterministic).
+// The ReLU derivatives of the update are decisions at 0 (and 6, ReLU6): an fp32 pre-activation within
+// its rounding error of the boundary may land on the other side than the exact value, and with raw
+// tile values as inputs (up to 2^17) a flipped hidden-unit mask moves a weight-gradient entry by a
+// whole row's term (dh x). So the update decides them on exact-enough values: a hidden pre-activation
+// (phase 2) or a logit (phase 1) whose fp32 value lies within the fp32 error bound of its boundary is
+// recomputed in fp64 (rare: a divergent branch taken by ~1e-5 of the units / logits).
 constexpr int kTrainWaves = 4;
+constexpr int kStash = 28;                 // x[16] | dz[4] | dv | max x | dz before the logits' ReLU [4] | pad
 constexpr int kRec = 2504;                 // 2,501 gradient floats + actor loss + critic loss + pad
 constexpr int kRecLossA = 2501, kRecLossC = 2502;
 // (the record's section offsets equal the blob's, kA1W .. kC2B; inside a1 / a2 / c1 the record has
 // the parameters' own [out][in] order)
 constexpr float kEntropyEps = 1e-5f;       // a3c.py:114
 constexpr float kLn2 = 0.69314718055994531f;
-typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-// the wave's LDS board area is written and read by different lanes: every outstanding LDS
-// operation completes (s_waitcnt lgkmcnt(0)) before the next access, and the compiler moves no LDS
-// access across the point
+// the wave's LDS stash is written by one phase and read by the other: every outstanding LDS
+// operation completes (s_waitcnt lgkmcnt(0)) before the next phase's first access, and the
+// compiler moves no LDS access across the point
 __device__ __forceinline__ void wave_lds_sync()
 {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -289,92 +282,27 @@ __device__ __forceinline__ float wave_sum(float v)
     return v;
 }
 
-// all-reduce over the 16 lanes of a DPP row by rotations 8, 4, 2, 1: at every level a lane adds
-// the same two operands as its partner (IEEE addition commutes), so all 16 lanes get the bitwise
-// same sum
-template <int N>
-__device__ __forceinline__ float row_ror(float v)
+// phase 2's (a_l, c_l) of one stashed row (its inputs returned as pairs (x_2i, x_2i+1)), in the
+// four-chain FMA order of phase 1 (hidden_into: chain q takes the inputs f = q mod 4 in order, the
+// bias starts chain 0), so the same values: chains (0, 1) are the pair p*, chains (2, 3) the pair q*
+__device__ __forceinline__ f32x2 unit_preacts(const float (&row)[kStash], const f32x2 (&wa)[8], const f32x2 (&wc)[8],
+                                              f32x2 bl, f32x2 (&xp)[8])
 {
-    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x120 + N, 0xF, 0xF, false));
-}
-__device__ __forceinline__ float row_sum16(float v)
-{
-    v += row_ror<8>(v);
-    v += row_ror<4>(v);
-    v += row_ror<2>(v);
-    v += row_ror<1>(v);
-    return v;
-}
-template <int N>
-__device__ __forceinline__ double row_ror_d(double v)
-{
-    const uint64_t u = (uint64_t)__double_as_longlong(v);
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)u, 0x120 + N, 0xF, 0xF, false);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(u >> 32), 0x120 + N, 0xF, 0xF, false);
-    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
-}
-__device__ __forceinline__ double row_sum16_d(double v)
-{
-    v += row_ror_d<8>(v);
-    v += row_ror_d<4>(v);
-    v += row_ror_d<2>(v);
-    v += row_ror_d<1>(v);
-    return v;
-}
-
-// blob accessors (pack_mlp layout: layer-1 and W2 grouped by hidden-unit pair)
-__device__ __forceinline__ float w1_at(const float *w, int base, int u, int f) { return w[base + 32 * (u >> 1) + 2 * f + (u & 1)]; }
-__device__ __forceinline__ float w2_at(const float *w, int u, int k) { return w[kA2W + 8 * (u >> 1) + 2 * k + (u & 1)]; }
-
-// fp64 pre-activation of hidden unit u of one network on the row whose 16 cell bytes are `cells`
-template <int MODE>
-__device__ __forceinline__ double preact64(const float *w, int base, int bbase, int u, const uint8_t *cells)
-{
-    // the weights are re-read here, on the rare path: an opaque pointer keeps the compiler from
-    // hoisting these loop-invariant loads out of the tile loop into 128 live registers
-    uint64_t wa = reinterpret_cast<uint64_t>(w);
-    asm volatile("" : "+s"(wa));
-    w = reinterpret_cast<const float *>(wa);
-    double a = w[bbase + u];
-    for (int f = 0; f < 16; f++)
-        a = __builtin_fma((double)w1_at(w, base, u, f), (double)cell_input<MODE>(cells[f]), a);
-    return a;
-}
-
-// per-wave LDS area of a 16-row tile (32-bit words): boards [16][4] | max input | row weight |
-// target | action | cm | counts [16][4] | pre-ReLU logits [16][4] | value | dz through the logits'
-// ReLU [16][4] | dv | near flag
-constexpr int kTB = 0, kTXm = 64, kTWt = 80, kTTg = 96, kTAc = 112, kTCm = 128, kTCn = 144, kTZr = 208, kTV = 272,
-              kTDz = 288, kTDv = 352, kTNr = 368, kTileWords = 384;
-
-// the inputs of one training row, loaded a tile ahead by lane j of every lane group
-struct RowIn {
-    uint4 b;
-    float wt, tgt, c;
-    int a;
-    float4 cnt;
-};
-
-template <bool REF>
-__device__ __forceinline__ RowIn fetch_row(int64_t r, int64_t rows, int64_t n_boards, const int8_t *boards,
-                                           const int8_t *actions, const float *targets, const float *wn,
-                                           const float *cm, const float *counts)
-{
-    const bool live = r < rows;
-    const int64_t rr = live ? r : rows - 1;   // padding rows: a valid row with weight 0
-    RowIn x;
-    x.b = *reinterpret_cast<const uint4 *>(boards + 16 * rr);
-    x.wt = live ? wn[rr] : 0.0f;
-    x.tgt = targets[rr];
-    x.a = actions[rr] & 3;
-    x.c = 0.0f;
-    x.cnt = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (REF) {
-        x.c = live ? cm[rr] : 0.0f;
-        const int64_t bidx = rows <= 0xFFFFFFFFll ? (int64_t)((uint32_t)rr % (uint32_t)n_boards) : rr % n_boards;
-        x.cnt = *reinterpret_cast<const float4 *>(counts + 4 * bidx);
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const float4 t4 = *reinterpret_cast<const float4 *>(&row[4 * q]);
+        xp[2 * q] = f32x2{t4.x, t4.y};
+        xp[2 * q + 1] = f32x2{t4.z, t4.w};
     }
-    return x;
+    f32x2 pa = f32x2{bl.x, 0.f}, qa = f32x2{0.f, 0.f}, pc = f32x2{bl.y, 0.f}, qc = f32x2{0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < 8; i += 2) {
+        pa = __builtin_elementwise_fma(wa[i], xp[i], pa);
+        pc = __builtin_elementwise_fma(wc[i], xp[i], pc);
+        qa = __builtin_elementwise_fma(wa[i + 1], xp[i + 1], qa);
+        qc = __builtin_elementwise_fma(wc[i + 1], xp[i + 1], qc);
+    }
+    return f32x2{(pa.x + pa.y) + (qa.x + qa.y), (pc.x + pc.y) + (qc.x + qc.y)};
 }
 
 template <int MODE, bool REF>
@@ -383,453 +311,273 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
     const float *__restrict__ targets, const float *__restrict__ wn, const float *__restrict__ cm,
     const float *__restrict__ counts, float beta, const float *__restrict__ w, float *__restrict__ partials)
 {
-    // per wave: the tile's 16 boards (64 words) and each row's largest input; per workgroup: the
-    // layer-1 B operands and biases of every lane (read back each tile: 40 registers the rest of
-    // the tile needs)
-    __shared__ __attribute__((aligned(16))) uint32_t tiles_lds[kTrainWaves][kTileWords];
-    __shared__ __attribute__((aligned(16))) float w1_lds[64][60];
-    // per lane: the db1 / dW2 / dwc2 partials, per unit block [dW2[k] x 4 | dwc2 | db1 | dbc1 | pad]
-    // (read-modified-written by the backward one unit block at a time: registers for two waves per
-    // SIMD)
-    __shared__ __attribute__((aligned(16))) float acc_lds[kTrainWaves][64][32];
-    const int lane = threadIdx.x & 63, j = lane & 15, g = lane >> 4;
+    __shared__ float stash[kTrainWaves][64][kStash];
+    const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    uint32_t *bw = tiles_lds[wave];
-    const uint8_t *cells = reinterpret_cast<const uint8_t *>(bw);
-    constexpr int kW1[2] = {kA1W, kC1W}, kB1[2] = {kA1B, kC1B};
-
-    // constants of lane (j, g)'s units 16ub + j: layer-1 B operands (inputs 4s + g) and biases in
-    // LDS (w1_lds[lane][8 (net, ub) + s], [32 + (net, ub)]), W2 / wc2 entries in registers
-    if (threadIdx.x < 64) {
+    float(*st)[kStash] = stash[wave];
+    // phase-2 weights of unit l = lane in input pairs (2i, 2i + 1) -- every phase-2 FMA is a
+    // v_pk_fma_f32 over two inputs, whose values the LDS reads deliver as aligned pairs -- and its
+    // gradient accumulators
+    f32x2 wa[8], wc[8], w2l[2];
+    const int pl = 32 * (lane >> 1) + (lane & 1);      // unit l's place in its pair's layer-1 block
 #pragma unroll
-        for (int net = 0; net < 2; net++)
-#pragma unroll
-            for (int ub = 0; ub < 4; ub++) {
-                const int u = 16 * ub + j;
-#pragma unroll
-                for (int s4 = 0; s4 < 4; s4++)
-                    w1_lds[lane][4 * (4 * net + ub) + s4] = w1_at(w, kW1[net], u, 4 * s4 + g);
-                w1_lds[lane][32 + 4 * net + ub] = w[kB1[net] + u];
-            }
-#pragma unroll
-        for (int ub = 0; ub < 4; ub++) {
-#pragma unroll
-            for (int k = 0; k < 4; k++)
-                w1_lds[lane][40 + 4 * ub + k] = w2_at(w, 16 * ub + j, k);
-            w1_lds[lane][56 + ub] = w[kC2W + 16 * ub + j];
-        }
+    for (int i = 0; i < 8; i++) {
+        wa[i] = f32x2{w[kA1W + pl + 4 * i], w[kA1W + pl + 4 * i + 2]};
+        wc[i] = f32x2{w[kC1W + pl + 4 * i], w[kC1W + pl + 4 * i + 2]};
     }
-    float *acc = acc_lds[wave][lane];
 #pragma unroll
-    for (int q = 0; q < 8; q++)
-        reinterpret_cast<float4 *>(acc)[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-    __syncthreads();
-    const float4 *wl = reinterpret_cast<const float4 *>(w1_lds[lane]);   // this lane's constants
-    // fp32 error bound of a hidden pre-activation: 16 roundings below |b| + sum |w| max x, i.e.
-    // < 2^-20 (|b| + sum |w| max x); 2x margin, + 2^-21 for the rounding of the decision's a - 3;
-    // with the largest |b| and sum |w| of the network's 64 units (wave-uniform, SGPRs)
-    float s1[2], e1[2];
+    for (int k = 0; k < 2; k++)
+        w2l[k] = f32x2{w[kA2W + 8 * (lane >> 1) + 4 * k + (lane & 1)], w[kA2W + 8 * (lane >> 1) + 4 * k + 2 + (lane & 1)]};
+    const float wc2l = w[kC2W + lane];
+    const f32x2 bl = f32x2{w[kA1B + lane], w[kC1B + lane]};
+    // fp32 error bound of the unit's pre-activation: 16 roundings of partial sums below
+    // |b| + sum |w| max x, i.e. < 2^-20 (|b| + sum |w| max x); 2x margin, + 2^-21 for the rounding
+    // of the decision's own al - 3 (phase 2)
+    f32x2 sl = f32x2{0.f, 0.f};
 #pragma unroll
-    for (int net = 0; net < 2; net++) {
-        float sm = 0.f, bm = 0.f;
-        for (int u = 0; u < 64; u++) {
-            float sa = 0.f;
-            for (int f = 0; f < 16; f++)
-                sa += fabsf(w1_at(w, kW1[net], u, f));
-            sm = fmaxf(sm, sa);
-            bm = fmaxf(bm, fabsf(w[kB1[net] + u]));
-        }
-        s1[net] = uniform(sm * 0x1p-19f);
-        e1[net] = uniform(fmaf(bm, 0x1p-19f, 0x1p-21f));
-    }
-    // fp32 error bound of a pre-ReLU logit: its own sum (64 products of |h| <= 6: < 2^-18 (|b2| +
-    // 6 sum |W2[k][:]|)) plus the hidden units' errors carried through W2 (each < 2^-20 (|b1| +
-    // sum |W1[u][:]| max x)); 2x-4x margins (wave-uniform: kept in SGPRs)
+    for (int i = 0; i < 8; i++)
+        sl += f32x2{fabsf(wa[i].x) + fabsf(wa[i].y), fabsf(wc[i].x) + fabsf(wc[i].y)};
+    sl *= 0x1p-19f;
+    const f32x2 el = f32x2{fmaf(fabsf(bl.x), 0x1p-19f, 0x1p-21f), fmaf(fabsf(bl.y), 0x1p-19f, 0x1p-21f)};
+    f32x2 ga[8], gc[8], gbl = f32x2{0.f, 0.f}, g2l[2] = {f32x2{0.f, 0.f}, f32x2{0.f, 0.f}};
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+        ga[i] = gc[i] = f32x2{0.f, 0.f};
+    float gc2 = 0.f;
+    // per-row-lane sums (reduced over the wave at the end)
+    float gb2[4] = {0.f, 0.f, 0.f, 0.f}, gbc2 = 0.f, loss_a = 0.f, loss_c = 0.f;
+    // fp32 error bound of a pre-ReLU logit: its own sum (64 products of |h| <= 6 in parity halves:
+    // < 2^-18 (|b2| + 6 sum |W2[k][:]|)) plus the hidden units' errors carried through W2 (each
+    // < 2^-20 (|b1| + sum |W1[j][:]| max x), see sl above); 2x-4x margins
+    // (wave-uniform: kept in SGPRs)
     float zedge[4], zcarry[4], hb = 0.f, hw = 0.f;
-    for (int u = 0; u < 64; u++) {
+    for (int j = 0; j < 64; j++) {
         float sw = 0.f;
         for (int f = 0; f < 16; f++)
-            sw += fabsf(w1_at(w, kA1W, u, f));
+            sw += fabsf(w[kA1W + 32 * (j >> 1) + 2 * f + (j & 1)]);
         hw = fmaxf(hw, sw);
-        hb = fmaxf(hb, fabsf(w[kA1B + u]));
+        hb = fmaxf(hb, fabsf(w[kA1B + j]));
     }
-    float b2[4];
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         float sa = 0.f;
-        for (int u = 0; u < 64; u++)
-            sa += fabsf(w2_at(w, u, k));
+        for (int j = 0; j < 64; j++)
+            sa += fabsf(w[kA2W + 8 * (j >> 1) + 2 * k + (j & 1)]);
         zedge[k] = uniform((fabsf(w[kA2B + k]) + 6.0f * sa) * 0x1p-16f);
         zcarry[k] = uniform(sa * 0x1p-19f);
-        b2[k] = uniform(w[kA2B + k]);
     }
     hb = uniform(hb);
     hw = uniform(hw);
-    const float bc2 = uniform(w[kC2B]);
 
-    // accumulators: dW1^T per net and unit block (MFMA C: f = 4g + i, unit 16ub + j), per-lane
-    // partials of db1, dW2, dwc2 (summed over the lane's rows; the four lane groups are added at the
-    // end), per-row sums (counted in the lanes j == 0)
-    f32x4 gw1[2][4];
-#pragma unroll
-    for (int ub = 0; ub < 4; ub++)
-        gw1[0][ub] = gw1[1][ub] = f32x4{0.f, 0.f, 0.f, 0.f};
-    float gb2[4] = {0.f, 0.f, 0.f, 0.f}, gbc2 = 0.f, loss_a = 0.f, loss_c = 0.f;
-    const float once = j == 0 ? 1.0f : 0.0f;   // the fix-up's per-row sums: one lane of the row group
-
-    const int64_t n_tiles = (rows + 15) / 16;
+    const int64_t n_tiles = (rows + 63) / 64;
     const int64_t stride = (int64_t)gridDim.x * kTrainWaves;
-    int64_t tile = (int64_t)blockIdx.x * kTrainWaves + wave;
-    // one wave per SIMD hides no load latency: row r0 + j's inputs arrive a tile ahead
-    RowIn next = fetch_row<REF>(std::min<int64_t>(tile, n_tiles - 1) * 16 + j, rows, n_boards, boards, actions, targets,
-                                wn, cm, counts);
-    for (; tile < n_tiles; tile += stride) {
-        // ---------------- inputs: row r0 + j in the four lanes j + 16g
-        const RowIn in = next;
-        next = fetch_row<REF>(std::min<int64_t>(tile + stride, n_tiles - 1) * 16 + j, rows, n_boards, boards, actions,
-                              targets, wn, cm, counts);
-        const uint4 bv = in.b;
-        const uint32_t bwd[4] = {bv.x, bv.y, bv.z, bv.w};
-        float xa[4];   // A operands of layer 1: x[r0 + j][4s + g]
+    for (int64_t tile = (int64_t)blockIdx.x * kTrainWaves + wave; tile < n_tiles; tile += stride) {
+        // ---------------- phase 1: lane = row
+        const int64_t r = tile * 64 + lane;
+        const bool live = r < rows;
+        const int64_t rr = live ? r : rows - 1;      // padding lanes: a valid row with weight 0
+        float x[16], zr[4], v;
+        board_inputs<MODE>(load_board(boards, rr), x);
+        const float xmax = fmaxf(fmaxf(fmaxf(fmaxf(x[0], x[1]), fmaxf(x[2], x[3])), fmaxf(fmaxf(x[4], x[5]), fmaxf(x[6], x[7]))),
+                                 fmaxf(fmaxf(fmaxf(x[8], x[9]), fmaxf(x[10], x[11])), fmaxf(fmaxf(x[12], x[13]), fmaxf(x[14], x[15]))));
+        // the row's inputs go to the stash at once (they are dead after the forward)
+        wave_lds_sync();   // the previous tile's phase 2 has read the stash
 #pragma unroll
-        for (int s4 = 0; s4 < 4; s4++)
-            xa[s4] = cell_input<MODE>((bwd[s4] >> (8 * g)) & 0xFFu);
-        uint32_t mb = 0;   // largest cell byte of the row (inputs grow with it)
-#pragma unroll
-        for (int s4 = 0; s4 < 4; s4++)
-#pragma unroll
-            for (int q = 0; q < 4; q++)
-                mb = std::max(mb, (bwd[s4] >> (8 * q)) & 0xFFu);
-        wave_lds_sync();   // the previous tile's reads of the board area are done
-        if (g == 0) {
-            *reinterpret_cast<uint4 *>(bw + kTB + 4 * j) = bv;
-            bw[kTXm + j] = __float_as_uint(cell_input<MODE>(mb));
-            bw[kTWt + j] = __float_as_uint(in.wt);
-            bw[kTTg + j] = __float_as_uint(in.tgt);
-            bw[kTAc + j] = (uint32_t)in.a;
-            if (REF) {
-                bw[kTCm + j] = __float_as_uint(in.c);
-                *reinterpret_cast<float4 *>(bw + kTCn + 4 * j) = in.cnt;
-            }
-        }
-        wave_lds_sync();
-        float xt[4], xm[4];   // A operands of dW1: x[r0 + 4g + i][j]; max input of row 4g + i
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            xt[i] = cell_input<MODE>(cells[16 * (4 * g + i) + j]);
-            xm[i] = __uint_as_float(bw[kTXm + 4 * g + i]);
-        }
-
-        // ---------------- layer 1 on the MFMA: register i = row 4g + i, lane j = unit 16ub + j
-        f32x4 pre[2][4];
-        const float4 bl0 = wl[8], bl1 = wl[9];
-        const float b1[2][4] = {{bl0.x, bl0.y, bl0.z, bl0.w}, {bl1.x, bl1.y, bl1.z, bl1.w}};
-#pragma unroll
-        for (int net = 0; net < 2; net++)
-#pragma unroll
-            for (int ub = 0; ub < 4; ub++) {
-                const float4 wb = wl[4 * net + ub];
-                f32x4 acc = f32x4{b1[net][ub], b1[net][ub], b1[net][ub], b1[net][ub]};
-                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[0], wb.x, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[1], wb.y, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[2], wb.z, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[3], wb.w, acc, 0, 0, 0);
-                pre[net][ub] = acc;
-            }
-        // ---------------- ReLU6 decisions 0 < a < 6, i.e. |a - 3| < 3; within the fp32 error bound
-        // of 0 or 6 (min(|a|, |a - 6|) = ||a - 3| - 3|) the pre-activation is redone in fp64
-        // (the hot path takes the fp32 decision where it uses a mask and only asks whether any of
-        // the tile's 512 pre-activations is near a boundary; the fix-up below finds which)
-        float bound[2][4];
-#pragma unroll
-        for (int net = 0; net < 2; net++)
-#pragma unroll
-            for (int i = 0; i < 4; i++)
-                bound[net][i] = fmaf(s1[net], xm[i], e1[net]);
-        bool edge_any = false;
-#pragma unroll
-        for (int net = 0; net < 2; net++)
-#pragma unroll
-            for (int ub = 0; ub < 4; ub++)
-#pragma unroll
-                for (int i = 0; i < 4; i++)
-                    edge_any |= fabsf(fabsf(pre[net][ub][i] - 3.0f) - 3.0f) < bound[net][i];
-        // ---------------- per row i of the lane group (rows 4g + i): layer 2 (the group's 16 lanes
-        // add up), the loss (every lane of the group computes it; counted once) -- the same code on
-        // the hot path and in the exact-decision fix-up below, so the same values
-        auto layer2 = [&](int i, float (&zr)[4], float &v) {
-            float pk[4] = {0.f, 0.f, 0.f, 0.f}, pv = 0.f;
-            const float4 c2 = wl[14];   // wc2 of the lane's 4 units
-            const float wc2[4] = {c2.x, c2.y, c2.z, c2.w};
-#pragma unroll
-            for (int ub = 0; ub < 4; ub++) {
-                const float4 w4 = wl[10 + ub];   // W2[k][16ub + j]
-                const float ha = __builtin_amdgcn_fmed3f(pre[0][ub][i], 0.0f, 6.0f);
-                pk[0] = fmaf(w4.x, ha, pk[0]);
-                pk[1] = fmaf(w4.y, ha, pk[1]);
-                pk[2] = fmaf(w4.z, ha, pk[2]);
-                pk[3] = fmaf(w4.w, ha, pk[3]);
-                pv = fmaf(wc2[ub], __builtin_amdgcn_fmed3f(pre[1][ub][i], 0.0f, 6.0f), pv);
-            }
+        for (int q = 0; q < 4; q++)
+            *reinterpret_cast<float4 *>(&st[lane][4 * q]) = make_float4(x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]);
+        st[lane][21] = xmax;
+        {
+            const float *wp = w;
+            f32x2 acc[4], c;
+            hidden_both(wp, x, acc, c);
 #pragma unroll
             for (int k = 0; k < 4; k++)
-                zr[k] = b2[k] + row_sum16(pk[k]);   // pre-ReLU
-            v = bc2 + row_sum16(pv);
-        };
-        // the loss of tile row ri from its pre-ReLU logits and value
-        auto loss_from = [&](int ri, const float (&zr)[4], float v, float (&dz)[4], float &dv, float &la, float &lc) {
-            const float wt = __uint_as_float(bw[kTWt + ri]);
-            const float tgt = __uint_as_float(bw[kTTg + ri]);
-            const int a = (int)bw[kTAc + ri];
-            float z[4], p[4], gr[4];
+                zr[k] = wp[kA2B + k] + (acc[k].x + acc[k].y);      // pre-ReLU
+            v = wp[kC2B] + (c.x + c.y);
+        }
+        const float wt = live ? wn[rr] : 0.0f;
+        const float tgt = targets[rr];
+        const int a = actions[rr] & 3;
+        float z[4], p[4], gr[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            z[k] = fmaxf(zr[k], 0.0f);                            // the logits' ReLU (a3c.py:153)
+        const float m = fmaxf(fmaxf(z[0], z[1]), fmaxf(z[2], z[3]));
+        float se = 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            p[k] = __expf(z[k] - m);
+            se += p[k];
+        }
+        const float inv = __builtin_amdgcn_rcpf(se), lse = m + kLn2 * __builtin_amdgcn_logf(se);
+        float H = 0.f, gbar = 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            p[k] *= inv;
+            const float lq = kLn2 * __builtin_amdgcn_logf(p[k] + kEntropyEps);
+            H -= p[k] * lq;
+            gr[k] = -(lq + p[k] * __builtin_amdgcn_rcpf(p[k] + kEntropyEps));   // dH/dp_k
+            gbar += p[k] * gr[k];
+        }
+        const float td = tgt - v;
+        float dz[4];
+        if (REF) {   // reference: -beta wn H - cm sum_k c_k log p_k  (losses.py, a3c.py:110-116)
+            const float c = live ? cm[rr] : 0.0f;
+            const int64_t bidx = rows <= 0xFFFFFFFFll ? (int64_t)((uint32_t)rr % (uint32_t)n_boards) : rr % n_boards;
+            const float4 cnt = *reinterpret_cast<const float4 *>(counts + 4 * bidx);
+            const float ck[4] = {cnt.x, cnt.y, cnt.z, cnt.w}, C = cnt.x + cnt.y + cnt.z + cnt.w;
+            float sa = 0.f;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                dz[k] = -beta * wt * p[k] * (gr[k] - gbar) - c * (ck[k] - p[k] * C);
+                sa += ck[k] * (z[k] - lse);
+            }
+            loss_a += -beta * wt * H - c * sa;
+        } else {     // textbook: -wn (beta H + td log p[a]), td constant for the actor
 #pragma unroll
             for (int k = 0; k < 4; k++)
-                z[k] = fmaxf(zr[k], 0.0f);                            // the logits' ReLU (a3c.py:153)
-            const float mz = fmaxf(fmaxf(z[0], z[1]), fmaxf(z[2], z[3]));
-            float se = 0.f;
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                p[k] = __expf(z[k] - mz);
-                se += p[k];
-            }
-            const float inv = __builtin_amdgcn_rcpf(se), lse = mz + kLn2 * __builtin_amdgcn_logf(se);
-            float H = 0.f, gbar = 0.f;
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                p[k] *= inv;
-                const float lq = kLn2 * __builtin_amdgcn_logf(p[k] + kEntropyEps);
-                H -= p[k] * lq;
-                gr[k] = -(lq + p[k] * __builtin_amdgcn_rcpf(p[k] + kEntropyEps));   // dH/dp_k
-                gbar += p[k] * gr[k];
-            }
-            const float td = tgt - v;
-            if (REF) {   // reference: -beta wn H - cm sum_k c_k log p_k  (losses.py, a3c.py:110-116)
-                const float c = __uint_as_float(bw[kTCm + ri]);
-                const float4 cnt = *reinterpret_cast<const float4 *>(bw + kTCn + 4 * ri);
-                const float ck[4] = {cnt.x, cnt.y, cnt.z, cnt.w}, C = cnt.x + cnt.y + cnt.z + cnt.w;
-                float sa = 0.f;
-#pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    dz[k] = -beta * wt * p[k] * (gr[k] - gbar) - c * (ck[k] - p[k] * C);
-                    sa += ck[k] * (z[k] - lse);
-                }
-                la = -beta * wt * H - c * sa;
-            } else {     // textbook: -wn (beta H + td log p[a]), td constant for the actor
-#pragma unroll
-                for (int k = 0; k < 4; k++)
-                    dz[k] = -wt * (beta * p[k] * (gr[k] - gbar) + td * ((k == a ? 1.0f : 0.0f) - p[k]));
-                la = -wt * (beta * H + td * (z[a] - lse));
-            }
-            dv = -2.0f * wt * td;                                      // critic = wn td^2
-            lc = wt * td * td;
-        };
-        // the backward of the lane group's 4 rows with output gradients dz (through the logits' ReLU)
-        // and dv, and hidden masks (the fp32 decisions, or the given bits in the fix-up): the per-lane
-        // partials (in LDS, one unit block at a time) and the rows' k-steps of dW1 on the MFMA
-        // (register i = row, lane = unit); `sel` picks the rows (bit i), the fix-up runs it on
-        // differences
-        auto rows_backward = [&](const float (&dz)[4][4], const float (&dv)[4], uint32_t sel, bool bits, uint32_t mk,
-                                 float scale_once) {
-#pragma unroll
-            for (int i = 0; i < 4; i++) {
-                if (!((sel >> i) & 1u))
-                    continue;
-#pragma unroll
-                for (int k = 0; k < 4; k++)
-                    gb2[k] += scale_once * dz[i][k];
-                gbc2 += scale_once * dv[i];
-            }
-            const float4 c2 = wl[14];
-            const float wc2[4] = {c2.x, c2.y, c2.z, c2.w};
-#pragma unroll
-            for (int ub = 0; ub < 4; ub++) {
-                const float4 w4 = wl[10 + ub];
-                float4 a2 = reinterpret_cast<float4 *>(acc)[2 * ub];        // dW2[k][16ub + j] partials
-                float4 a1 = reinterpret_cast<float4 *>(acc)[2 * ub + 1];    // dwc2 | db1 | dbc1 | -
-#pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    if (!((sel >> i) & 1u))
-                        continue;
-                    const float ha = __builtin_amdgcn_fmed3f(pre[0][ub][i], 0.0f, 6.0f);
-                    const float hc = __builtin_amdgcn_fmed3f(pre[1][ub][i], 0.0f, 6.0f);
-                    const float sdh = fmaf(w4.w, dz[i][3], fmaf(w4.z, dz[i][2], fmaf(w4.y, dz[i][1], w4.x * dz[i][0])));
-                    // the masks: the given bits (fix-up) or the fp32 decisions 0 < a < 6, i.e. |a - 3| < 3
-                    const bool ma = bits ? ((mk >> (4 * ub + i)) & 1u) != 0 : fabsf(pre[0][ub][i] - 3.0f) < 3.0f;
-                    const bool mc = bits ? ((mk >> (16 + 4 * ub + i)) & 1u) != 0 : fabsf(pre[1][ub][i] - 3.0f) < 3.0f;
-                    const float dha = ma ? sdh : 0.0f;
-                    const float dhc = mc ? wc2[ub] * dv[i] : 0.0f;
-                    a2.x = fmaf(dz[i][0], ha, a2.x);
-                    a2.y = fmaf(dz[i][1], ha, a2.y);
-                    a2.z = fmaf(dz[i][2], ha, a2.z);
-                    a2.w = fmaf(dz[i][3], ha, a2.w);
-                    a1.x = fmaf(dv[i], hc, a1.x);
-                    a1.y += dha;
-                    a1.z += dhc;
-                    gw1[0][ub] = __builtin_amdgcn_mfma_f32_16x16x4f32(xt[i], dha, gw1[0][ub], 0, 0, 0);
-                    gw1[1][ub] = __builtin_amdgcn_mfma_f32_16x16x4f32(xt[i], dhc, gw1[1][ub], 0, 0, 0);
-                }
-                reinterpret_cast<float4 *>(acc)[2 * ub] = a2;
-                reinterpret_cast<float4 *>(acc)[2 * ub + 1] = a1;
-            }
-        };
-        // hot path: fp32 decisions everywhere; rows whose logit lies within its fp32 error bound of
-        // 0 are flagged in `near` (bit i). Layer 2 of the lane group's rows, then the 16 rows' losses
-        // in lanes 0..15 (one lane per row, through the tile's LDS area), then the backward
-        {
-            float zr4[4][4], v4[4];
-#pragma unroll
-            for (int i = 0; i < 4; i++)
-                layer2(i, zr4[i], v4[i]);
-            if (j == 0) {
-#pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    *reinterpret_cast<float4 *>(bw + kTZr + 4 * (4 * g + i)) = make_float4(zr4[i][0], zr4[i][1], zr4[i][2], zr4[i][3]);
-                    bw[kTV + 4 * g + i] = __float_as_uint(v4[i]);
-                }
-            }
+                dz[k] = -wt * (beta * p[k] * (gr[k] - gbar) + td * ((k == a ? 1.0f : 0.0f) - p[k]));
+            loss_a += -wt * (beta * H + td * (z[a] - lse));
         }
+        const float dv = -2.0f * wt * td;                          // critic = wn td^2
+        loss_c += wt * td * td;
+        // through the logits' ReLU; a logit within its fp32 error bound of 0 is decided on its exact
+        // value by the whole wave at the start of phase 2 (rows flagged in `near_rows`)
+        bool near = false;
+        float dzm[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            near |= fabsf(zr[k]) < zedge[k] + zcarry[k] * (hb + hw * xmax);
+            dzm[k] = zr[k] > 0.0f ? dz[k] : 0.0f;
+        }
+        if (!near) {
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                gb2[k] += dzm[k];
+        }
+        const uint64_t near_rows = __ballot(near);
+        gbc2 += dv;
+        *reinterpret_cast<float4 *>(&st[lane][16]) = make_float4(dzm[0], dzm[1], dzm[2], dzm[3]);
+        st[lane][20] = dv;
+        if (near_rows)
+            *reinterpret_cast<float4 *>(&st[lane][24]) = make_float4(dz[0], dz[1], dz[2], dz[3]);
         wave_lds_sync();
-        if (lane < 16) {
-            const float4 z4 = *reinterpret_cast<const float4 *>(bw + kTZr + 4 * lane);
-            const float zr[4] = {z4.x, z4.y, z4.z, z4.w};
-            float dz[4], dv, la, lc;
-            loss_from(lane, zr, __uint_as_float(bw[kTV + lane]), dz, dv, la, lc);
-            const float xml = __uint_as_float(bw[kTXm + lane]);
-            bool nr = false;
+        // exact logits of the flagged rows, lane = hidden unit: its fp64 pre-activation, times W2,
+        // summed over the wave; lane 0 writes the row's dz through the exact ReLU decision
+        for (uint64_t m = near_rows; m; m &= m - 1) {
+            const int j = __builtin_ctzll(m);
+            double ad = bl.x;
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                ad = __builtin_fma((double)wa[i].x, (double)st[j][2 * i], ad);
+                ad = __builtin_fma((double)wa[i].y, (double)st[j][2 * i + 1], ad);
+            }
+            const double hd = ad < 0.0 ? 0.0 : (ad > 6.0 ? 6.0 : ad);
+            const double w2d[4] = {w2l[0].x, w2l[0].y, w2l[1].x, w2l[1].y};
+            double t[4];
 #pragma unroll
             for (int k = 0; k < 4; k++) {
-                nr |= fabsf(zr[k]) < zedge[k] + zcarry[k] * (hb + hw * xml);
-                dz[k] = zr[k] > 0.0f ? dz[k] : 0.0f;
-                gb2[k] += dz[k];
+                t[k] = w2d[k] * hd;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1)
+                    t[k] += __shfl_xor(t[k], o);
             }
-            gbc2 += dv;
-            loss_a += la;
-            loss_c += lc;
-            *reinterpret_cast<float4 *>(bw + kTDz + 4 * lane) = make_float4(dz[0], dz[1], dz[2], dz[3]);
-            bw[kTDv + lane] = __float_as_uint(dv);
-            bw[kTNr + lane] = nr ? 1u : 0u;
-        }
-        wave_lds_sync();
-        uint32_t near = 0;
-        {
-            float dz[4][4], dv[4];
-#pragma unroll
-            for (int i = 0; i < 4; i++) {
-                const float4 d4 = *reinterpret_cast<const float4 *>(bw + kTDz + 4 * (4 * g + i));
-                dz[i][0] = d4.x, dz[i][1] = d4.y, dz[i][2] = d4.z, dz[i][3] = d4.w;
-                dv[i] = __uint_as_float(bw[kTDv + 4 * g + i]);
-                near |= bw[kTNr + 4 * g + i] << i;
-            }
-            rows_backward(dz, dv, 0xFu, false, 0u, 0.0f);
-        }
-        // ---------------- exact decisions (rare: the whole wave enters, lanes pick their own rows):
-        // for a flagged row, the exact logits' ReLU and hidden masks, and the row's backward run again
-        // on the differences (exact minus what the hot path accumulated)
-        if (__builtin_amdgcn_ballot_w64(edge_any || near != 0)) {
-            // opaque copies of the tile's pre-activations: the fix-up recomputes the rows' losses
-            // from them instead of keeping the hot path's values alive across the loop
-#pragma unroll
-            for (int net = 0; net < 2; net++)
-#pragma unroll
-                for (int ub = 0; ub < 4; ub++)
-                    asm volatile("" : "+v"(pre[net][ub]));
-            uint32_t mask = 0, edge = 0;   // fp32 decisions and flags, bit 16 net + 4 ub + i
-#pragma unroll
-            for (int net = 0; net < 2; net++)
-#pragma unroll
-                for (int ub = 0; ub < 4; ub++)
-#pragma unroll
-                    for (int i = 0; i < 4; i++) {
-                        const float d = fabsf(pre[net][ub][i] - 3.0f);
-                        const uint32_t bit = 1u << (16 * net + 4 * ub + i);
-                        mask |= d < 3.0f ? bit : 0u;
-                        edge |= fabsf(d - 3.0f) < bound[net][i] ? bit : 0u;
-                    }
-            uint32_t mx = mask;   // exact hidden masks
-            for (uint32_t m = edge; m; m &= m - 1) {
-                const int bit = __builtin_ctz(m), net = bit >> 4, ub = (bit >> 2) & 3, i = bit & 3;
-                const double ad = preact64<MODE>(w, net ? kC1W : kA1W, net ? kC1B : kA1B, 16 * ub + j,
-                                                 cells + 16 * (4 * g + i));
-                mx = (ad > 0.0 && ad < 6.0) ? (mx | (1u << bit)) : (mx & ~(1u << bit));
-            }
-#pragma unroll
-            for (int i = 0; i < 4; i++) {
-                if (!__builtin_amdgcn_ballot_w64((((edge >> i) & 0x1111u) | ((edge >> (16 + i)) & 0x1111u) | ((near >> i) & 1u)) != 0))
-                    continue;
-                float zr[4], v, dz[4], dv, la, lc;
-                layer2(i, zr, v);
-                loss_from(4 * g + i, zr, v, dz, dv, la, lc);
-                float pos[4];   // exact logits' ReLU decisions (1 / 0)
-#pragma unroll
-                for (int k = 0; k < 4; k++)
-                    pos[k] = zr[k] > 0.0f ? 1.0f : 0.0f;
-                if ((near >> i) & 1u) {   // the group's lanes together (DPP sums within the group)
-                    const uint8_t *rc = cells + 16 * (4 * g + i);
-                    double pk[4] = {0.0, 0.0, 0.0, 0.0};
-                    for (int ub = 0; ub < 4; ub++) {
-                        const double ad = preact64<MODE>(w, kA1W, kA1B, 16 * ub + j, rc);
-                        const double h = ad < 0.0 ? 0.0 : (ad > 6.0 ? 6.0 : ad);
-#pragma unroll
-                        for (int k = 0; k < 4; k++)
-                            pk[k] = __builtin_fma((double)w1_lds[lane][40 + 4 * ub + k], h, pk[k]);
-                    }
-#pragma unroll
-                    for (int k = 0; k < 4; k++)
-                        pos[k] = (double)b2[k] + row_sum16_d(pk[k]) > 0.0 ? 1.0f : 0.0f;
-                }
-                // the hot path's terms, with its decisions, then the exact ones: backward(exact) -
-                // backward(hot) is linear in dz and dv, so run the difference on each mask set
-                float dz32[4], dzx[4];
+            if (lane == 0) {
 #pragma unroll
                 for (int k = 0; k < 4; k++) {
-                    dz32[k] = zr[k] > 0.0f ? dz[k] : 0.0f;
-                    dzx[k] = pos[k] != 0.0f ? dz[k] : 0.0f;
+                    const float d = (double)w[kA2B + k] + t[k] > 0.0 ? st[j][24 + k] : 0.0f;
+                    st[j][16 + k] = d;
+                    gb2[k] += d;
                 }
-                float ndz[4][4] = {}, pdz[4][4] = {}, ndv[4] = {}, pdv[4] = {};
-#pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    ndz[i][k] = -dz32[k];
-                    pdz[i][k] = dzx[k];
-                }
-                ndv[i] = -dv;
-                pdv[i] = dv;
-                rows_backward(ndz, ndv, 1u << i, true, mask, once);
-                rows_backward(pdz, pdv, 1u << i, true, mx, once);
             }
+        }
+        if (near_rows)
+            wave_lds_sync();
+        // ---------------- phase 2: lane = hidden unit
+        // the ReLU6 decisions 0 < a < 6, i.e. |a - 3| < 3, are taken on the fp32 values; a row whose
+        // pre-activation lies within the fp32 error bound of 0 or 6 (min(|a|, |a - 6|) = ||a - 3| - 3|)
+        // is flagged, and after the row loop its decision is redone in fp64 and, where it differs,
+        // the row's term is moved (no branch in the row loop)
+        uint32_t flagged[2] = {0u, 0u};
+#pragma unroll 1
+        for (int half = 0; half < 2; half++) {
+            uint32_t fl = 0u;
+#pragma unroll 2
+            for (int jj = 0; jj < 32; jj++) {
+                const int j = 32 * half + jj;
+                f32x2 xp[8];
+                const f32x2 ac = unit_preacts(st[j], wa, wc, bl, xp);
+                const float4 dz4 = *reinterpret_cast<const float4 *>(&st[j][16]);
+                const f32x2 dvm = *reinterpret_cast<const f32x2 *>(&st[j][20]);   // dv | max x
+                const f32x2 d = ac - f32x2{3.0f, 3.0f};
+                const f32x2 bound = __builtin_elementwise_fma(sl, f32x2{dvm.y, dvm.y}, el);
+                const int edge = (int)(fabsf(fabsf(d.x) - 3.0f) < bound.x) | (int)(fabsf(fabsf(d.y) - 3.0f) < bound.y);
+                fl = edge ? fl | (1u << jj) : fl;
+                const float hl = __builtin_amdgcn_fmed3f(ac.x, 0.0f, 6.0f), hcl = __builtin_amdgcn_fmed3f(ac.y, 0.0f, 6.0f);
+                const f32x2 sdh = w2l[0] * f32x2{dz4.x, dz4.y} + w2l[1] * f32x2{dz4.z, dz4.w};
+                const float dha = fabsf(d.x) < 3.0f ? sdh.x + sdh.y : 0.0f;
+                const float dhc = fabsf(d.y) < 3.0f ? wc2l * dvm.x : 0.0f;
+#pragma unroll
+                for (int i = 0; i < 8; i++) {
+                    ga[i] = __builtin_elementwise_fma(f32x2{dha, dha}, xp[i], ga[i]);
+                    gc[i] = __builtin_elementwise_fma(f32x2{dhc, dhc}, xp[i], gc[i]);
+                }
+                gbl += f32x2{dha, dhc};
+                g2l[0] = __builtin_elementwise_fma(f32x2{dz4.x, dz4.y}, f32x2{hl, hl}, g2l[0]);
+                g2l[1] = __builtin_elementwise_fma(f32x2{dz4.z, dz4.w}, f32x2{hl, hl}, g2l[1]);
+                gc2 = __builtin_fmaf(dvm.x, hcl, gc2);
+            }
+            flagged[half] = fl;
+        }
+        // the flagged rows of this lane's unit (~1e-5 of the decisions; lanes diverge here)
+        for (uint64_t m = ((uint64_t)flagged[1] << 32) | flagged[0]; m; m &= m - 1) {
+            const int j = __builtin_ctzll(m);
+            f32x2 xp[8];
+            const f32x2 ac = unit_preacts(st[j], wa, wc, bl, xp);
+            const float4 dz4 = *reinterpret_cast<const float4 *>(&st[j][16]);
+            const float dvr = st[j][20];
+            double ad = bl.x, cd = bl.y;
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                ad = __builtin_fma((double)wa[i].x, (double)xp[i].x, ad);
+                ad = __builtin_fma((double)wa[i].y, (double)xp[i].y, ad);
+                cd = __builtin_fma((double)wc[i].x, (double)xp[i].x, cd);
+                cd = __builtin_fma((double)wc[i].y, (double)xp[i].y, cd);
+            }
+            const bool ma = ad > 0.0 && ad < 6.0, mc = cd > 0.0 && cd < 6.0;
+            const bool ma32 = fabsf(ac.x - 3.0f) < 3.0f, mc32 = fabsf(ac.y - 3.0f) < 3.0f;
+            const f32x2 sdh = w2l[0] * f32x2{dz4.x, dz4.y} + w2l[1] * f32x2{dz4.z, dz4.w};
+            // + the row's term where the exact decision is "on", - where the fp32 one was
+            const float dha = ma == ma32 ? 0.0f : (ma ? sdh.x + sdh.y : -(sdh.x + sdh.y));
+            const float dhc = mc == mc32 ? 0.0f : (mc ? wc2l * dvr : -(wc2l * dvr));
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                ga[i] = __builtin_elementwise_fma(f32x2{dha, dha}, xp[i], ga[i]);
+                gc[i] = __builtin_elementwise_fma(f32x2{dhc, dhc}, xp[i], gc[i]);
+            }
+            gbl += f32x2{dha, dhc};
         }
     }
     // ---------------- this wave's record (FlatParams order)
     float *rec = partials + ((int64_t)blockIdx.x * kTrainWaves + wave) * kRec;
 #pragma unroll
-    for (int ub = 0; ub < 4; ub++) {
-        const int u = 16 * ub + j;
-        *reinterpret_cast<float4 *>(rec + kA1W + 16 * u + 4 * g) = make_float4(gw1[0][ub][0], gw1[0][ub][1], gw1[0][ub][2], gw1[0][ub][3]);
-        *reinterpret_cast<float4 *>(rec + kC1W + 16 * u + 4 * g) = make_float4(gw1[1][ub][0], gw1[1][ub][1], gw1[1][ub][2], gw1[1][ub][3]);
+    for (int q = 0; q < 4; q++) {
+        *reinterpret_cast<float4 *>(rec + kA1W + 16 * lane + 4 * q) =
+            make_float4(ga[2 * q].x, ga[2 * q].y, ga[2 * q + 1].x, ga[2 * q + 1].y);
+        *reinterpret_cast<float4 *>(rec + kC1W + 16 * lane + 4 * q) =
+            make_float4(gc[2 * q].x, gc[2 * q].y, gc[2 * q + 1].x, gc[2 * q + 1].y);
     }
-    // per-lane partials over the four lane groups (fixed order: (g0 + g1) + (g2 + g3) in every lane)
-    auto groups = [](float x) {
-        x += __shfl_xor(x, 16);
-        return x + __shfl_xor(x, 32);
-    };
-#pragma unroll
-    for (int ub = 0; ub < 4; ub++) {
-        const int u = 16 * ub + j;
-        const float4 a2 = reinterpret_cast<const float4 *>(acc)[2 * ub], a1 = reinterpret_cast<const float4 *>(acc)[2 * ub + 1];
-        const float a1b = groups(a1.y), c1b = groups(a1.z), c2w = groups(a1.x);
-        const float a2w[4] = {groups(a2.x), groups(a2.y), groups(a2.z), groups(a2.w)};
-        if (g == 0) {
-            rec[kA1B + u] = a1b;
-            rec[kC1B + u] = c1b;
-            rec[kC2W + u] = c2w;
-#pragma unroll
-            for (int k = 0; k < 4; k++)
-                rec[kA2W + 64 * k + u] = a2w[k];
-        }
-    }
-    const float s0 = wave_sum(gb2[0]), s1s = wave_sum(gb2[1]), s2 = wave_sum(gb2[2]), s3 = wave_sum(gb2[3]);
+    rec[kA1B + lane] = gbl.x;
+    rec[kC1B + lane] = gbl.y;
+    rec[kA2W + lane] = g2l[0].x;
+    rec[kA2W + 64 + lane] = g2l[0].y;
+    rec[kA2W + 128 + lane] = g2l[1].x;
+    rec[kA2W + 192 + lane] = g2l[1].y;
+    rec[kC2W + lane] = gc2;
+    const float s0 = wave_sum(gb2[0]), s1 = wave_sum(gb2[1]), s2 = wave_sum(gb2[2]), s3 = wave_sum(gb2[3]);
     const float sc = wave_sum(gbc2), la = wave_sum(loss_a), lc = wave_sum(loss_c);
     if (lane == 0) {
-        *reinterpret_cast<float4 *>(rec + kA2B) = make_float4(s0, s1s, s2, s3);
+        *reinterpret_cast<float4 *>(rec + kA2B) = make_float4(s0, s1, s2, s3);
         rec[kC2B] = sc;
         rec[kRecLossA] = la;
         rec[kRecLossC] = lc;
@@ -871,7 +619,7 @@ __global__ __launch_bounds__(256) void k_mlp_reduce2(const float4 *__restrict__ 
     out[e] = s;
 }
 
-constexpr int kTrainGroups = 512;    // persistent grid: two workgroups of 4 waves per CU (two waves per SIMD) on 256 CUs
+constexpr int kTrainGroups = 1024;   // persistent grid: 4 workgroups of 4 waves per CU on 256 CUs
 
 int fail(int code, const std::string &msg)
 {
