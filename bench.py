@@ -130,6 +130,7 @@ def _load_profile(name):
 
 SETTLE_S = 0.3   # minimum untimed stepping before a timed region: GPU clocks ramp over ~20 ms+
 SYNC_POLL = False  # --sync: poll the region's last HIP event before the closing synchronize
+SETTLE_SPIN = False  # --settle-spin: the settle loop polls its last event instead of sleeping in the wait
 DRY_PASSES = 3  # --dry-passes: untimed passes through the region's exact host path before t0
 CLOSE_DEVICE = False  # --close device: t1 after torch.cuda.synchronize() instead of the last event's wait
 
@@ -150,10 +151,15 @@ def timed_steps(env, plan, W, chunk, world, dev):
     for c in chunks(W, chunk) if W else []:
         env.step_n(c, auto_reset=True)
     torch.cuda.synchronize(dev)
+    s = torch.cuda.current_stream(dev)
+    done_ev = torch.cuda.Event()
     while time.perf_counter() - t_w < SETTLE_S:
         env.step_n(chunk, auto_reset=True)
+        if SETTLE_SPIN:
+            done_ev.record(s)
+            while not done_ev.query():
+                pass
         torch.cuda.synchronize(dev)
-    s = torch.cuda.current_stream(dev)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in plan]
     # untimed passes through the region's exact host path (event records, the calls, the closing
     # event wait): torch creates the HIP events at their first record, which does not belong in the
@@ -490,7 +496,7 @@ def hip_schedule_spin(local):
 
 
 def main():
-    global SYNC_POLL, SETTLE_S, CLOSE_DEVICE, DRY_PASSES
+    global SYNC_POLL, SETTLE_S, CLOSE_DEVICE, DRY_PASSES, SETTLE_SPIN
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=6000)
@@ -512,11 +518,14 @@ def main():
     ap.add_argument("--close", choices=("event", "device"), default="event",
                     help="end of the timed region: wait on the region's last HIP event (event) or on the "
                          "device (torch.cuda.synchronize) before t1")
+    ap.add_argument("--settle-spin", action="store_true",
+                    help="the settle loop spins on its last event instead of sleeping in the blocking wait")
     ap.add_argument("--dry-passes", type=int, default=DRY_PASSES,
                     help="untimed passes through the timed region's exact host path before t0")
     args = ap.parse_args()
     SYNC_POLL = args.sync == "poll"
     DRY_PASSES = args.dry_passes
+    SETTLE_SPIN = args.settle_spin
     CLOSE_DEVICE = args.close == "device"
     SETTLE_S = args.settle
 
