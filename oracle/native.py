@@ -44,6 +44,7 @@ def lib():
             "orc_mt_random": (C.c_double, [P]),
             "orc_pyrand_episode": (C.c_int, [P, C.c_int] + [P] * 9),
             "orc_philox4x32_10": (None, [P, P, P]),
+            "orc_philox4x32_r": (None, [P, P, P, C.c_int]),
             "orc_step_philox": (C.c_int64, [P, C.c_int64, C.c_uint64, C.c_int64, C.c_uint32, C.c_uint32,
                                             P, P, P, P, P]),
             "orc_step_draws": (C.c_int64, [P, C.c_int64, P, P, P, P, P, P, C.c_uint32]),
@@ -162,11 +163,14 @@ def score(boards):
     return out
 
 
-def philox(ctr, key):
+def philox(ctr, key, rounds=10):
     c = np.ascontiguousarray(ctr, np.uint32)
     k = np.ascontiguousarray(key, np.uint32)
     out = np.zeros(4, np.uint32)
-    lib().orc_philox4x32_10(_p(c), _p(k), _p(out))
+    if rounds == 10:
+        lib().orc_philox4x32_10(_p(c), _p(k), _p(out))
+    else:
+        lib().orc_philox4x32_r(_p(c), _p(k), _p(out), int(rounds))
     return out
 
 

@@ -94,6 +94,31 @@ def test_philox_known_answers():
         [0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1]
 
 
+def _philox_py(ctr, key, rounds):
+    """Philox4x32-R restated in plain Python from the Random123 paper (Salmon et al., SC'11): the
+    check of the oracle's round-count parameter (Random123's KATs above cover 10 rounds only)."""
+    c0, c1, c2, c3 = ctr
+    k0, k1 = key
+    m = 0xFFFFFFFF
+    for _ in range(rounds):
+        p0, p1 = 0xD2511F53 * c0, 0xCD9E8D57 * c2
+        c0, c1, c2, c3 = ((p1 >> 32) ^ c1 ^ k0) & m, p1 & m, ((p0 >> 32) ^ c3 ^ k1) & m, p0 & m
+        k0, k1 = (k0 + 0x9E3779B9) & m, (k1 + 0xBB67AE85) & m
+    return [c0, c1, c2, c3]
+
+
+def test_philox_rounds_parameter():
+    """The oracle's Philox4x32-R (draw contract 3: the env step's draws use R = 7) equals the
+    plain-Python restatement, which itself reproduces the 10-round KATs."""
+    assert _philox_py([0, 0, 0, 0], [0, 0], 10) == [0x6627e8d5, 0xe169c58d, 0xbc57ac4c, 0x9b00dbd8]
+    rng = np.random.default_rng(7)
+    for _ in range(64):
+        ctr = [int(v) for v in rng.integers(0, 2 ** 32, 4)]
+        key = [int(v) for v in rng.integers(0, 2 ** 32, 2)]
+        for rounds in (7, 10):
+            assert O.philox(ctr, key, rounds).tolist() == _philox_py(ctr, key, rounds), (ctr, key, rounds)
+
+
 def test_python_port_matches_reference_trajectories(golden):
     """oracle/game_port.py (the CPU baseline) plays the same seeded games as the reference."""
     z = golden["traj"]
