@@ -3,8 +3,8 @@ HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -Wall -Wno-unused-function
 LIBDIR := rein48_amd/lib
-SRC := rein48_amd/csrc/r48_env.hip rein48_amd/csrc/r48_a3c.hip rein48_amd/csrc/r48_policy.hip rein48_amd/csrc/r48_replay.hip rein48_amd/csrc/r48_dqn.hip rein48_amd/csrc/r48_resnet.hip rein48_amd/csrc/r48_a3c_train.hip rein48_amd/csrc/r48_bn.hip rein48_amd/csrc/r48_conv.hip rein48_amd/csrc/r48_game.hip rein48_amd/csrc/r48_mlp.hip
-DEPS := rein48_amd/csrc/r48_board.h rein48_amd/csrc/r48_cnn_common.h include/rein48.h
+SRC := rein48_amd/csrc/r48_env.hip rein48_amd/csrc/r48_a3c.hip rein48_amd/csrc/r48_policy.hip rein48_amd/csrc/r48_replay.hip rein48_amd/csrc/r48_dqn.hip rein48_amd/csrc/r48_resnet.hip rein48_amd/csrc/r48_a3c_train.hip rein48_amd/csrc/r48_bn.hip rein48_amd/csrc/r48_conv.hip rein48_amd/csrc/r48_game.hip rein48_amd/csrc/r48_mlp.hip rein48_amd/csrc/r48_mlp_train.hip
+DEPS := rein48_amd/csrc/r48_board.h rein48_amd/csrc/r48_cnn_common.h rein48_amd/csrc/r48_mlp_common.h include/rein48.h
 
 all: $(LIBDIR)/librein48.so oracle
 
@@ -17,6 +17,8 @@ FLAGS_r48_policy ?=
 # the cell-grouped ResNet kernel keeps its 16 x 4 live accumulators in VGPRs (the epilogue reads
 # them without v_accvgpr_read) and the block input in AGPRs
 FLAGS_r48_resnet ?= -mllvm -amdgpu-mfma-vgpr-form=1
+# the MLP update: no SLP packing of its scalar f32 adds / FMAs (packed f32 VALU issues at half rate)
+FLAGS_r48_mlp_train ?= -fno-slp-vectorize
 
 $(LIBDIR)/librein48.so: $(OBJ)
 	@mkdir -p $(LIBDIR)

@@ -269,7 +269,7 @@ class A3CTrainer:
                 stats = {"B": self.mask.float().sum(0).clamp(min=1.0)}
         if fused_upd:
             # pass 2 as ONE fused kernel over all T x n states (no activation hits HBM): MFMA for the
-            # CNN (r48_a3c_train.hip), fp32 VALU for the reference MLP (r48_mlp.hip)
+            # CNN (r48_a3c_train.hip), fp32 MFMA + VALU for the reference MLP (r48_mlp_train.hip)
             actor_total, critic_total = self._fused_gradient(states, targets, stats)
             self.flat.allreduce_grad(self.group)
             self.opt.step()

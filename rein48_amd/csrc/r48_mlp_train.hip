@@ -1,0 +1,724 @@
+// r48_mlp_train.hip -- the fused A3C update of the reference's own network (algorithm/a3c/a3c.py:99-169,
+// fp32) on gfx950: r48_mlp_train_grad (include/rein48.h). The forward / rollout kernels are in
+// r48_mlp.hip; this file is built on its own because its scalar f32 VALU code must not be SLP-packed
+// (packed f32 VALU issues at half rate; Makefile FLAGS_r48_mlp_train).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <string>
+
+#include "../../include/rein48.h"
+#include "r48_mlp_common.h"
+
+namespace r48 {
+void set_last_error(const std::string &msg);
+}
+
+namespace {
+
+using namespace r48mlp;
+
+// ---------------------------------------------------------------- fused update
+// k_mlp_train: the gradient of the A3C loss (rein48_amd/a3c/losses.py restating a3c.py:99-123,
+// textbook or the reference's broadcast actor loss; the per-row formulas of r48_a3c_train.hip's
+// k_cnn_train) w.r.t. all 2,501 parameters, fp32, in ONE pass over the training states.
+// The two 16 -> 64 layers are the bulk of the work (4,096 of ~5,000 FMAs per row: the forward and the
+// dW1 contraction of both networks) and run on the fp32 MFMA (v_mfma_f32_16x16x4_f32: bit-for-bit
+// a k-ordered fmaf chain, 1,024 FMAs per 32-cycle issue); the rest is VALU. The f32 MFMA runs at the
+// f32 VALU rate and did not co-execute with the VALU here (SQ_VALU_MFMA_COEXEC_CYCLES 0): what it
+// buys is instruction count -- 4 MFMAs per row for the 4,096 FMAs -- not overlap. A wave takes 16 rows
+// per tile in ONE orientation, rows in registers and hidden units on the lanes:
+//   layer 1   pre-activation P[r][u] = b1[u] + sum_f x[r][f] W1[u][f] (one fmaf chain over f = 0..15):
+//             A = x (16 rows x 4 inputs per k-step, lane j + 16g holds x[r0 + j][4s + g]), B = W1^T
+//             (lane j + 16g: W1[16ub + j][4s + g], constant); D lane j + 16g, register i = row
+//             4g + i, unit 16ub + j.  2 nets x 4 unit blocks x 4 k-steps = 32 MFMAs per tile
+//   ReLU6     mask / h elementwise in that layout (exact decisions near 0 and 6, below)
+//   layer 2   logits and value of row 4g + i: each lane sums its 4 units, the 16 lanes of the row
+//             group add up with a DPP rotation butterfly (every lane gets the bitwise same sum)
+//   loss      per row (every lane of the group, counted once): softmax, entropy, td -> dz, dv
+//   dh        [mask] W2^T dz / [mask] wc2 dv, elementwise; db1, dW2, dwc2 in per-lane partials
+//   dW1       += x^T dh on the MFMA: A = x^T (lane j + 16g, k-step i: x[r0 + 4g + i][j]), B = dh (the
+//             layer-1 layout IS the B layout of a k = rows contraction), C = dW1^T (f x units, 4
+//             accumulators per net and unit block, in AGPRs).  32 MFMAs per tile
+// Per wave one record of the flat gradient in FlatParams order (a1.w [64][16] | a1.b | a2.w [4][64] |
+// a2.b | c1.w | c1.b | c2.w | c2.b) + the two losses; k_mlp_reduce sums the records in a fixed order
+// (deterministic).
+// The ReLU derivatives are decisions at 0 (and 6, ReLU6): an fp32 pre-activation within its rounding
+// error of the boundary may land on the other side than the exact value, and with raw tile values as
+// inputs (up to 2^17) a flipped hidden-unit mask moves a weight-gradient entry by a whole row's term
+// (dh x). So the update decides them on exact-enough values: a hidden pre-activation or a logit whose
+// fp32 value lies within its fp32 error bound of the boundary is recomputed in fp64 (rare: a branch
+// taken by ~1e-5 of the units, ~1e-3 of the rows' logits).
+constexpr int kTrainWaves = 4;
+constexpr int kRec = 2504;                 // 2,501 gradient floats + actor loss + critic loss + pad
+constexpr int kRecLossA = 2501, kRecLossC = 2502;
+// (the record's section offsets equal the blob's, kA1W .. kC2B; inside a1 / a2 / c1 the record has
+// the parameters' own [out][in] order)
+constexpr float kEntropyEps = 1e-5f;       // a3c.py:114
+constexpr float kLn2 = 0.69314718055994531f;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// the wave's LDS board area is written and read by different lanes: every outstanding LDS
+// operation completes (s_waitcnt lgkmcnt(0)) before the next access, and the compiler moves no LDS
+// access across the point
+__device__ __forceinline__ void wave_lds_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ float uniform(float v)
+{
+    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
+}
+
+__device__ __forceinline__ float wave_sum(float v)
+{
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1)
+        v += __shfl_xor(v, m);
+    return v;
+}
+
+// all-reduce over the 16 lanes of a DPP row by rotations 8, 4, 2, 1: at every level a lane adds
+// the same two operands as its partner (IEEE addition commutes), so all 16 lanes get the bitwise
+// same sum
+template <int N>
+__device__ __forceinline__ float row_ror(float v)
+{
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x120 + N, 0xF, 0xF, true));
+}
+__device__ __forceinline__ float row_sum16(float v)
+{
+    v += row_ror<8>(v);
+    v += row_ror<4>(v);
+    v += row_ror<2>(v);
+    v += row_ror<1>(v);
+    return v;
+}
+template <int N>
+__device__ __forceinline__ double row_ror_d(double v)
+{
+    const uint64_t u = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)u, 0x120 + N, 0xF, 0xF, true);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(u >> 32), 0x120 + N, 0xF, 0xF, true);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+__device__ __forceinline__ double row_sum16_d(double v)
+{
+    v += row_ror_d<8>(v);
+    v += row_ror_d<4>(v);
+    v += row_ror_d<2>(v);
+    v += row_ror_d<1>(v);
+    return v;
+}
+
+// blob accessors (pack_mlp layout: layer-1 and W2 grouped by hidden-unit pair)
+__device__ __forceinline__ float w1_at(const float *w, int base, int u, int f) { return w[base + 32 * (u >> 1) + 2 * f + (u & 1)]; }
+__device__ __forceinline__ float w2_at(const float *w, int u, int k) { return w[kA2W + 8 * (u >> 1) + 2 * k + (u & 1)]; }
+
+// fp64 pre-activation of hidden unit u of one network on the row whose 16 cell bytes are `cells`
+template <int MODE>
+__device__ __forceinline__ double preact64(const float *w, int base, int bbase, int u, const uint8_t *cells)
+{
+    // the weights are re-read here, on the rare path: an opaque pointer keeps the compiler from
+    // hoisting these loop-invariant loads out of the tile loop into 128 live registers
+    uint64_t wa = reinterpret_cast<uint64_t>(w);
+    asm volatile("" : "+s"(wa));
+    w = reinterpret_cast<const float *>(wa);
+    double a = w[bbase + u];
+    for (int f = 0; f < 16; f++)
+        a = __builtin_fma((double)w1_at(w, base, u, f), (double)cell_input<MODE>(cells[f]), a);
+    return a;
+}
+
+// per-wave LDS area of a 16-row tile (32-bit words): boards [16][4] | max input | row weight |
+// target | action | cm | counts [16][4] | pre-ReLU logits [16][4] | value | dz through the logits'
+// ReLU [16][4] | dv | near flag
+constexpr int kTB = 0, kTXm = 64, kTWt = 80, kTTg = 96, kTAc = 112, kTCm = 128, kTCn = 144, kTZr = 208, kTV = 272,
+              kTDz = 288, kTDv = 352, kTNr = 368, kTileWords = 384;
+
+// the inputs of one training row, loaded a tile ahead by lane j of every lane group
+struct RowIn {
+    uint4 b;
+    float wt, tgt, c;
+    int a;
+    float4 cnt;
+};
+
+template <bool REF>
+__device__ __forceinline__ RowIn fetch_row(int64_t r, int64_t rows, int64_t n_boards, const int8_t *boards,
+                                           const int8_t *actions, const float *targets, const float *wn,
+                                           const float *cm, const float *counts)
+{
+    const bool live = r < rows;
+    const int64_t rr = live ? r : rows - 1;   // padding rows: a valid row with weight 0
+    RowIn x;
+    x.b = *reinterpret_cast<const uint4 *>(boards + 16 * rr);
+    x.wt = live ? wn[rr] : 0.0f;
+    x.tgt = targets[rr];
+    x.a = actions[rr] & 3;
+    x.c = 0.0f;
+    x.cnt = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (REF) {
+        x.c = live ? cm[rr] : 0.0f;
+        const int64_t bidx = rows <= 0xFFFFFFFFll ? (int64_t)((uint32_t)rr % (uint32_t)n_boards) : rr % n_boards;
+        x.cnt = *reinterpret_cast<const float4 *>(counts + 4 * bidx);
+    }
+    return x;
+}
+
+template <int MODE, bool REF>
+__global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_eu(2))) void k_mlp_train(
+    const int8_t *__restrict__ boards, int64_t rows, int64_t n_boards, const int8_t *__restrict__ actions,
+    const float *__restrict__ targets, const float *__restrict__ wn, const float *__restrict__ cm,
+    const float *__restrict__ counts, float beta, const float *__restrict__ w, float *__restrict__ partials)
+{
+    // per wave: the tile's 16 boards (64 words) and each row's largest input; per workgroup: the
+    // layer-1 B operands and biases of every lane (read back each tile: 40 registers the rest of
+    // the tile needs)
+    __shared__ __attribute__((aligned(16))) uint32_t tiles_lds[kTrainWaves][kTileWords];
+    __shared__ __attribute__((aligned(16))) float w1_lds[64][60];
+    // per lane: the db1 / dW2 / dwc2 partials, per unit block [dW2[k] x 4 | dwc2 | db1 | dbc1 | pad]
+    // (read-modified-written by the backward one unit block at a time: registers for two waves per
+    // SIMD)
+    __shared__ __attribute__((aligned(16))) float acc_lds[kTrainWaves][64][36];   // 36: conflict-free b128 reads and writes
+    const int lane = threadIdx.x & 63, j = lane & 15, g = lane >> 4;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint32_t *bw = tiles_lds[wave];
+    const uint8_t *cells = reinterpret_cast<const uint8_t *>(bw);
+    constexpr int kW1[2] = {kA1W, kC1W}, kB1[2] = {kA1B, kC1B};
+
+    // constants of lane (j, g)'s units 16ub + j: layer-1 B operands (inputs 4s + g) and biases in
+    // LDS (w1_lds[lane][8 (net, ub) + s], [32 + (net, ub)]), W2 / wc2 entries in registers
+    if (threadIdx.x < 64) {
+#pragma unroll
+        for (int net = 0; net < 2; net++)
+#pragma unroll
+            for (int ub = 0; ub < 4; ub++) {
+                const int u = 16 * ub + j;
+#pragma unroll
+                for (int s4 = 0; s4 < 4; s4++)
+                    w1_lds[lane][4 * (4 * net + ub) + s4] = w1_at(w, kW1[net], u, 4 * s4 + g);
+                w1_lds[lane][32 + 4 * net + ub] = w[kB1[net] + u];
+            }
+#pragma unroll
+        for (int ub = 0; ub < 4; ub++) {
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                w1_lds[lane][40 + 4 * ub + k] = w2_at(w, 16 * ub + j, k);
+            w1_lds[lane][56 + ub] = w[kC2W + 16 * ub + j];
+        }
+    }
+    float *acc = acc_lds[wave][lane];
+#pragma unroll
+    for (int q = 0; q < 8; q++)
+        reinterpret_cast<float4 *>(acc)[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+    __syncthreads();
+    const float4 *wl = reinterpret_cast<const float4 *>(w1_lds[lane]);   // this lane's constants
+    // fp32 error bound of a hidden pre-activation: 16 roundings below |b| + sum |w| max x, i.e.
+    // < 2^-20 (|b| + sum |w| max x); 2x margin, + 2^-21 for the rounding of the decision's a - 3;
+    // with the largest |b| and sum |w| of the network's 64 units (wave-uniform, SGPRs)
+    float s1[2], e1[2];
+#pragma unroll
+    for (int net = 0; net < 2; net++) {
+        float sm = 0.f, bm = 0.f;
+        for (int u = 0; u < 64; u++) {
+            float sa = 0.f;
+            for (int f = 0; f < 16; f++)
+                sa += fabsf(w1_at(w, kW1[net], u, f));
+            sm = fmaxf(sm, sa);
+            bm = fmaxf(bm, fabsf(w[kB1[net] + u]));
+        }
+        s1[net] = uniform(sm * 0x1p-19f);
+        e1[net] = uniform(fmaf(bm, 0x1p-19f, 0x1p-21f));
+    }
+    // fp32 error bound of a pre-ReLU logit: its own sum (64 products of |h| <= 6: < 2^-18 (|b2| +
+    // 6 sum |W2[k][:]|)) plus the hidden units' errors carried through W2 (each < 2^-20 (|b1| +
+    // sum |W1[u][:]| max x)); 2x-4x margins (wave-uniform: kept in SGPRs)
+    float zedge[4], zcarry[4], hb = 0.f, hw = 0.f;
+    for (int u = 0; u < 64; u++) {
+        float sw = 0.f;
+        for (int f = 0; f < 16; f++)
+            sw += fabsf(w1_at(w, kA1W, u, f));
+        hw = fmaxf(hw, sw);
+        hb = fmaxf(hb, fabsf(w[kA1B + u]));
+    }
+    float b2[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        float sa = 0.f;
+        for (int u = 0; u < 64; u++)
+            sa += fabsf(w2_at(w, u, k));
+        zedge[k] = uniform((fabsf(w[kA2B + k]) + 6.0f * sa) * 0x1p-16f);
+        zcarry[k] = uniform(sa * 0x1p-19f);
+        b2[k] = uniform(w[kA2B + k]);
+    }
+    hb = uniform(hb);
+    hw = uniform(hw);
+    const float bc2 = uniform(w[kC2B]);
+
+    // accumulators: dW1^T per net and unit block (MFMA C: f = 4g + i, unit 16ub + j), per-lane
+    // partials of db1, dW2, dwc2 (summed over the lane's rows; the four lane groups are added at the
+    // end), per-row sums (counted in the lanes j == 0)
+    f32x4 gw1[2][4];
+#pragma unroll
+    for (int ub = 0; ub < 4; ub++)
+        gw1[0][ub] = gw1[1][ub] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float gb2[4] = {0.f, 0.f, 0.f, 0.f}, gbc2 = 0.f, loss_a = 0.f, loss_c = 0.f;
+    const float once = j == 0 ? 1.0f : 0.0f;   // the fix-up's per-row sums: one lane of the row group
+
+    const int64_t n_tiles = (rows + 15) / 16;
+    const int64_t stride = (int64_t)gridDim.x * kTrainWaves;
+    int64_t tile = (int64_t)blockIdx.x * kTrainWaves + wave;
+    // one wave per SIMD hides no load latency: row r0 + j's inputs arrive a tile ahead
+    RowIn next = fetch_row<REF>(std::min<int64_t>(tile, n_tiles - 1) * 16 + j, rows, n_boards, boards, actions, targets,
+                                wn, cm, counts);
+    for (; tile < n_tiles; tile += stride) {
+        // ---------------- inputs: row r0 + j in the four lanes j + 16g
+        const RowIn in = next;
+        next = fetch_row<REF>(std::min<int64_t>(tile + stride, n_tiles - 1) * 16 + j, rows, n_boards, boards, actions,
+                              targets, wn, cm, counts);
+        const uint4 bv = in.b;
+        const uint32_t bwd[4] = {bv.x, bv.y, bv.z, bv.w};
+        float xa[4];   // A operands of layer 1: x[r0 + j][4s + g]
+#pragma unroll
+        for (int s4 = 0; s4 < 4; s4++)
+            xa[s4] = cell_input<MODE>((bwd[s4] >> (8 * g)) & 0xFFu);
+        uint32_t mb = 0;   // largest cell byte of the row (inputs grow with it)
+#pragma unroll
+        for (int s4 = 0; s4 < 4; s4++)
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                mb = std::max(mb, (bwd[s4] >> (8 * q)) & 0xFFu);
+        wave_lds_sync();   // the previous tile's reads of the board area are done
+        if (g == 0) {
+            *reinterpret_cast<uint4 *>(bw + kTB + 4 * j) = bv;
+            bw[kTXm + j] = __float_as_uint(cell_input<MODE>(mb));
+            bw[kTWt + j] = __float_as_uint(in.wt);
+            bw[kTTg + j] = __float_as_uint(in.tgt);
+            bw[kTAc + j] = (uint32_t)in.a;
+            if (REF) {
+                bw[kTCm + j] = __float_as_uint(in.c);
+                *reinterpret_cast<float4 *>(bw + kTCn + 4 * j) = in.cnt;
+            }
+        }
+        wave_lds_sync();
+        float xt[4], xm[4];   // A operands of dW1: x[r0 + 4g + i][j]; max input of row 4g + i
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            xt[i] = cell_input<MODE>(cells[16 * (4 * g + i) + j]);
+            xm[i] = __uint_as_float(bw[kTXm + 4 * g + i]);
+        }
+
+        // ---------------- layer 1 on the MFMA: register i = row 4g + i, lane j = unit 16ub + j
+        f32x4 pre[2][4];
+        const float4 bl0 = wl[8], bl1 = wl[9];
+        const float b1[2][4] = {{bl0.x, bl0.y, bl0.z, bl0.w}, {bl1.x, bl1.y, bl1.z, bl1.w}};
+#pragma unroll
+        for (int net = 0; net < 2; net++)
+#pragma unroll
+            for (int ub = 0; ub < 4; ub++) {
+                const float4 wb = wl[4 * net + ub];
+                f32x4 acc = f32x4{b1[net][ub], b1[net][ub], b1[net][ub], b1[net][ub]};
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[0], wb.x, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[1], wb.y, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[2], wb.z, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[3], wb.w, acc, 0, 0, 0);
+                pre[net][ub] = acc;
+            }
+        // ---------------- ReLU6 decisions 0 < a < 6, i.e. |a - 3| < 3; within the fp32 error bound
+        // of 0 or 6 (min(|a|, |a - 6|) = ||a - 3| - 3|) the pre-activation is redone in fp64
+        // (the hot path takes the fp32 decision where it uses a mask and only asks whether any of
+        // the tile's 512 pre-activations is near a boundary; the fix-up below finds which)
+        float bound[2][4];
+#pragma unroll
+        for (int net = 0; net < 2; net++)
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+                bound[net][i] = fmaf(s1[net], xm[i], e1[net]);
+        bool edge_any = false;
+#pragma unroll
+        for (int net = 0; net < 2; net++)
+#pragma unroll
+            for (int ub = 0; ub < 4; ub++)
+#pragma unroll
+                for (int i = 0; i < 4; i++)
+                    edge_any |= fabsf(fabsf(pre[net][ub][i] - 3.0f) - 3.0f) < bound[net][i];
+        // ---------------- per row i of the lane group (rows 4g + i): layer 2 (the group's 16 lanes
+        // add up), the loss (every lane of the group computes it; counted once) -- the same code on
+        // the hot path and in the exact-decision fix-up below, so the same values
+        auto layer2 = [&](int i, float (&zr)[4], float &v) {
+            float pk[4] = {0.f, 0.f, 0.f, 0.f}, pv = 0.f;
+            const float4 c2 = wl[14];   // wc2 of the lane's 4 units
+            const float wc2[4] = {c2.x, c2.y, c2.z, c2.w};
+#pragma unroll
+            for (int ub = 0; ub < 4; ub++) {
+                const float4 w4 = wl[10 + ub];   // W2[k][16ub + j]
+                const float ha = __builtin_amdgcn_fmed3f(pre[0][ub][i], 0.0f, 6.0f);
+                pk[0] = fmaf(w4.x, ha, pk[0]);
+                pk[1] = fmaf(w4.y, ha, pk[1]);
+                pk[2] = fmaf(w4.z, ha, pk[2]);
+                pk[3] = fmaf(w4.w, ha, pk[3]);
+                pv = fmaf(wc2[ub], __builtin_amdgcn_fmed3f(pre[1][ub][i], 0.0f, 6.0f), pv);
+            }
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                zr[k] = b2[k] + row_sum16(pk[k]);   // pre-ReLU
+            v = bc2 + row_sum16(pv);
+        };
+        // the loss of tile row ri from its pre-ReLU logits and value
+        auto loss_from = [&](int ri, const float (&zr)[4], float v, float (&dz)[4], float &dv, float &la, float &lc) {
+            const float wt = __uint_as_float(bw[kTWt + ri]);
+            const float tgt = __uint_as_float(bw[kTTg + ri]);
+            const int a = (int)bw[kTAc + ri];
+            float z[4], p[4], gr[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                z[k] = fmaxf(zr[k], 0.0f);                            // the logits' ReLU (a3c.py:153)
+            const float mz = fmaxf(fmaxf(z[0], z[1]), fmaxf(z[2], z[3]));
+            float se = 0.f;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                p[k] = __expf(z[k] - mz);
+                se += p[k];
+            }
+            const float inv = __builtin_amdgcn_rcpf(se), lse = mz + kLn2 * __builtin_amdgcn_logf(se);
+            float H = 0.f, gbar = 0.f;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                p[k] *= inv;
+                const float lq = kLn2 * __builtin_amdgcn_logf(p[k] + kEntropyEps);
+                H -= p[k] * lq;
+                gr[k] = -(lq + p[k] * __builtin_amdgcn_rcpf(p[k] + kEntropyEps));   // dH/dp_k
+                gbar += p[k] * gr[k];
+            }
+            const float td = tgt - v;
+            if (REF) {   // reference: -beta wn H - cm sum_k c_k log p_k  (losses.py, a3c.py:110-116)
+                const float c = __uint_as_float(bw[kTCm + ri]);
+                const float4 cnt = *reinterpret_cast<const float4 *>(bw + kTCn + 4 * ri);
+                const float ck[4] = {cnt.x, cnt.y, cnt.z, cnt.w}, C = cnt.x + cnt.y + cnt.z + cnt.w;
+                float sa = 0.f;
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    dz[k] = -beta * wt * p[k] * (gr[k] - gbar) - c * (ck[k] - p[k] * C);
+                    sa += ck[k] * (z[k] - lse);
+                }
+                la = -beta * wt * H - c * sa;
+            } else {     // textbook: -wn (beta H + td log p[a]), td constant for the actor
+#pragma unroll
+                for (int k = 0; k < 4; k++)
+                    dz[k] = -wt * (beta * p[k] * (gr[k] - gbar) + td * ((k == a ? 1.0f : 0.0f) - p[k]));
+                la = -wt * (beta * H + td * (z[a] - lse));
+            }
+            dv = -2.0f * wt * td;                                      // critic = wn td^2
+            lc = wt * td * td;
+        };
+        // the backward of the lane group's 4 rows with output gradients dz (through the logits' ReLU)
+        // and dv, and hidden masks (the fp32 decisions, or the given bits in the fix-up): the per-lane
+        // partials (in LDS, one unit block at a time) and the rows' k-steps of dW1 on the MFMA
+        // (register i = row, lane = unit); `sel` picks the rows (bit i), the fix-up runs it on
+        // differences
+        auto rows_backward = [&](const float (&dz)[4][4], const float (&dv)[4], uint32_t sel, bool bits, uint32_t mk,
+                                 float scale_once) {
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                if (!((sel >> i) & 1u))
+                    continue;
+#pragma unroll
+                for (int k = 0; k < 4; k++)
+                    gb2[k] += scale_once * dz[i][k];
+                gbc2 += scale_once * dv[i];
+            }
+            const float4 c2 = wl[14];
+            const float wc2[4] = {c2.x, c2.y, c2.z, c2.w};
+#pragma unroll
+            for (int ub = 0; ub < 4; ub++) {
+                const float4 w4 = wl[10 + ub];
+                float4 a2 = reinterpret_cast<float4 *>(acc)[2 * ub];        // dW2[k][16ub + j] partials
+                float4 a1 = reinterpret_cast<float4 *>(acc)[2 * ub + 1];    // dwc2 | db1 | dbc1 | -
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    if (!((sel >> i) & 1u))
+                        continue;
+                    const float ha = __builtin_amdgcn_fmed3f(pre[0][ub][i], 0.0f, 6.0f);
+                    const float hc = __builtin_amdgcn_fmed3f(pre[1][ub][i], 0.0f, 6.0f);
+                    const float sdh = fmaf(w4.w, dz[i][3], fmaf(w4.z, dz[i][2], fmaf(w4.y, dz[i][1], w4.x * dz[i][0])));
+                    // the masks: the given bits (fix-up) or the fp32 decisions 0 < a < 6, i.e. |a - 3| < 3
+                    const bool ma = bits ? ((mk >> (4 * ub + i)) & 1u) != 0 : fabsf(pre[0][ub][i] - 3.0f) < 3.0f;
+                    const bool mc = bits ? ((mk >> (16 + 4 * ub + i)) & 1u) != 0 : fabsf(pre[1][ub][i] - 3.0f) < 3.0f;
+                    const float dha = ma ? sdh : 0.0f;
+                    const float dhc = mc ? wc2[ub] * dv[i] : 0.0f;
+                    a2.x = fmaf(dz[i][0], ha, a2.x);
+                    a2.y = fmaf(dz[i][1], ha, a2.y);
+                    a2.z = fmaf(dz[i][2], ha, a2.z);
+                    a2.w = fmaf(dz[i][3], ha, a2.w);
+                    a1.x = fmaf(dv[i], hc, a1.x);
+                    a1.y += dha;
+                    a1.z += dhc;
+                    gw1[0][ub] = __builtin_amdgcn_mfma_f32_16x16x4f32(xt[i], dha, gw1[0][ub], 0, 0, 0);
+                    gw1[1][ub] = __builtin_amdgcn_mfma_f32_16x16x4f32(xt[i], dhc, gw1[1][ub], 0, 0, 0);
+                }
+                reinterpret_cast<float4 *>(acc)[2 * ub] = a2;
+                reinterpret_cast<float4 *>(acc)[2 * ub + 1] = a1;
+            }
+        };
+        // hot path: fp32 decisions everywhere; rows whose logit lies within its fp32 error bound of
+        // 0 are flagged in `near` (bit i). Layer 2 of the lane group's rows, then the 16 rows' losses
+        // in lanes 0..15 (one lane per row, through the tile's LDS area), then the backward
+        {
+            float zr4[4][4], v4[4];
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+                layer2(i, zr4[i], v4[i]);
+            if (j == 0) {
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    *reinterpret_cast<float4 *>(bw + kTZr + 4 * (4 * g + i)) = make_float4(zr4[i][0], zr4[i][1], zr4[i][2], zr4[i][3]);
+                    bw[kTV + 4 * g + i] = __float_as_uint(v4[i]);
+                }
+            }
+        }
+        wave_lds_sync();
+        if (lane < 16) {
+            const float4 z4 = *reinterpret_cast<const float4 *>(bw + kTZr + 4 * lane);
+            const float zr[4] = {z4.x, z4.y, z4.z, z4.w};
+            float dz[4], dv, la, lc;
+            loss_from(lane, zr, __uint_as_float(bw[kTV + lane]), dz, dv, la, lc);
+            const float xml = __uint_as_float(bw[kTXm + lane]);
+            bool nr = false;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                nr |= fabsf(zr[k]) < zedge[k] + zcarry[k] * (hb + hw * xml);
+                dz[k] = zr[k] > 0.0f ? dz[k] : 0.0f;
+                gb2[k] += dz[k];
+            }
+            gbc2 += dv;
+            loss_a += la;
+            loss_c += lc;
+            *reinterpret_cast<float4 *>(bw + kTDz + 4 * lane) = make_float4(dz[0], dz[1], dz[2], dz[3]);
+            bw[kTDv + lane] = __float_as_uint(dv);
+            bw[kTNr + lane] = nr ? 1u : 0u;
+        }
+        wave_lds_sync();
+        uint32_t near = 0;
+        {
+            float dz[4][4], dv[4];
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const float4 d4 = *reinterpret_cast<const float4 *>(bw + kTDz + 4 * (4 * g + i));
+                dz[i][0] = d4.x, dz[i][1] = d4.y, dz[i][2] = d4.z, dz[i][3] = d4.w;
+                dv[i] = __uint_as_float(bw[kTDv + 4 * g + i]);
+                near |= bw[kTNr + 4 * g + i] << i;
+            }
+            rows_backward(dz, dv, 0xFu, false, 0u, 0.0f);
+        }
+        // ---------------- exact decisions (rare: the whole wave enters, lanes pick their own rows):
+        // for a flagged row, the exact logits' ReLU and hidden masks, and the row's backward run again
+        // on the differences (exact minus what the hot path accumulated)
+        if (__builtin_amdgcn_ballot_w64(edge_any || near != 0)) {
+            // opaque copies of the tile's pre-activations: the fix-up recomputes the rows' losses
+            // from them instead of keeping the hot path's values alive across the loop
+#pragma unroll
+            for (int net = 0; net < 2; net++)
+#pragma unroll
+                for (int ub = 0; ub < 4; ub++)
+                    asm volatile("" : "+v"(pre[net][ub]));
+            uint32_t mask = 0, edge = 0;   // fp32 decisions and flags, bit 16 net + 4 ub + i
+#pragma unroll
+            for (int net = 0; net < 2; net++)
+#pragma unroll
+                for (int ub = 0; ub < 4; ub++)
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {
+                        const float d = fabsf(pre[net][ub][i] - 3.0f);
+                        const uint32_t bit = 1u << (16 * net + 4 * ub + i);
+                        mask |= d < 3.0f ? bit : 0u;
+                        edge |= fabsf(d - 3.0f) < bound[net][i] ? bit : 0u;
+                    }
+            uint32_t mx = mask;   // exact hidden masks
+            for (uint32_t m = edge; m; m &= m - 1) {
+                const int bit = __builtin_ctz(m), net = bit >> 4, ub = (bit >> 2) & 3, i = bit & 3;
+                const double ad = preact64<MODE>(w, net ? kC1W : kA1W, net ? kC1B : kA1B, 16 * ub + j,
+                                                 cells + 16 * (4 * g + i));
+                mx = (ad > 0.0 && ad < 6.0) ? (mx | (1u << bit)) : (mx & ~(1u << bit));
+            }
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                if (!__builtin_amdgcn_ballot_w64((((edge >> i) & 0x1111u) | ((edge >> (16 + i)) & 0x1111u) | ((near >> i) & 1u)) != 0))
+                    continue;
+                float zr[4], v, dz[4], dv, la, lc;
+                layer2(i, zr, v);
+                loss_from(4 * g + i, zr, v, dz, dv, la, lc);
+                float pos[4];   // exact logits' ReLU decisions (1 / 0)
+#pragma unroll
+                for (int k = 0; k < 4; k++)
+                    pos[k] = zr[k] > 0.0f ? 1.0f : 0.0f;
+                if ((near >> i) & 1u) {   // the group's lanes together (DPP sums within the group)
+                    const uint8_t *rc = cells + 16 * (4 * g + i);
+                    double pk[4] = {0.0, 0.0, 0.0, 0.0};
+                    for (int ub = 0; ub < 4; ub++) {
+                        const double ad = preact64<MODE>(w, kA1W, kA1B, 16 * ub + j, rc);
+                        const double h = ad < 0.0 ? 0.0 : (ad > 6.0 ? 6.0 : ad);
+#pragma unroll
+                        for (int k = 0; k < 4; k++)
+                            pk[k] = __builtin_fma((double)w1_lds[lane][40 + 4 * ub + k], h, pk[k]);
+                    }
+#pragma unroll
+                    for (int k = 0; k < 4; k++)
+                        pos[k] = (double)b2[k] + row_sum16_d(pk[k]) > 0.0 ? 1.0f : 0.0f;
+                }
+                // the hot path's terms, with its decisions, then the exact ones: backward(exact) -
+                // backward(hot) is linear in dz and dv, so run the difference on each mask set
+                float dz32[4], dzx[4];
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    dz32[k] = zr[k] > 0.0f ? dz[k] : 0.0f;
+                    dzx[k] = pos[k] != 0.0f ? dz[k] : 0.0f;
+                }
+                float ndz[4][4] = {}, pdz[4][4] = {}, ndv[4] = {}, pdv[4] = {};
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    ndz[i][k] = -dz32[k];
+                    pdz[i][k] = dzx[k];
+                }
+                ndv[i] = -dv;
+                pdv[i] = dv;
+                rows_backward(ndz, ndv, 1u << i, true, mask, once);
+                rows_backward(pdz, pdv, 1u << i, true, mx, once);
+            }
+        }
+    }
+    // ---------------- this wave's record (FlatParams order)
+    float *rec = partials + ((int64_t)blockIdx.x * kTrainWaves + wave) * kRec;
+#pragma unroll
+    for (int ub = 0; ub < 4; ub++) {
+        const int u = 16 * ub + j;
+        *reinterpret_cast<float4 *>(rec + kA1W + 16 * u + 4 * g) = make_float4(gw1[0][ub][0], gw1[0][ub][1], gw1[0][ub][2], gw1[0][ub][3]);
+        *reinterpret_cast<float4 *>(rec + kC1W + 16 * u + 4 * g) = make_float4(gw1[1][ub][0], gw1[1][ub][1], gw1[1][ub][2], gw1[1][ub][3]);
+    }
+    // per-lane partials over the four lane groups (fixed order: (g0 + g1) + (g2 + g3) in every lane)
+    auto groups = [](float x) {
+        x += __shfl_xor(x, 16);
+        return x + __shfl_xor(x, 32);
+    };
+#pragma unroll
+    for (int ub = 0; ub < 4; ub++) {
+        const int u = 16 * ub + j;
+        const float4 a2 = reinterpret_cast<const float4 *>(acc)[2 * ub], a1 = reinterpret_cast<const float4 *>(acc)[2 * ub + 1];
+        const float a1b = groups(a1.y), c1b = groups(a1.z), c2w = groups(a1.x);
+        const float a2w[4] = {groups(a2.x), groups(a2.y), groups(a2.z), groups(a2.w)};
+        if (g == 0) {
+            rec[kA1B + u] = a1b;
+            rec[kC1B + u] = c1b;
+            rec[kC2W + u] = c2w;
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                rec[kA2W + 64 * k + u] = a2w[k];
+        }
+    }
+    const float s0 = wave_sum(gb2[0]), s1s = wave_sum(gb2[1]), s2 = wave_sum(gb2[2]), s3 = wave_sum(gb2[3]);
+    const float sc = wave_sum(gbc2), la = wave_sum(loss_a), lc = wave_sum(loss_c);
+    if (lane == 0) {
+        *reinterpret_cast<float4 *>(rec + kA2B) = make_float4(s0, s1s, s2, s3);
+        rec[kC2B] = sc;
+        rec[kRecLossA] = la;
+        rec[kRecLossC] = lc;
+        rec[kRec - 1] = 0.0f;
+    }
+}
+
+// fixed-order sum of `n_rec` records of kRec floats into out[kRec]: pass 1 sums groups of kRedGroup
+// records (one thread per (group, float4)), pass 2 the group sums
+constexpr int kRedGroup = 64;
+
+__global__ __launch_bounds__(256) void k_mlp_reduce1(const float4 *__restrict__ rec, int n_rec, float4 *__restrict__ groups)
+{
+    constexpr int q = kRec / 4;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int n_grp = (n_rec + kRedGroup - 1) / kRedGroup;
+    if (i >= q * n_grp)
+        return;
+    const int g = i / q, e = i % q;
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int r = g * kRedGroup; r < n_rec && r < (g + 1) * kRedGroup; r++) {
+        const float4 v = rec[(int64_t)r * q + e];
+        s.x += v.x, s.y += v.y, s.z += v.z, s.w += v.w;
+    }
+    groups[(int64_t)g * q + e] = s;
+}
+
+__global__ __launch_bounds__(256) void k_mlp_reduce2(const float4 *__restrict__ groups, int n_grp, float4 *__restrict__ out)
+{
+    constexpr int q = kRec / 4;
+    const int e = blockIdx.x * 256 + threadIdx.x;
+    if (e >= q)
+        return;
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int g = 0; g < n_grp; g++) {
+        const float4 v = groups[(int64_t)g * q + e];
+        s.x += v.x, s.y += v.y, s.z += v.z, s.w += v.w;
+    }
+    out[e] = s;
+}
+
+constexpr int kTrainGroups = 512;    // persistent grid: two workgroups of 4 waves per CU (two waves per SIMD) on 256 CUs
+
+int fail(int code, const std::string &msg)
+{
+    r48::set_last_error(msg);
+    return code;
+}
+
+int launched(const char *what)
+{
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess)
+        return fail(R48_EHIP, std::string(what) + ": " + hipGetErrorString(e));
+    return R48_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+/* workspace floats of r48_mlp_train_grad: the per-wave records + the first reduction pass's groups */
+int64_t r48_mlp_train_workspace_floats(void)
+{
+    const int64_t recs = (int64_t)kTrainGroups * kTrainWaves;
+    return (recs + (recs + kRedGroup - 1) / kRedGroup) * kRec;
+}
+
+int r48_mlp_train_grad(const int8_t *boards, int64_t rows, int64_t n_boards, const int8_t *actions,
+                       const float *targets, const float *wn, const float *cm, const float *counts, float beta,
+                       int32_t mode, const float *w, float *workspace, float *grad, void *stream)
+{
+    if (!boards || !actions || !targets || !wn || !w || !workspace || !grad || rows < 1 || n_boards < 1 ||
+        (mode != R48_FEAT_VALUES && mode != R48_FEAT_EXPONENTS) || (cm && !counts))
+        return fail(R48_EINVAL, "r48_mlp_train_grad: NULL argument, rows/n_boards < 1, bad mode, or cm without counts");
+    if ((reinterpret_cast<uintptr_t>(boards) | reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(counts) |
+         reinterpret_cast<uintptr_t>(workspace) | reinterpret_cast<uintptr_t>(grad)) & 15u)
+        return fail(R48_EINVAL, "r48_mlp_train_grad: boards, w, counts, workspace and grad must be 16-byte aligned");
+    const int n_rec = kTrainGroups * kTrainWaves, n_grp = (n_rec + kRedGroup - 1) / kRedGroup;
+    hipStream_t s = (hipStream_t)stream;
+    auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(kTrainGroups), dim3(64 * kTrainWaves), 0, s, boards, rows, n_boards, actions,
+                           targets, wn, cm, counts, beta, w, workspace);
+    };
+    if (mode == R48_FEAT_VALUES)
+        cm ? go(k_mlp_train<R48_FEAT_VALUES, true>) : go(k_mlp_train<R48_FEAT_VALUES, false>);
+    else
+        cm ? go(k_mlp_train<R48_FEAT_EXPONENTS, true>) : go(k_mlp_train<R48_FEAT_EXPONENTS, false>);
+    float4 *groups = reinterpret_cast<float4 *>(workspace + (int64_t)n_rec * kRec);
+    constexpr int q = kRec / 4;
+    hipLaunchKernelGGL(k_mlp_reduce1, dim3((q * n_grp + 255) / 256), dim3(256), 0, s, (const float4 *)workspace, n_rec,
+                       groups);
+    hipLaunchKernelGGL(k_mlp_reduce2, dim3((q + 255) / 256), dim3(256), 0, s, (const float4 *)groups, n_grp,
+                       (float4 *)grad);
+    return launched("k_mlp_train");
+}
+
+}  // extern "C"
