@@ -85,11 +85,29 @@ __device__ __forceinline__ float wave_sum(float v)
 
 // all-reduce over the 16 lanes of a DPP row by rotations 8, 4, 2, 1: at every level a lane adds
 // the same two operands as its partner (IEEE addition commutes), so all 16 lanes get the bitwise
-// same sum
+// same sum. (A row rotation reads no lane outside the row, so bound_ctrl is moot; set, it lets the
+// compiler fold each move into its add as a DPP operand.)
 template <int N>
 __device__ __forceinline__ float row_ror(float v)
 {
     return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x120 + N, 0xF, 0xF, true));
+}
+// max / sum over the 4 lanes of a DPP quad (quad_perm [1,0,3,2] then [2,3,0,1]): all four lanes get
+// the bitwise same result ((a + b) + (c + d) in every lane, by commutativity)
+template <int CTRL>
+__device__ __forceinline__ float quad_perm(float v)
+{
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+__device__ __forceinline__ float quad_sum(float v)
+{
+    v += quad_perm<0xB1>(v);
+    return v + quad_perm<0x4E>(v);
+}
+__device__ __forceinline__ float quad_max(float v)
+{
+    v = fmaxf(v, quad_perm<0xB1>(v));
+    return fmaxf(v, quad_perm<0x4E>(v));
 }
 __device__ __forceinline__ float row_sum16(float v)
 {
@@ -137,9 +155,9 @@ __device__ __forceinline__ double preact64(const float *w, int base, int bbase, 
 
 // per-wave LDS area of a 16-row tile (32-bit words): boards [16][4] | max input | row weight |
 // target | action | cm | counts [16][4] | pre-ReLU logits [16][4] | value | dz through the logits'
-// ReLU [16][4] | dv | near flag
+// ReLU [16][4] | dv | dz before it [16][4]
 constexpr int kTB = 0, kTXm = 64, kTWt = 80, kTTg = 96, kTAc = 112, kTCm = 128, kTCn = 144, kTZr = 208, kTV = 272,
-              kTDz = 288, kTDv = 352, kTNr = 368, kTileWords = 384;
+              kTDz = 288, kTDv = 352, kTDu = 368, kTileWords = 432;
 
 // the inputs of one training row, loaded a tile ahead by lane j of every lane group
 struct RowIn {
@@ -150,7 +168,7 @@ struct RowIn {
 };
 
 template <bool REF>
-__device__ __forceinline__ RowIn fetch_row(int64_t r, int64_t rows, int64_t n_boards, const int8_t *boards,
+__device__ __forceinline__ RowIn fetch_row(int64_t r, int64_t rows, int64_t bidx, const int8_t *boards,
                                            const int8_t *actions, const float *targets, const float *wn,
                                            const float *cm, const float *counts)
 {
@@ -165,7 +183,6 @@ __device__ __forceinline__ RowIn fetch_row(int64_t r, int64_t rows, int64_t n_bo
     x.cnt = make_float4(0.f, 0.f, 0.f, 0.f);
     if (REF) {
         x.c = live ? cm[rr] : 0.0f;
-        const int64_t bidx = rows <= 0xFFFFFFFFll ? (int64_t)((uint32_t)rr % (uint32_t)n_boards) : rr % n_boards;
         x.cnt = *reinterpret_cast<const float4 *>(counts + 4 * bidx);
     }
     return x;
@@ -181,7 +198,7 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
     // layer-1 B operands and biases of every lane (read back each tile: 40 registers the rest of
     // the tile needs)
     __shared__ __attribute__((aligned(16))) uint32_t tiles_lds[kTrainWaves][kTileWords];
-    __shared__ __attribute__((aligned(16))) float w1_lds[64][60];
+    __shared__ __attribute__((aligned(16))) float w1_lds[64][92];   // 92: conflict-free b128 reads
     // per lane: the db1 / dW2 / dwc2 partials, per unit block [dW2[k] x 4 | dwc2 | db1 | dbc1 | pad]
     // (read-modified-written by the backward one unit block at a time: registers for two waves per
     // SIMD)
@@ -193,7 +210,8 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
     constexpr int kW1[2] = {kA1W, kC1W}, kB1[2] = {kA1B, kC1B};
 
     // constants of lane (j, g)'s units 16ub + j: layer-1 B operands (inputs 4s + g) and biases in
-    // LDS (w1_lds[lane][8 (net, ub) + s], [32 + (net, ub)]), W2 / wc2 entries in registers
+    // LDS (w1_lds[lane][4 (4 net + ub) + s], [32 + 4 net + ub], W2 [40 + 4 ub + k], wc2 [56 + ub], the
+    // bias broadcast [60 + 4 (4 net + ub) + q])
     if (threadIdx.x < 64) {
 #pragma unroll
         for (int net = 0; net < 2; net++)
@@ -204,6 +222,9 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
                 for (int s4 = 0; s4 < 4; s4++)
                     w1_lds[lane][4 * (4 * net + ub) + s4] = w1_at(w, kW1[net], u, 4 * s4 + g);
                 w1_lds[lane][32 + 4 * net + ub] = w[kB1[net] + u];
+#pragma unroll
+                for (int q = 0; q < 4; q++)   // the bias again, broadcast: layer 1's C operand as one read
+                    w1_lds[lane][60 + 4 * (4 * net + ub) + q] = w[kB1[net] + u];
             }
 #pragma unroll
         for (int ub = 0; ub < 4; ub++) {
@@ -268,19 +289,33 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
 #pragma unroll
     for (int ub = 0; ub < 4; ub++)
         gw1[0][ub] = gw1[1][ub] = f32x4{0.f, 0.f, 0.f, 0.f};
-    float gb2[4] = {0.f, 0.f, 0.f, 0.f}, gbc2 = 0.f, loss_a = 0.f, loss_c = 0.f;
+    // per-lane sums of the loss phase (lane 4r + k works on logit k = lk): db2[k], and the rows'
+    // dbc2 and losses; the fix-up's db2 changes go to the LDS partials (slot a1.w of unit block k)
+    float gb2l = 0.f, gbc2 = 0.f, loss_a = 0.f, loss_c = 0.f;
+    const int lk = lane & 3;
+    const float zedge_l = lk == 0 ? zedge[0] : lk == 1 ? zedge[1] : lk == 2 ? zedge[2] : zedge[3];
+    const float zcarry_l = lk == 0 ? zcarry[0] : lk == 1 ? zcarry[1] : lk == 2 ? zcarry[2] : zcarry[3];
     const float once = j == 0 ? 1.0f : 0.0f;   // the fix-up's per-row sums: one lane of the row group
 
     const int64_t n_tiles = (rows + 15) / 16;
     const int64_t stride = (int64_t)gridDim.x * kTrainWaves;
     int64_t tile = (int64_t)blockIdx.x * kTrainWaves + wave;
     // one wave per SIMD hides no load latency: row r0 + j's inputs arrive a tile ahead
-    RowIn next = fetch_row<REF>(std::min<int64_t>(tile, n_tiles - 1) * 16 + j, rows, n_boards, boards, actions, targets,
+    // the counts row of training row r is r mod n_boards (rows are step-major, t * n_boards + board):
+    // kept incrementally as the lane's row advances by 16 * stride (a prefetch past the end, clamped
+    // to the last tile, reads a valid counts row it never uses)
+    int64_t bnext = REF ? (std::min<int64_t>(tile, n_tiles - 1) * 16 + j) % n_boards : 0;
+    const int64_t bstep = REF ? (stride * 16) % n_boards : 0;
+    RowIn next = fetch_row<REF>(std::min<int64_t>(tile, n_tiles - 1) * 16 + j, rows, bnext, boards, actions, targets,
                                 wn, cm, counts);
     for (; tile < n_tiles; tile += stride) {
         // ---------------- inputs: row r0 + j in the four lanes j + 16g
         const RowIn in = next;
-        next = fetch_row<REF>(std::min<int64_t>(tile + stride, n_tiles - 1) * 16 + j, rows, n_boards, boards, actions,
+        if (REF) {
+            bnext += bstep;
+            bnext -= bnext >= n_boards ? n_boards : 0;
+        }
+        next = fetch_row<REF>(std::min<int64_t>(tile + stride, n_tiles - 1) * 16 + j, rows, bnext, boards, actions,
                               targets, wn, cm, counts);
         const uint4 bv = in.b;
         const uint32_t bwd[4] = {bv.x, bv.y, bv.z, bv.w};
@@ -316,14 +351,13 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
 
         // ---------------- layer 1 on the MFMA: register i = row 4g + i, lane j = unit 16ub + j
         f32x4 pre[2][4];
-        const float4 bl0 = wl[8], bl1 = wl[9];
-        const float b1[2][4] = {{bl0.x, bl0.y, bl0.z, bl0.w}, {bl1.x, bl1.y, bl1.z, bl1.w}};
 #pragma unroll
         for (int net = 0; net < 2; net++)
 #pragma unroll
             for (int ub = 0; ub < 4; ub++) {
                 const float4 wb = wl[4 * net + ub];
-                f32x4 acc = f32x4{b1[net][ub], b1[net][ub], b1[net][ub], b1[net][ub]};
+                const float4 b4 = wl[15 + 4 * net + ub];
+                f32x4 acc = f32x4{b4.x, b4.y, b4.z, b4.w};
                 acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[0], wb.x, acc, 0, 0, 0);
                 acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[1], wb.y, acc, 0, 0, 0);
                 acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[2], wb.z, acc, 0, 0, 0);
@@ -340,14 +374,18 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
 #pragma unroll
             for (int i = 0; i < 4; i++)
                 bound[net][i] = fmaf(s1[net], xm[i], e1[net]);
+        // (per row and net: the nearest of the lane's 4 units against the row's bound)
         bool edge_any = false;
 #pragma unroll
         for (int net = 0; net < 2; net++)
 #pragma unroll
-            for (int ub = 0; ub < 4; ub++)
+            for (int i = 0; i < 4; i++) {
+                float dn[4];
 #pragma unroll
-                for (int i = 0; i < 4; i++)
-                    edge_any |= fabsf(fabsf(pre[net][ub][i] - 3.0f) - 3.0f) < bound[net][i];
+                for (int ub = 0; ub < 4; ub++)
+                    dn[ub] = fabsf(fabsf(pre[net][ub][i] - 3.0f) - 3.0f);
+                edge_any |= fminf(fminf(dn[0], dn[1]), fminf(dn[2], dn[3])) < bound[net][i];
+            }
         // ---------------- per row i of the lane group (rows 4g + i): layer 2 (the group's 16 lanes
         // add up), the loss (every lane of the group computes it; counted once) -- the same code on
         // the hot path and in the exact-decision fix-up below, so the same values
@@ -370,76 +408,21 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
                 zr[k] = b2[k] + row_sum16(pk[k]);   // pre-ReLU
             v = bc2 + row_sum16(pv);
         };
-        // the loss of tile row ri from its pre-ReLU logits and value
-        auto loss_from = [&](int ri, const float (&zr)[4], float v, float (&dz)[4], float &dv, float &la, float &lc) {
-            const float wt = __uint_as_float(bw[kTWt + ri]);
-            const float tgt = __uint_as_float(bw[kTTg + ri]);
-            const int a = (int)bw[kTAc + ri];
-            float z[4], p[4], gr[4];
-#pragma unroll
-            for (int k = 0; k < 4; k++)
-                z[k] = fmaxf(zr[k], 0.0f);                            // the logits' ReLU (a3c.py:153)
-            const float mz = fmaxf(fmaxf(z[0], z[1]), fmaxf(z[2], z[3]));
-            float se = 0.f;
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                p[k] = __expf(z[k] - mz);
-                se += p[k];
-            }
-            const float inv = __builtin_amdgcn_rcpf(se), lse = mz + kLn2 * __builtin_amdgcn_logf(se);
-            float H = 0.f, gbar = 0.f;
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                p[k] *= inv;
-                const float lq = kLn2 * __builtin_amdgcn_logf(p[k] + kEntropyEps);
-                H -= p[k] * lq;
-                gr[k] = -(lq + p[k] * __builtin_amdgcn_rcpf(p[k] + kEntropyEps));   // dH/dp_k
-                gbar += p[k] * gr[k];
-            }
-            const float td = tgt - v;
-            if (REF) {   // reference: -beta wn H - cm sum_k c_k log p_k  (losses.py, a3c.py:110-116)
-                const float c = __uint_as_float(bw[kTCm + ri]);
-                const float4 cnt = *reinterpret_cast<const float4 *>(bw + kTCn + 4 * ri);
-                const float ck[4] = {cnt.x, cnt.y, cnt.z, cnt.w}, C = cnt.x + cnt.y + cnt.z + cnt.w;
-                float sa = 0.f;
-#pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    dz[k] = -beta * wt * p[k] * (gr[k] - gbar) - c * (ck[k] - p[k] * C);
-                    sa += ck[k] * (z[k] - lse);
-                }
-                la = -beta * wt * H - c * sa;
-            } else {     // textbook: -wn (beta H + td log p[a]), td constant for the actor
-#pragma unroll
-                for (int k = 0; k < 4; k++)
-                    dz[k] = -wt * (beta * p[k] * (gr[k] - gbar) + td * ((k == a ? 1.0f : 0.0f) - p[k]));
-                la = -wt * (beta * H + td * (z[a] - lse));
-            }
-            dv = -2.0f * wt * td;                                      // critic = wn td^2
-            lc = wt * td * td;
-        };
         // the backward of the lane group's 4 rows with output gradients dz (through the logits' ReLU)
         // and dv, and hidden masks (the fp32 decisions, or the given bits in the fix-up): the per-lane
         // partials (in LDS, one unit block at a time) and the rows' k-steps of dW1 on the MFMA
-        // (register i = row, lane = unit); `sel` picks the rows (bit i), the fix-up runs it on
-        // differences
+        // (register i = row, lane = unit); `sel` picks the rows (bit i). The fix-up runs it on
+        // differences (`fix`): dv does not depend on any decision, so only its mask terms move there,
+        // and the db2 change goes to the unit block's spare slot (slot k = ub, once per row group)
         auto rows_backward = [&](const float (&dz)[4][4], const float (&dv)[4], uint32_t sel, bool bits, uint32_t mk,
-                                 float scale_once) {
-#pragma unroll
-            for (int i = 0; i < 4; i++) {
-                if (!((sel >> i) & 1u))
-                    continue;
-#pragma unroll
-                for (int k = 0; k < 4; k++)
-                    gb2[k] += scale_once * dz[i][k];
-                gbc2 += scale_once * dv[i];
-            }
+                                 bool fix) {
             const float4 c2 = wl[14];
             const float wc2[4] = {c2.x, c2.y, c2.z, c2.w};
 #pragma unroll
             for (int ub = 0; ub < 4; ub++) {
                 const float4 w4 = wl[10 + ub];
                 float4 a2 = reinterpret_cast<float4 *>(acc)[2 * ub];        // dW2[k][16ub + j] partials
-                float4 a1 = reinterpret_cast<float4 *>(acc)[2 * ub + 1];    // dwc2 | db1 | dbc1 | -
+                float4 a1 = reinterpret_cast<float4 *>(acc)[2 * ub + 1];    // dwc2 | db1 | dbc1 | db2 fix-ups
 #pragma unroll
                 for (int i = 0; i < 4; i++) {
                     if (!((sel >> i) & 1u))
@@ -456,7 +439,11 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
                     a2.y = fmaf(dz[i][1], ha, a2.y);
                     a2.z = fmaf(dz[i][2], ha, a2.z);
                     a2.w = fmaf(dz[i][3], ha, a2.w);
-                    a1.x = fmaf(dv[i], hc, a1.x);
+                    if (fix) {
+                        a1.w = fmaf(once, dz[i][ub], a1.w);
+                    } else {
+                        a1.x = fmaf(dv[i], hc, a1.x);
+                    }
                     a1.y += dha;
                     a1.z += dhc;
                     gw1[0][ub] = __builtin_amdgcn_mfma_f32_16x16x4f32(xt[i], dha, gw1[0][ub], 0, 0, 0);
@@ -466,9 +453,10 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
                 reinterpret_cast<float4 *>(acc)[2 * ub + 1] = a1;
             }
         };
-        // hot path: fp32 decisions everywhere; rows whose logit lies within its fp32 error bound of
-        // 0 are flagged in `near` (bit i). Layer 2 of the lane group's rows, then the 16 rows' losses
-        // in lanes 0..15 (one lane per row, through the tile's LDS area), then the backward
+        // hot path: fp32 decisions everywhere. Layer 2 of the lane group's rows; then the loss with
+        // lane 4r + k on logit k of tile row r (the row's DPP quad does the sums over k), rows whose
+        // logit lies within its fp32 error bound of 0 flagged in `near_rows` (bit 4r + k); then the
+        // backward
         {
             float zr4[4][4], v4[4];
 #pragma unroll
@@ -483,28 +471,57 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
             }
         }
         wave_lds_sync();
-        if (lane < 16) {
-            const float4 z4 = *reinterpret_cast<const float4 *>(bw + kTZr + 4 * lane);
-            const float zr[4] = {z4.x, z4.y, z4.z, z4.w};
-            float dz[4], dv, la, lc;
-            loss_from(lane, zr, __uint_as_float(bw[kTV + lane]), dz, dv, la, lc);
-            const float xml = __uint_as_float(bw[kTXm + lane]);
-            bool nr = false;
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                nr |= fabsf(zr[k]) < zedge[k] + zcarry[k] * (hb + hw * xml);
-                dz[k] = zr[k] > 0.0f ? dz[k] : 0.0f;
-                gb2[k] += dz[k];
+        uint64_t near_rows;
+        {
+            const int r = lane >> 2;
+            const float zr = __uint_as_float(bw[kTZr + lane]);
+            const float v = __uint_as_float(bw[kTV + r]);
+            const float wt = __uint_as_float(bw[kTWt + r]);
+            const float tgt = __uint_as_float(bw[kTTg + r]);
+            const float z = fmaxf(zr, 0.0f);                               // the logits' ReLU (a3c.py:153)
+            const float mz = quad_max(z);
+            float p = __expf(z - mz);
+            const float se = quad_sum(p);
+            const float inv = __builtin_amdgcn_rcpf(se), lse = mz + kLn2 * __builtin_amdgcn_logf(se);
+            p *= inv;
+            const float lq = kLn2 * __builtin_amdgcn_logf(p + kEntropyEps);
+            const float hk = -p * lq;                                       // logit k's term of the entropy
+            const float gr = -(lq + p * __builtin_amdgcn_rcpf(p + kEntropyEps));   // dH/dp_k
+            const float gbar = quad_sum(p * gr);
+            const float td = tgt - v;
+            float dz, la;
+            if (REF) {   // reference: -beta wn H - cm sum_k c_k log p_k  (losses.py, a3c.py:110-116)
+                const float c = __uint_as_float(bw[kTCm + r]);
+                const float ck = __uint_as_float(bw[kTCn + lane]);
+                const float C = quad_sum(ck);
+                dz = -beta * wt * p * (gr - gbar) - c * (ck - p * C);
+                la = -beta * wt * hk - c * (ck * (z - lse));
+            } else {     // textbook: -wn (beta H + td log p[a]), td constant for the actor
+                const bool act = lk == (int)bw[kTAc + r];
+                dz = -wt * (beta * p * (gr - gbar) + td * ((act ? 1.0f : 0.0f) - p));
+                la = -wt * (beta * hk + (act ? td * (z - lse) : 0.0f));
             }
-            gbc2 += dv;
+            const float dv = -2.0f * wt * td;                               // critic = wn td^2
+            const float xml = __uint_as_float(bw[kTXm + r]);
+            near_rows = __builtin_amdgcn_ballot_w64(fabsf(zr) < zedge_l + zcarry_l * (hb + hw * xml));
+            const float dzm = zr > 0.0f ? dz : 0.0f;
+            gb2l += dzm;
             loss_a += la;
-            loss_c += lc;
-            *reinterpret_cast<float4 *>(bw + kTDz + 4 * lane) = make_float4(dz[0], dz[1], dz[2], dz[3]);
-            bw[kTDv + lane] = __float_as_uint(dv);
-            bw[kTNr + lane] = nr ? 1u : 0u;
+            if (lk == 0) {   // the row's terms once
+                gbc2 += dv;
+                loss_c += wt * td * td;
+                bw[kTDv + r] = __float_as_uint(dv);
+            }
+            bw[kTDz + lane] = __float_as_uint(dzm);
+            bw[kTDu + lane] = __float_as_uint(dz);
         }
         wave_lds_sync();
+        // this lane group's rows 4g + i near a logit boundary (bit i)
+        const uint32_t near_q = (uint32_t)(near_rows >> (16 * g)) & 0xFFFFu;
         uint32_t near = 0;
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+            near |= ((near_q >> (4 * i)) & 0xFu) != 0 ? 1u << i : 0u;
         {
             float dz[4][4], dv[4];
 #pragma unroll
@@ -512,16 +529,15 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
                 const float4 d4 = *reinterpret_cast<const float4 *>(bw + kTDz + 4 * (4 * g + i));
                 dz[i][0] = d4.x, dz[i][1] = d4.y, dz[i][2] = d4.z, dz[i][3] = d4.w;
                 dv[i] = __uint_as_float(bw[kTDv + 4 * g + i]);
-                near |= bw[kTNr + 4 * g + i] << i;
             }
-            rows_backward(dz, dv, 0xFu, false, 0u, 0.0f);
+            rows_backward(dz, dv, 0xFu, false, 0u, false);
         }
         // ---------------- exact decisions (rare: the whole wave enters, lanes pick their own rows):
         // for a flagged row, the exact logits' ReLU and hidden masks, and the row's backward run again
-        // on the differences (exact minus what the hot path accumulated)
+        // on the differences (exact minus what the hot path accumulated, from the hot path's dz in LDS)
         if (__builtin_amdgcn_ballot_w64(edge_any || near != 0)) {
-            // opaque copies of the tile's pre-activations: the fix-up recomputes the rows' losses
-            // from them instead of keeping the hot path's values alive across the loop
+            // opaque copies of the tile's pre-activations: the fix-up reads them from registers the
+            // hot path is done with
 #pragma unroll
             for (int net = 0; net < 2; net++)
 #pragma unroll
@@ -550,15 +566,19 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
             for (int i = 0; i < 4; i++) {
                 if (!__builtin_amdgcn_ballot_w64((((edge >> i) & 0x1111u) | ((edge >> (16 + i)) & 0x1111u) | ((near >> i) & 1u)) != 0))
                     continue;
-                float zr[4], v, dz[4], dv, la, lc;
-                layer2(i, zr, v);
-                loss_from(4 * g + i, zr, v, dz, dv, la, lc);
+                const int ri = 4 * g + i;
+                const float4 z4 = *reinterpret_cast<const float4 *>(bw + kTZr + 4 * ri);
+                const float4 m4 = *reinterpret_cast<const float4 *>(bw + kTDz + 4 * ri);
+                const float4 u4 = *reinterpret_cast<const float4 *>(bw + kTDu + 4 * ri);
+                const float zr[4] = {z4.x, z4.y, z4.z, z4.w}, dzm[4] = {m4.x, m4.y, m4.z, m4.w},
+                            dzu[4] = {u4.x, u4.y, u4.z, u4.w};
+                const float dv = __uint_as_float(bw[kTDv + ri]);
                 float pos[4];   // exact logits' ReLU decisions (1 / 0)
 #pragma unroll
                 for (int k = 0; k < 4; k++)
                     pos[k] = zr[k] > 0.0f ? 1.0f : 0.0f;
                 if ((near >> i) & 1u) {   // the group's lanes together (DPP sums within the group)
-                    const uint8_t *rc = cells + 16 * (4 * g + i);
+                    const uint8_t *rc = cells + 16 * ri;
                     double pk[4] = {0.0, 0.0, 0.0, 0.0};
                     for (int ub = 0; ub < 4; ub++) {
                         const double ad = preact64<MODE>(w, kA1W, kA1B, 16 * ub + j, rc);
@@ -571,24 +591,19 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
                     for (int k = 0; k < 4; k++)
                         pos[k] = (double)b2[k] + row_sum16_d(pk[k]) > 0.0 ? 1.0f : 0.0f;
                 }
-                // the hot path's terms, with its decisions, then the exact ones: backward(exact) -
+                // the hot path's terms with its decisions, then the exact ones: backward(exact) -
                 // backward(hot) is linear in dz and dv, so run the difference on each mask set
-                float dz32[4], dzx[4];
+                float ndz[4][4] = {}, pdz[4][4] = {}, dv4[4] = {};
 #pragma unroll
                 for (int k = 0; k < 4; k++) {
-                    dz32[k] = zr[k] > 0.0f ? dz[k] : 0.0f;
-                    dzx[k] = pos[k] != 0.0f ? dz[k] : 0.0f;
+                    ndz[i][k] = -dzm[k];
+                    pdz[i][k] = pos[k] != 0.0f ? dzu[k] : 0.0f;
                 }
-                float ndz[4][4] = {}, pdz[4][4] = {}, ndv[4] = {}, pdv[4] = {};
-#pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    ndz[i][k] = -dz32[k];
-                    pdz[i][k] = dzx[k];
-                }
-                ndv[i] = -dv;
-                pdv[i] = dv;
-                rows_backward(ndz, ndv, 1u << i, true, mask, once);
-                rows_backward(pdz, pdv, 1u << i, true, mx, once);
+                dv4[i] = dv;
+                float ndv4[4] = {};
+                ndv4[i] = -dv;
+                rows_backward(ndz, ndv4, 1u << i, true, mask, true);
+                rows_backward(pdz, dv4, 1u << i, true, mx, true);
             }
         }
     }
@@ -620,7 +635,11 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
                 rec[kA2W + 64 * k + u] = a2w[k];
         }
     }
-    const float s0 = wave_sum(gb2[0]), s1s = wave_sum(gb2[1]), s2 = wave_sum(gb2[2]), s3 = wave_sum(gb2[3]);
+    float gk[4];   // db2[k]: the loss lanes of logit k + every lane's fix-up slot
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+        gk[k] = (lk == k ? gb2l : 0.0f) + reinterpret_cast<const float4 *>(acc)[2 * k + 1].w;
+    const float s0 = wave_sum(gk[0]), s1s = wave_sum(gk[1]), s2 = wave_sum(gk[2]), s3 = wave_sum(gk[3]);
     const float sc = wave_sum(gbc2), la = wave_sum(loss_a), lc = wave_sum(loss_c);
     if (lane == 0) {
         *reinterpret_cast<float4 *>(rec + kA2B) = make_float4(s0, s1s, s2, s3);
