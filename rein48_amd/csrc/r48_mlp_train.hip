@@ -83,10 +83,9 @@ __device__ __forceinline__ float wave_sum(float v)
     return v;
 }
 
-// all-reduce over the 16 lanes of a DPP row by rotations 8, 4, 2, 1: at every level a lane adds
-// the same two operands as its partner (IEEE addition commutes), so all 16 lanes get the bitwise
-// same sum. (A row rotation reads no lane outside the row, so bound_ctrl is moot; set, it lets the
-// compiler fold each move into its add as a DPP operand.)
+// DPP moves within a 16-lane row. (A row rotation or mirror and a quad permutation read no lane
+// outside the row, so bound_ctrl is moot; set, it lets the compiler fold each move into its add as a
+// DPP operand.)
 template <int N>
 __device__ __forceinline__ float row_ror(float v)
 {
@@ -109,14 +108,23 @@ __device__ __forceinline__ float quad_max(float v)
     v = fmaxf(v, quad_perm<0xB1>(v));
     return fmaxf(v, quad_perm<0x4E>(v));
 }
-__device__ __forceinline__ float row_sum16(float v)
+// four 16-lane sums at once, transposed: v0..v3 are a lane's terms of rows 0..3, and lane j ends with
+// the sum over the 16 lanes of its DPP row of row 2 bit3(j) + bit2(j). Lanes j, j ^ 8 split the rows
+// in halves (row_ror:8 is the exchange j ^ 8), lanes j, j ^ 7 (row_half_mirror) halve again, then
+// the quad adds the rest (^1, ^2): 6 selects + 5 DPP adds instead of 4 x 4 adds. The four lanes of a
+// row get the bitwise same sum.
+__device__ __forceinline__ float row_sum4x16(float v0, float v1, float v2, float v3, bool hi8, bool hi4)
 {
-    v += row_ror<8>(v);
-    v += row_ror<4>(v);
-    v += row_ror<2>(v);
-    v += row_ror<1>(v);
-    return v;
+    const float a0 = hi8 ? v2 : v0, a1 = hi8 ? v3 : v1, s0 = hi8 ? v0 : v2, s1 = hi8 ? v1 : v3;
+    const float r0 = a0 + row_ror<8>(s0), r1 = a1 + row_ror<8>(s1);
+    const float c = hi4 ? r1 : r0, s = hi4 ? r0 : r1;
+    float t = c + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(s), 0x141, 0xF, 0xF, true));
+    t += quad_perm<0xB1>(t);
+    return t + quad_perm<0x4E>(t);
 }
+// fp64 all-reduce over the 16 lanes of a DPP row by rotations 8, 4, 2, 1: at every level a lane adds
+// the same two operands as its partner (IEEE addition commutes), so all 16 lanes get the bitwise
+// same sum
 template <int N>
 __device__ __forceinline__ double row_ror_d(double v)
 {
@@ -293,6 +301,9 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
     // dbc2 and losses; the fix-up's db2 changes go to the LDS partials (slot a1.w of unit block k)
     float gb2l = 0.f, gbc2 = 0.f, loss_a = 0.f, loss_c = 0.f;
     const int lk = lane & 3;
+    // layer 2's reduction: lane j of a row group ends with row lrow = 2 bit3(j) + bit2(j)
+    const bool hi8 = (j & 8) != 0, hi4 = (j & 4) != 0;
+    const int lrow = (hi8 ? 2 : 0) + (hi4 ? 1 : 0);
     const float zedge_l = lk == 0 ? zedge[0] : lk == 1 ? zedge[1] : lk == 2 ? zedge[2] : zedge[3];
     const float zcarry_l = lk == 0 ? zcarry[0] : lk == 1 ? zcarry[1] : lk == 2 ? zcarry[2] : zcarry[3];
     const float once = j == 0 ? 1.0f : 0.0f;   // the fix-up's per-row sums: one lane of the row group
@@ -389,24 +400,31 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
         // ---------------- per row i of the lane group (rows 4g + i): layer 2 (the group's 16 lanes
         // add up), the loss (every lane of the group computes it; counted once) -- the same code on
         // the hot path and in the exact-decision fix-up below, so the same values
-        auto layer2 = [&](int i, float (&zr)[4], float &v) {
-            float pk[4] = {0.f, 0.f, 0.f, 0.f}, pv = 0.f;
+        // layer 2: each lane's partial sums over its 4 units for the group's 4 rows, then one
+        // transposing reduction over the 16 lanes per output (row_sum4x16): lane j ends with row
+        // 4g + lrow's logits (pre-ReLU) and value
+        auto layer2 = [&](float (&zr)[4], float &v) {
+            float pk[4][4], pv[4];   // [i][k]
             const float4 c2 = wl[14];   // wc2 of the lane's 4 units
             const float wc2[4] = {c2.x, c2.y, c2.z, c2.w};
 #pragma unroll
-            for (int ub = 0; ub < 4; ub++) {
-                const float4 w4 = wl[10 + ub];   // W2[k][16ub + j]
-                const float ha = __builtin_amdgcn_fmed3f(pre[0][ub][i], 0.0f, 6.0f);
-                pk[0] = fmaf(w4.x, ha, pk[0]);
-                pk[1] = fmaf(w4.y, ha, pk[1]);
-                pk[2] = fmaf(w4.z, ha, pk[2]);
-                pk[3] = fmaf(w4.w, ha, pk[3]);
-                pv = fmaf(wc2[ub], __builtin_amdgcn_fmed3f(pre[1][ub][i], 0.0f, 6.0f), pv);
+            for (int i = 0; i < 4; i++) {
+                pk[i][0] = pk[i][1] = pk[i][2] = pk[i][3] = pv[i] = 0.0f;
+#pragma unroll
+                for (int ub = 0; ub < 4; ub++) {
+                    const float4 w4 = wl[10 + ub];   // W2[k][16ub + j]
+                    const float ha = __builtin_amdgcn_fmed3f(pre[0][ub][i], 0.0f, 6.0f);
+                    pk[i][0] = fmaf(w4.x, ha, pk[i][0]);
+                    pk[i][1] = fmaf(w4.y, ha, pk[i][1]);
+                    pk[i][2] = fmaf(w4.z, ha, pk[i][2]);
+                    pk[i][3] = fmaf(w4.w, ha, pk[i][3]);
+                    pv[i] = fmaf(wc2[ub], __builtin_amdgcn_fmed3f(pre[1][ub][i], 0.0f, 6.0f), pv[i]);
+                }
             }
 #pragma unroll
             for (int k = 0; k < 4; k++)
-                zr[k] = b2[k] + row_sum16(pk[k]);   // pre-ReLU
-            v = bc2 + row_sum16(pv);
+                zr[k] = b2[k] + row_sum4x16(pk[0][k], pk[1][k], pk[2][k], pk[3][k], hi8, hi4);   // pre-ReLU
+            v = bc2 + row_sum4x16(pv[0], pv[1], pv[2], pv[3], hi8, hi4);
         };
         // the backward of the lane group's 4 rows with output gradients dz (through the logits' ReLU)
         // and dv, and hidden masks (the fp32 decisions, or the given bits in the fix-up): the per-lane
@@ -458,16 +476,11 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
         // logit lies within its fp32 error bound of 0 flagged in `near_rows` (bit 4r + k); then the
         // backward
         {
-            float zr4[4][4], v4[4];
-#pragma unroll
-            for (int i = 0; i < 4; i++)
-                layer2(i, zr4[i], v4[i]);
-            if (j == 0) {
-#pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    *reinterpret_cast<float4 *>(bw + kTZr + 4 * (4 * g + i)) = make_float4(zr4[i][0], zr4[i][1], zr4[i][2], zr4[i][3]);
-                    bw[kTV + 4 * g + i] = __float_as_uint(v4[i]);
-                }
+            float zq[4], vq;
+            layer2(zq, vq);
+            if ((j & 3) == 0) {   // the four lanes of a row hold the bitwise same sums
+                *reinterpret_cast<float4 *>(bw + kTZr + 4 * (4 * g + lrow)) = make_float4(zq[0], zq[1], zq[2], zq[3]);
+                bw[kTV + 4 * g + lrow] = __float_as_uint(vq);
             }
         }
         wave_lds_sync();
