@@ -34,10 +34,12 @@ using namespace r48mlp;
 //             (lane j + 16g: W1[16ub + j][4s + g], constant); D lane j + 16g, register i = row
 //             4g + i, unit 16ub + j.  2 nets x 4 unit blocks x 4 k-steps = 32 MFMAs per tile
 //   ReLU6     mask / h elementwise in that layout (exact decisions near 0 and 6, below)
-//   layer 2   logits and value of row 4g + i: each lane sums its 4 units, the 16 lanes of the row
-//             group add up with a DPP rotation butterfly (every lane gets the bitwise same sum)
-//   loss      per row (every lane of the group, counted once): softmax, entropy, td -> dz, dv
-//   dh        [mask] W2^T dz / [mask] wc2 dv, elementwise; db1, dW2, dwc2 in per-lane partials
+//   layer 2   logits and value of the group's rows: each lane sums its 4 units per row, then one
+//             transposing DPP reduction over the 16 lanes per output leaves row 4g + lrow in lane j
+//             (lrow = 2 bit3(j) + bit2(j); the row's four lanes hold the bitwise same sums)
+//   loss      lane 4r + k on logit k of tile row r (sums / max over k within the DPP quad):
+//             softmax, entropy, td -> dz (through the logits' ReLU), dv; via the wave's LDS tile area
+//   dh        [mask] W2^T dz / [mask] wc2 dv, elementwise; db1, dW2, dwc2 in per-lane LDS partials
 //   dW1       += x^T dh on the MFMA: A = x^T (lane j + 16g, k-step i: x[r0 + 4g + i][j]), B = dh (the
 //             layer-1 layout IS the B layout of a k = rows contraction), C = dW1^T (f x units, 4
 //             accumulators per net and unit block, in AGPRs).  32 MFMAs per tile
@@ -48,8 +50,8 @@ using namespace r48mlp;
 // error of the boundary may land on the other side than the exact value, and with raw tile values as
 // inputs (up to 2^17) a flipped hidden-unit mask moves a weight-gradient entry by a whole row's term
 // (dh x). So the update decides them on exact-enough values: a hidden pre-activation or a logit whose
-// fp32 value lies within its fp32 error bound of the boundary is recomputed in fp64 (rare: a branch
-// taken by ~1e-5 of the units, ~1e-3 of the rows' logits).
+// fp32 value lies within its fp32 error bound of the boundary is recomputed in fp64 (rare: the hot path
+// only flags the tile; a fix-up redoes the flagged rows' backward on the difference).
 constexpr int kTrainWaves = 4;
 constexpr int kRec = 2504;                 // 2,501 gradient floats + actor loss + critic loss + pad
 constexpr int kRecLossA = 2501, kRecLossC = 2502;
