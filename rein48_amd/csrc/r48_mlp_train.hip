@@ -208,7 +208,7 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
     // layer-1 B operands and biases of every lane (read back each tile: 40 registers the rest of
     // the tile needs)
     __shared__ __attribute__((aligned(16))) uint32_t tiles_lds[kTrainWaves][kTileWords];
-    __shared__ __attribute__((aligned(16))) float w1_lds[64][92];   // 92: conflict-free b128 reads
+    __shared__ __attribute__((aligned(16))) float w1_lds[64][100];   // 100: conflict-free b128 reads
     // per lane: the db1 / dW2 / dwc2 partials, per unit block [dW2[k] x 4 | dwc2 | db1 | dbc1 | pad]
     // (read-modified-written by the backward one unit block at a time: registers for two waves per
     // SIMD)
@@ -242,6 +242,7 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
             for (int k = 0; k < 4; k++)
                 w1_lds[lane][40 + 4 * ub + k] = w2_at(w, 16 * ub + j, k);
             w1_lds[lane][56 + ub] = w[kC2W + 16 * ub + j];
+            w1_lds[lane][92 + ub] = w2_at(w, 16 * ub + j, g);   // the dh MFMA's B operand: W2[g][16ub + j]
         }
     }
     float *acc = acc_lds[wave][lane];
@@ -434,6 +435,7 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
         // (register i = row, lane = unit); `sel` picks the rows (bit i). The fix-up runs it on
         // differences (`fix`): dv does not depend on any decision, so only its mask terms move there,
         // and the db2 change goes to the unit block's spare slot (slot k = ub, once per row group)
+        f32x4 sdhm[4];   // the hot path's W2^T dz (MFMA, below)
         auto rows_backward = [&](const float (&dz)[4][4], const float (&dv)[4], uint32_t sel, bool bits, uint32_t mk,
                                  bool fix) {
             const float4 c2 = wl[14];
@@ -449,7 +451,8 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
                         continue;
                     const float ha = __builtin_amdgcn_fmed3f(pre[0][ub][i], 0.0f, 6.0f);
                     const float hc = __builtin_amdgcn_fmed3f(pre[1][ub][i], 0.0f, 6.0f);
-                    const float sdh = fmaf(w4.w, dz[i][3], fmaf(w4.z, dz[i][2], fmaf(w4.y, dz[i][1], w4.x * dz[i][0])));
+                    const float sdh = fix ? fmaf(w4.w, dz[i][3], fmaf(w4.z, dz[i][2], fmaf(w4.y, dz[i][1], w4.x * dz[i][0])))
+                                          : sdhm[ub][i];
                     // the masks: the given bits (fix-up) or the fp32 decisions 0 < a < 6, i.e. |a - 3| < 3
                     const bool ma = bits ? ((mk >> (4 * ub + i)) & 1u) != 0 : fabsf(pre[0][ub][i] - 3.0f) < 3.0f;
                     const bool mc = bits ? ((mk >> (16 + 4 * ub + i)) & 1u) != 0 : fabsf(pre[1][ub][i] - 3.0f) < 3.0f;
@@ -545,6 +548,14 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
                 dz[i][0] = d4.x, dz[i][1] = d4.y, dz[i][2] = d4.z, dz[i][3] = d4.w;
                 dv[i] = __uint_as_float(bw[kTDv + 4 * g + i]);
             }
+            // W2^T dz on the MFMA: A = dz (lane j + 16g: row j, logit g), B = W2[g][16ub + j], D = [row
+            // 4g + i][unit 16ub + j] -- the same k-ordered fmaf chain as the fix-up's VALU form
+            const float adz = __uint_as_float(bw[kTDz + 4 * j + g]);
+            const float4 w2g = wl[23];
+            const float w2b[4] = {w2g.x, w2g.y, w2g.z, w2g.w};
+#pragma unroll
+            for (int ub = 0; ub < 4; ub++)
+                sdhm[ub] = __builtin_amdgcn_mfma_f32_16x16x4f32(adz, w2b[ub], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
             rows_backward(dz, dv, 0xFu, false, 0u, false);
         }
         // ---------------- exact decisions (rare: the whole wave enters, lanes pick their own rows):
@@ -606,6 +617,14 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
                     for (int k = 0; k < 4; k++)
                         pos[k] = (double)b2[k] + row_sum16_d(pk[k]) > 0.0 ? 1.0f : 0.0f;
                 }
+                // nothing to correct where every exact decision equals the hot path's (nearly always:
+                // the bounds flag ~7 % of the tiles, ~1e-3 of the flagged decisions flip)
+                bool changed = (((mx ^ mask) >> i) & 0x11111111u) != 0;
+#pragma unroll
+                for (int k = 0; k < 4; k++)
+                    changed |= (pos[k] != 0.0f) != (zr[k] > 0.0f);
+                if (!__builtin_amdgcn_ballot_w64(changed))
+                    continue;
                 // the hot path's terms with its decisions, then the exact ones: backward(exact) -
                 // backward(hot) is linear in dz and dv, so run the difference on each mask set
                 float ndz[4][4] = {}, pdz[4][4] = {}, dv4[4] = {};
