@@ -148,18 +148,14 @@ __device__ __forceinline__ double row_sum16_d(double v)
 __device__ __forceinline__ float w1_at(const float *w, int base, int u, int f) { return w[base + 32 * (u >> 1) + 2 * f + (u & 1)]; }
 __device__ __forceinline__ float w2_at(const float *w, int u, int k) { return w[kA2W + 8 * (u >> 1) + 2 * k + (u & 1)]; }
 
-// fp64 pre-activation of hidden unit u of one network on the row whose 16 cell bytes are `cells`
+// fp64 pre-activation of one hidden unit on the row whose 16 cell bytes are `cells`; `unit` = the
+// unit's 16 weights and bias in the workgroup's LDS copy (unit-major, 17 floats: conflict-free)
 template <int MODE>
-__device__ __forceinline__ double preact64(const float *w, int base, int bbase, int u, const uint8_t *cells)
+__device__ __forceinline__ double preact64(const float *unit, const uint8_t *cells)
 {
-    // the weights are re-read here, on the rare path: an opaque pointer keeps the compiler from
-    // hoisting these loop-invariant loads out of the tile loop into 128 live registers
-    uint64_t wa = reinterpret_cast<uint64_t>(w);
-    asm volatile("" : "+s"(wa));
-    w = reinterpret_cast<const float *>(wa);
-    double a = w[bbase + u];
+    double a = unit[16];
     for (int f = 0; f < 16; f++)
-        a = __builtin_fma((double)w1_at(w, base, u, f), (double)cell_input<MODE>(cells[f]), a);
+        a = __builtin_fma((double)unit[f], (double)cell_input<MODE>(cells[f]), a);
     return a;
 }
 
@@ -209,6 +205,8 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
     // the tile needs)
     __shared__ __attribute__((aligned(16))) uint32_t tiles_lds[kTrainWaves][kTileWords];
     __shared__ __attribute__((aligned(16))) float w1_lds[64][100];   // 100: conflict-free b128 reads
+    // both networks' layer 1 for the fix-up's fp64 recompute: [net][unit][16 weights | bias]
+    __shared__ float w1x_lds[2][64][17];
     // per lane: the db1 / dW2 / dwc2 partials, per unit block [dW2[k] x 4 | dwc2 | db1 | dbc1 | pad]
     // (read-modified-written by the backward one unit block at a time: registers for two waves per
     // SIMD)
@@ -249,6 +247,10 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
 #pragma unroll
     for (int q = 0; q < 8; q++)
         reinterpret_cast<float4 *>(acc)[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int q = threadIdx.x; q < 2 * 64 * 17; q += 64 * kTrainWaves) {
+        const int net = q / (64 * 17), u = (q / 17) % 64, f = q % 17;
+        w1x_lds[net][u][f] = f < 16 ? w1_at(w, kW1[net], u, f) : w[kB1[net] + u];
+    }
     __syncthreads();
     const float4 *wl = reinterpret_cast<const float4 *>(w1_lds[lane]);   // this lane's constants
     // fp32 error bound of a hidden pre-activation: 16 roundings below |b| + sum |w| max x, i.e.
@@ -584,8 +586,7 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
             uint32_t mx = mask;   // exact hidden masks
             for (uint32_t m = edge; m; m &= m - 1) {
                 const int bit = __builtin_ctz(m), net = bit >> 4, ub = (bit >> 2) & 3, i = bit & 3;
-                const double ad = preact64<MODE>(w, net ? kC1W : kA1W, net ? kC1B : kA1B, 16 * ub + j,
-                                                 cells + 16 * (4 * g + i));
+                const double ad = preact64<MODE>(&w1x_lds[net][16 * ub + j][0], cells + 16 * (4 * g + i));
                 mx = (ad > 0.0 && ad < 6.0) ? (mx | (1u << bit)) : (mx & ~(1u << bit));
             }
 #pragma unroll
@@ -607,7 +608,7 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
                     const uint8_t *rc = cells + 16 * ri;
                     double pk[4] = {0.0, 0.0, 0.0, 0.0};
                     for (int ub = 0; ub < 4; ub++) {
-                        const double ad = preact64<MODE>(w, kA1W, kA1B, 16 * ub + j, rc);
+                        const double ad = preact64<MODE>(&w1x_lds[0][16 * ub + j][0], rc);
                         const double h = ad < 0.0 ? 0.0 : (ad > 6.0 ? 6.0 : ad);
 #pragma unroll
                         for (int k = 0; k < 4; k++)
