@@ -253,8 +253,10 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
     }
     __syncthreads();
     const float4 *wl = reinterpret_cast<const float4 *>(w1_lds[lane]);   // this lane's constants
-    // fp32 error bound of a hidden pre-activation: 16 roundings below |b| + sum |w| max x, i.e.
-    // < 2^-20 (|b| + sum |w| max x); 2x margin, + 2^-21 for the rounding of the decision's a - 3;
+    // fp32 error bound of a hidden pre-activation: the MFMA's k-ordered chain of 16 fmaf from b is
+    // within gamma_16 (|b| + sum |w x|) of the exact value (gamma_n = n u / (1 - n u), u = 2^-24:
+    // 2^-20 (1 + 2^-20)); bounded by 1.0625 * 2^-20 (|b| + sum |w| max x) (the 1/16 covers gamma's
+    // excess and the bound's own fp32 roundings), + 2^-21 for the rounding of the decision's a - 3;
     // with the largest |b| and sum |w| of the network's 64 units (wave-uniform, SGPRs)
     float s1[2], e1[2];
 #pragma unroll
@@ -267,12 +269,14 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
             sm = fmaxf(sm, sa);
             bm = fmaxf(bm, fabsf(w[kB1[net] + u]));
         }
-        s1[net] = uniform(sm * 0x1p-19f);
-        e1[net] = uniform(fmaf(bm, 0x1p-19f, 0x1p-21f));
+        s1[net] = uniform(sm * 0x1.1p-20f);
+        e1[net] = uniform(fmaf(bm, 0x1.1p-20f, 0x1p-21f));
     }
-    // fp32 error bound of a pre-ReLU logit: its own sum (64 products of |h| <= 6: < 2^-18 (|b2| +
-    // 6 sum |W2[k][:]|)) plus the hidden units' errors carried through W2 (each < 2^-20 (|b1| +
-    // sum |W1[u][:]| max x)); 2x-4x margins (wave-uniform: kept in SGPRs)
+    // fp32 error bound of a pre-ReLU logit: its own sum (64 products of |h| <= 6, b2 added last; every
+    // term passes 9 roundings -- a 4-fmaf chain per lane, the 4 levels of the 16-lane reduction, the
+    // bias: < 9 u (|b2| + 6 sum |W2[k][:]|), bounded by 2^-19 (...)) plus the hidden units' errors
+    // carried through W2 (each < 1.0625 * 2^-20 (|b1| + sum |W1[u][:]| max x), see above; the clamp
+    // is 1-Lipschitz) (wave-uniform: kept in SGPRs)
     float zedge[4], zcarry[4], hb = 0.f, hw = 0.f;
     for (int u = 0; u < 64; u++) {
         float sw = 0.f;
@@ -287,8 +291,8 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
         float sa = 0.f;
         for (int u = 0; u < 64; u++)
             sa += fabsf(w2_at(w, u, k));
-        zedge[k] = uniform((fabsf(w[kA2B + k]) + 6.0f * sa) * 0x1p-16f);
-        zcarry[k] = uniform(sa * 0x1p-19f);
+        zedge[k] = uniform((fabsf(w[kA2B + k]) + 6.0f * sa) * 0x1p-19f);
+        zcarry[k] = uniform(sa * 0x1.1p-20f);
         b2[k] = uniform(w[kA2B + k]);
     }
     hb = uniform(hb);
