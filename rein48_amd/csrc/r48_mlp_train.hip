@@ -585,7 +585,8 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
                         const float d = fabsf(pre[net][ub][i] - 3.0f);
                         const uint32_t bit = 1u << (16 * net + 4 * ub + i);
                         mask |= d < 3.0f ? bit : 0u;
-                        edge |= fabsf(d - 3.0f) < bound[net][i] ? bit : 0u;
+                        // (the bound again, from the row's max input in LDS: not kept live across the tile)
+                        edge |= fabsf(d - 3.0f) < fmaf(s1[net], __uint_as_float(bw[kTXm + 4 * g + i]), e1[net]) ? bit : 0u;
                     }
             uint32_t mx = mask;   // exact hidden masks
             for (uint32_t m = edge; m; m &= m - 1) {
