@@ -13,7 +13,9 @@ OBJ := $(patsubst rein48_amd/csrc/%.hip,$(OBJDIR)/%.o,$(SRC))
 # the fused A3C update keeps its loop-carried gradient slices in AGPRs and its MFMA results in
 # VGPRs (no accumulator round trips through v_accvgpr_read before each epilogue)
 FLAGS_r48_a3c_train := -mllvm -amdgpu-mfma-vgpr-form=1
-FLAGS_r48_policy ?=
+# the CNN rollout megakernel: the max-ILP machine scheduler (rollout 7.82 -> 7.70 ms textbook, 7.46 -> 7.35 ms
+# reference over 4 alternated samples each, profiles/r04/a3c/rollout_sched_max_ilp_ab.txt)
+FLAGS_r48_policy ?= -mllvm -amdgpu-sched-strategy=max-ilp
 # the cell-grouped ResNet kernel keeps its 16 x 4 live accumulators in VGPRs (the epilogue reads
 # them without v_accvgpr_read) and the block input in AGPRs
 FLAGS_r48_resnet ?= -mllvm -amdgpu-mfma-vgpr-form=1
