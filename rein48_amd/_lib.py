@@ -22,6 +22,7 @@ AUTO_RESET, RANDOM_POLICY, MERGE_REWARD = 1, 2, 4
 FEAT_VALUES, FEAT_EXPONENTS = 0, 1
 F32, BF16 = 0, 1
 REPLAY_RING, REPLAY_FILL_DRAIN = 0, 1
+DRAW_CONTRACT = 3          # R48_DRAW_CONTRACT (include/rein48.h); test_abi checks the two agree
 
 # name -> (restype, argtypes); mirrors include/rein48.h one to one
 _P, _I32, _I64, _U32, _U64 = C.c_void_p, C.c_int32, C.c_int64, C.c_uint32, C.c_uint64

@@ -15,18 +15,31 @@ counters restores every later draw.
 One file per rank: each rank owns its boards and its replay shard, so pass a
 per-rank path (e.g. "ckpt.rank%d.pt" % rank). Files are written with torch.save and read back with
 torch.load(weights_only=True): plain tensors, numbers and strings, nothing executable.
+
+load() refuses (ValueError) a file whose resume could not be bit-identical: another kind or format,
+another draw contract (R48_DRAW_CONTRACT: the same counters would give other draws), another rank's
+shard (its first global board id, which keys every Philox draw), or a configuration that differs in a
+field that fixes buffer shapes, the draws (seed), the network's inputs (features) or numerics (bf16),
+or the loss (mode). Hyper-parameters such as lr, gamma or epsilon may differ (a deliberate change).
 """
 import dataclasses
 
 import torch
 
-FORMAT = 1
+from ._lib import DRAW_CONTRACT
 
-# configuration fields that fix buffer shapes: a checkpoint only loads into a trainer that agrees
-_SHAPE_FIELDS = {
-    "a3c": ("n_boards", "max_steps", "net"),
-    "dqn": ("n_boards", "replay_capacity", "channels", "blocks", "bn", "bf16"),
+FORMAT = 2
+
+# configuration fields a checkpoint must agree on: buffer shapes, draws, inputs, numerics, loss
+_MATCH_FIELDS = {
+    "a3c": ("n_boards", "max_steps", "net", "seed", "mode", "features", "bf16"),
+    "dqn": ("n_boards", "replay_capacity", "channels", "blocks", "bn", "bf16", "seed", "reward_transform"),
 }
+
+
+def _gid0(trainer, kind):
+    """Global id of the trainer's first board (rank * n_boards): keys the Philox draws of its shard."""
+    return int(trainer.gid0) if kind == "a3c" else int(trainer.rank) * int(trainer.cfg.n_boards)
 
 
 def _kind(trainer):
@@ -78,16 +91,20 @@ def _load_replay(rep, st):
         d = rep.device
         rep.store(rows["state"].to(d), rows["action"].to(d), rows["reward"].to(d), rows["next_state"].to(d),
                   rows["done"].to(d))
-    rep.set_counters(st["size"], st["head"], st["sample_ctr"])
+        rep.set_counters(st["size"], st["head"], st["sample_ctr"])
+    else:                  # contents not saved: an empty ring that refills (no stale rows sampled)
+        rep.set_counters(0, 0, st["sample_ctr"])
 
 
 def save(trainer, path, replay=True):
     """Write `trainer`'s state to `path` (replay=False leaves the DQN ring's contents out: the
-    resumed ring then holds `size` zero transitions until they are overwritten)."""
+    resumed ring starts empty and refills from the env before it is sampled again, so that resume
+    is not bit-identical to uninterrupted training)."""
     kind = _kind(trainer)
     if trainer.device.type == "cuda":
         torch.cuda.synchronize(trainer.device)
-    st = {"format": FORMAT, "kind": kind, "cfg": dataclasses.asdict(trainer.cfg), "updates": int(trainer.updates)}
+    st = {"format": FORMAT, "kind": kind, "cfg": dataclasses.asdict(trainer.cfg), "updates": int(trainer.updates),
+          "draw_contract": DRAW_CONTRACT, "gid0": _gid0(trainer, kind)}
     if kind == "a3c":
         st.update(net=_cpu_state(trainer.net), ms=_cpu(trainer.opt.ms), mom=_cpu(trainer.opt.mom),
                   env=_env_state(trainer.env), sample_ctr=int(trainer.sample_ctr))
@@ -107,8 +124,14 @@ def load(trainer, path):
     if st.get("format") != FORMAT or st.get("kind") != kind:
         raise ValueError("checkpoint: %s is a %s checkpoint of format %s, not a %s one of format %d"
                          % (path, st.get("kind"), st.get("format"), kind, FORMAT))
+    if st["draw_contract"] != DRAW_CONTRACT:
+        raise ValueError("checkpoint: %s was written under draw contract %d, this library draws under %d"
+                         % (path, st["draw_contract"], DRAW_CONTRACT))
+    if st["gid0"] != _gid0(trainer, kind):
+        raise ValueError("checkpoint: %s holds the shard starting at board %d, this trainer's starts at %d "
+                         "(another rank's file?)" % (path, st["gid0"], _gid0(trainer, kind)))
     cfg = dataclasses.asdict(trainer.cfg)
-    for f in _SHAPE_FIELDS[kind]:
+    for f in _MATCH_FIELDS[kind]:
         if cfg[f] != st["cfg"][f]:
             raise ValueError("checkpoint: %s = %r in the trainer, %r in %s" % (f, cfg[f], st["cfg"][f], path))
     dev = trainer.device

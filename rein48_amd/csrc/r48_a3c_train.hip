@@ -43,6 +43,7 @@
 
 #include "../../include/rein48.h"
 #include "r48_cnn_common.h"
+#include "r48_host.h"
 
 namespace r48 {
 void set_last_error(const std::string &msg);
@@ -739,12 +740,7 @@ int r48_cnn_train_grad(const int8_t *boards, int64_t rows, int64_t n_boards, con
     const size_t lds = kLds;
     // one instantiation per input encoding (no per-cell branch); each needs the LDS opt-in once
     auto kern = mode == R48_FEAT_VALUES ? k_cnn_train<R48_FEAT_VALUES> : k_cnn_train<R48_FEAT_EXPONENTS>;
-    static bool attr_set[2] = {false, false};
-    if (!attr_set[mode == R48_FEAT_VALUES]) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)lds);
-        attr_set[mode == R48_FEAT_VALUES] = true;
-    }
+    r48::ensure_dynamic_lds(reinterpret_cast<const void *>(kern), (int)lds, r48::stream_device((hipStream_t)stream));
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), lds, (hipStream_t)stream, boards, rows, n_boards, actions,
                        targets, wn, cm, counts, beta, (const uint4 *)wfrag, bias, workspace);
     // the group sums go after the records in the workspace (r48_cnn_train_workspace_floats)

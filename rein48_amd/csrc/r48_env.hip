@@ -10,10 +10,15 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <map>
+#include <mutex>
+#include <set>
 #include <string>
+#include <utility>
 
 #include "../../include/rein48.h"
 #include "r48_board.h"
+#include "r48_host.h"
 
 using r48::Board;
 
@@ -819,6 +824,43 @@ thread_local std::string g_last_error;
 
 namespace r48 {
 void set_last_error(const std::string &msg) { g_last_error = msg; }
+
+int stream_device(hipStream_t stream)
+{
+    int dev = 0;
+    if (stream != nullptr && hipStreamGetDevice(stream, &dev) == hipSuccess)
+        return dev;
+    return hipGetDevice(&dev) == hipSuccess ? dev : 0;
+}
+
+int device_cus(int device)
+{
+    static std::mutex mu;
+    static std::map<int, int> cache;
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = cache.find(device);
+    if (it != cache.end())
+        return it->second;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0)
+        cus = 256;
+    cache[device] = cus;
+    return cus;
+}
+
+void ensure_dynamic_lds(const void *kernel, int bytes, int device)
+{
+    static std::mutex mu;
+    static std::set<std::pair<const void *, int>> done;
+    std::lock_guard<std::mutex> lock(mu);
+    if (!done.insert({kernel, device}).second)
+        return;
+    int prev = -1;
+    const bool switched = hipGetDevice(&prev) == hipSuccess && prev != device && hipSetDevice(device) == hipSuccess;
+    (void)hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    if (switched)
+        (void)hipSetDevice(prev);
+}
 }  // namespace r48
 
 namespace {

@@ -26,6 +26,7 @@
 #include "../../include/rein48.h"
 #include "r48_board.h"
 #include "r48_cnn_common.h"
+#include "r48_host.h"
 
 namespace r48 {
 void set_last_error(const std::string &msg);
@@ -377,9 +378,7 @@ int r48_cnn_policy_forward(const int8_t *boards, int64_t n, const void *wfrag, c
         return fail(R48_EINVAL, "boards, boards_out, wfrag and logits must be 16-byte aligned");
     if (n == 0)
         return R48_OK;
-    int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) == hipSuccess)
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const int cus = r48::device_cus(r48::stream_device((hipStream_t)stream));
     const int64_t tiles = (n + 31) / 32;
     const int64_t blocks = std::min<int64_t>((tiles + kWaves - 1) / kWaves, (int64_t)cus * kOcc);
     // one instantiation per input encoding (no per-cell branch)
@@ -406,9 +405,7 @@ int r48_cnn_rollout(int8_t *boards, int64_t n, int32_t n_steps, const void *wfra
         return fail(R48_EINVAL, "boards, traj_boards and wfrag must be 16-byte aligned");
     if (n == 0)
         return R48_OK;
-    int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) == hipSuccess)
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const int cus = r48::device_cus(r48::stream_device((hipStream_t)stream));
     const int64_t pairs = (n + 63) / 64;
     const int64_t blocks = std::min<int64_t>((pairs + kWaves - 1) / kWaves, (int64_t)cus * kOccRoll);
     const bool rw = flags & R48_MERGE_REWARD;

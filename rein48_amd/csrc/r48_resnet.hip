@@ -37,6 +37,7 @@
 
 #include "../../include/rein48.h"
 #include "r48_board.h"
+#include "r48_host.h"
 
 namespace r48 {
 void set_last_error(const std::string &msg);
@@ -367,19 +368,12 @@ int r48_resnet_q_forward(const int8_t *boards, int64_t n, const void *wblob, flo
         return fail(R48_EINVAL, "boards, wblob and q must be 16-byte aligned");
     if (n == 0)
         return R48_OK;
-    int dev = 0, cus = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-        cus = 256;
+    const int dev = r48::stream_device((hipStream_t)stream);
+    const int cus = r48::device_cus(dev);
     const int64_t tiles = (n + kBoardsPerTile - 1) / kBoardsPerTile;
     const int grid = (int)(tiles < cus ? tiles : cus);
     const size_t lds = (size_t)(2 * kBufFrags * 64) * 16;
-    static bool attr_set = false;
-    if (!attr_set) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(k_resnet_q),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        attr_set = true;
-    }
+    r48::ensure_dynamic_lds(reinterpret_cast<const void *>(k_resnet_q), (int)lds, dev);
     hipLaunchKernelGGL(k_resnet_q, dim3(grid), dim3(kThreads), lds, (hipStream_t)stream, boards, n,
                        reinterpret_cast<const uint4 *>(wblob), q, actions, eps, (uint32_t)seed,
                        (uint32_t)(seed >> 32), gid0, ctr);

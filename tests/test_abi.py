@@ -24,6 +24,15 @@ def test_header_parses():
     assert "r48_env_step" in names and "r48_last_error" in names and len(names) >= 20
 
 
+def test_binding_constants_mirror_the_header():
+    text = open(HEADER).read()
+    consts = {k: int(v, 0) for k, v in
+              re.findall(r"^#define (R48_\w+)\s+\(?(-?(?:0x[0-9a-fA-F]+|\d+))u?\)?", text, re.M)}
+    assert consts["R48_DRAW_CONTRACT"] == _lib.DRAW_CONTRACT
+    assert (consts["R48_AUTO_RESET"], consts["R48_RANDOM_POLICY"], consts["R48_MERGE_REWARD"]) == \
+        (_lib.AUTO_RESET, _lib.RANDOM_POLICY, _lib.MERGE_REWARD)
+
+
 def test_library_exports_every_declared_symbol():
     lib = _lib.load()
     out = subprocess.check_output(["nm", "-D", "--defined-only", _lib.LIB_PATH], text=True)

@@ -53,3 +53,25 @@ def test_checkpoint_rejects_a_mismatched_trainer(tmp_path):
         checkpoint.load(other, path)
     with pytest.raises(TypeError):
         checkpoint.save(object(), path)
+
+
+def test_checkpoint_rejects_another_seed_rank_or_contract(tmp_path):
+    """seed, rank shard and draw contract must match (a resume under other draws is not
+    bit-identical); hyper-parameters such as lr may differ."""
+    from rein48_amd import checkpoint
+    from rein48_amd.dqn import DQNConfig, DQNLearner
+    a = _learner()
+    path = tmp_path / "dqn.pt"
+    checkpoint.save(a, path)
+    with pytest.raises(ValueError, match="seed"):
+        checkpoint.load(DQNLearner(DQNConfig(channels=8, blocks=2, bf16=False, seed=4), device="cpu"), path)
+    b = _learner()
+    b.rank = 1
+    with pytest.raises(ValueError, match="shard"):
+        checkpoint.load(b, path)
+    st = torch.load(path, weights_only=True)
+    st["draw_contract"] = 2
+    torch.save(st, tmp_path / "old.pt")
+    with pytest.raises(ValueError, match="draw contract"):
+        checkpoint.load(_learner(), tmp_path / "old.pt")
+    checkpoint.load(DQNLearner(DQNConfig(channels=8, blocks=2, bf16=False, seed=3, lr=5e-4), device="cpu"), path)

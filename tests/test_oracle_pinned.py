@@ -160,6 +160,35 @@ def test_philox_mode_matches_reference_fingerprint(golden):
     assert abs(lengths.std(ddof=1) - ref["sd"]) < 0.05 * ref["sd"]
 
 
+def test_philox_mode_matches_whole_reference_fingerprint(golden):
+    """Draw contract 3 (Philox4x32-7 step draws, r48_board.h kStepRounds) against every statistic of
+    the reference fingerprint (tests/fingerprint_check.py): episode-length histogram (chi-square),
+    score mean / sd, max-tile histogram (chi-square) and the no-op fraction. Boards are stepped
+    without auto-reset so that the final board of every episode is seen, then reset by the masked
+    Philox reset (GameClient.py:33-38's contract, r48_env_reset)."""
+    from fingerprint_check import check
+    n, T, window = 4096, 1400, 700
+    seed = 0x5EED7
+    boards = O.reset_philox(np.zeros((n, 16), np.int8), seed=seed, reset_ctr=0)
+    start = np.zeros(n, np.int64)
+    noop = np.zeros(n, np.int64)
+    L, S, M, N = [], [], [], []
+    for t in range(T):
+        r = O.step_philox(boards, seed=seed, step=t, flags=O.RANDOM_POLICY, want_score=True)
+        noop += r["changed"] == 0
+        d = np.nonzero(r["done"])[0]
+        keep = d[start[d] < window]
+        L.append(t + 1 - start[keep])
+        S.append(r["score"][keep])
+        M.append(1 << r["boards"][keep].max(1).astype(np.int64))
+        N.append(noop[keep].copy())
+        start[d] = t + 1
+        noop[d] = 0
+        boards = O.reset_philox(r["boards"], seed=seed, reset_ctr=t + 1, mask=r["done"]) if d.size else r["boards"]
+    res = check(golden["fingerprint"], *(np.concatenate(x) for x in (L, S, M, N)), sd_tol=0.05)
+    assert res["episodes"] > 15_000, res
+
+
 def test_oracle_rejects_bad_action():
     with pytest.raises(ValueError):
         O.move(np.zeros(16, np.int8), 7)
