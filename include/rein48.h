@@ -281,10 +281,11 @@ int r48_mlp_rollout(int8_t *boards, int64_t n, int32_t n_steps, const float *w, 
  * through the logits' ReLU): arguments as r48_cnn_train_grad with the MLP weight blob w of
  * r48_mlp_policy_forward; grad float[2504] (16-byte aligned) receives the gradient in FlatParams
  * order (a1.w [64][16] | a1.b | a2.w [4][64] | a2.b | c1.w | c1.b | c2.w | c2.b = 2,501 floats),
- * then the actor and critic losses. workspace: r48_mlp_train_workspace_floats() floats.
- * Deterministic (fixed-order reduction). Replaces NetworkTool.get_loss_value + compute_gradients
- * (a3c.py:99-123, 73-80). */
-int64_t r48_mlp_train_workspace_floats(void);
+ * then the actor and critic losses. workspace: r48_mlp_train_workspace_floats(rows) 4-byte words
+ * (16-byte aligned; the per-wave records of the hot and the exact-decision pass and the hot pass's
+ * per-wave lists of flagged tiles). Deterministic (fixed-order reduction). Replaces
+ * NetworkTool.get_loss_value + compute_gradients (a3c.py:99-123, 73-80). */
+int64_t r48_mlp_train_workspace_floats(int64_t rows);
 int r48_mlp_train_grad(const int8_t *boards, int64_t rows, int64_t n_boards, const int8_t *actions,
                        const float *targets, const float *wn, const float *cm, const float *counts, float beta,
                        int32_t mode, const float *w, float *workspace, float *grad, void *stream);

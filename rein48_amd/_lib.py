@@ -109,7 +109,7 @@ SIGNATURES = {
     "r48_mlp_policy_forward": (C.c_int, [_P, _I64, _P, _I32, _P, _P, _P, _U64, _I64, _U32, _P]),
     "r48_mlp_rollout": (C.c_int, [_P, _I64, _I32, _P, _I32, _P, _P, _P, _P, _P, _P, _U64, _I64, _U32, _U64, _U32,
                                   _U32, _P]),
-    "r48_mlp_train_workspace_floats": (_I64, []),
+    "r48_mlp_train_workspace_floats": (_I64, [_I64]),
     "r48_mlp_train_grad": (C.c_int, [_P, _I64, _I64, _P, _P, _P, _P, _P, C.c_float, _I32, _P, _P, _P, _P]),
     "r48_conv3x3_bn_in": (C.c_int, [_P, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "r48_bn_finish": (C.c_int, [_P, _I32, _I64, _I32, _P, _P, _P, _P, C.c_float, C.c_float, _P, _P, _P]),

@@ -213,7 +213,7 @@ def mlp_train_grad(net, boards, actions, targets, wn, cm=None, counts=None, beta
         w = pack_mlp(net)
     L = _lib.load()
     if workspace is None:
-        workspace = torch.empty(int(L.r48_mlp_train_workspace_floats()), dtype=torch.float32, device=dev)
+        workspace = torch.empty(int(L.r48_mlp_train_workspace_floats(rows)), dtype=torch.float32, device=dev)
     out = torch.empty(2504, dtype=torch.float32, device=dev)
     check(L.r48_mlp_train_grad(ptr(boards), rows, int(n_boards or rows), ptr(actions), ptr(targets), ptr(wn), ptr(cm),
                                ptr(counts), float(beta), _lib.FEAT_EXPONENTS if exponents else _lib.FEAT_VALUES,

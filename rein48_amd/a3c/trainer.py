@@ -310,7 +310,7 @@ class A3CTrainer:
         if self._mlp_fused():
             from .fused import mlp_train_grad
             if getattr(self, "_mlp_ws", None) is None:
-                self._mlp_ws = torch.empty(int(_lib.load().r48_mlp_train_workspace_floats()), dtype=torch.float32,
+                self._mlp_ws = torch.empty(int(_lib.load().r48_mlp_train_workspace_floats(states.numel() // 16)), dtype=torch.float32,
                                            device=self.device)
             g, actor, critic = mlp_train_grad(
                 self.net, states.reshape(-1, 16), self.actions.reshape(-1), targets.reshape(-1).contiguous(),

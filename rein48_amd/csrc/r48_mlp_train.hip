@@ -50,8 +50,15 @@ using namespace r48mlp;
 // error of the boundary may land on the other side than the exact value, and with raw tile values as
 // inputs (up to 2^17) a flipped hidden-unit mask moves a weight-gradient entry by a whole row's term
 // (dh x). So the update decides them on exact-enough values: a hidden pre-activation or a logit whose
-// fp32 value lies within its fp32 error bound of the boundary is recomputed in fp64 (rare: the hot path
-// only flags the tile; a fix-up redoes the flagged rows' backward on the difference).
+// fp32 value lies within its fp32 error bound of the boundary is recomputed in fp64. Two passes:
+//   FIX = false  the hot path: fp32 decisions everywhere; a tile with any decision inside its bound
+//                (6.6-6.9 % of the config-3 tiles) only goes on the wave's list (no fix-up code in
+//                this kernel: its registers stay free for the hot loop)
+//   FIX = true   one wave per hot wave walks that wave's list in order: the same forward (the same
+//                instructions, so the same bits), the exact decisions of the flagged units and rows,
+//                and -- only where a decision changes (~1e-3 of them) -- the loss and the row's backward
+//                on the difference (exact decisions minus the hot path's), into its own record.
+// The records of both passes are summed in one fixed order (deterministic).
 constexpr int kTrainWaves = 4;
 constexpr int kRec = 2504;                 // 2,501 gradient floats + actor loss + critic loss + pad
 constexpr int kRecLossA = 2501, kRecLossC = 2502;
@@ -194,11 +201,14 @@ __device__ __forceinline__ RowIn fetch_row(int64_t r, int64_t rows, int64_t bidx
     return x;
 }
 
-template <int MODE, bool REF>
+// flag list of hot wave q: int2 entries (tile, any logit near its boundary) at list[2 q cap ..], its
+// length in list_len[q]; cap >= the wave's tile count
+template <int MODE, bool REF, bool FIX>
 __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_eu(2))) void k_mlp_train(
     const int8_t *__restrict__ boards, int64_t rows, int64_t n_boards, const int8_t *__restrict__ actions,
     const float *__restrict__ targets, const float *__restrict__ wn, const float *__restrict__ cm,
-    const float *__restrict__ counts, float beta, const float *__restrict__ w, float *__restrict__ partials)
+    const float *__restrict__ counts, float beta, const float *__restrict__ w, float *__restrict__ partials,
+    int32_t *__restrict__ list, int32_t *__restrict__ list_len, int64_t cap)
 {
     // per wave: the tile's 16 boards (64 words) and each row's largest input; per workgroup: the
     // layer-1 B operands and biases of every lane (read back each tile: 40 registers the rest of
@@ -213,6 +223,45 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
     __shared__ __attribute__((aligned(16))) float acc_lds[kTrainWaves][64][36];   // 36: conflict-free b128 reads and writes
     const int lane = threadIdx.x & 63, j = lane & 15, g = lane >> 4;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t qw = (int64_t)blockIdx.x * kTrainWaves + wave;   // this wave's record / list
+    const int n_waves = (int)gridDim.x * kTrainWaves;
+    // FIX: the entries of all lists in one order (hot wave, position) -- deterministic -- split evenly:
+    // this wave takes entries [e_lo, e_hi); (fw, fo) = list and position of entry e_lo
+    int64_t e_lo = 0, e_hi = 0;
+    int fw = 0, fo = 0;
+    if (FIX) {
+        // lane l sums the lengths of lists [l * per, (l + 1) * per); an inclusive scan over the lanes
+        const int per = (n_waves + 63) / 64;
+        int64_t part = 0;
+        for (int k = 0; k < per; k++) {
+            const int w = lane * per + k;
+            part += w < n_waves ? list_len[w] : 0;
+        }
+        int64_t incl = part;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int64_t o = __shfl_up(incl, d);
+            incl += lane >= d ? o : 0;
+        }
+        const int64_t total = __shfl(incl, 63);
+        e_lo = total * qw / n_waves;
+        e_hi = total * (qw + 1) / n_waves;
+        // the lane whose lists hold entry e_lo, then the list within them (scalar walk over <= per lists)
+        const uint64_t past = __builtin_amdgcn_ballot_w64(incl <= e_lo);
+        const int l0 = __builtin_popcountll(past);   // first lane with incl > e_lo (64 if none)
+        if (e_lo < e_hi) {
+            int64_t before = l0 > 0 ? __shfl(incl, l0 - 1) : 0;
+            before = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(before >> 32)) << 32) |
+                               (uint32_t)__builtin_amdgcn_readfirstlane((int)before));
+            int w = l0 * per;
+            while (before + list_len[w] <= e_lo) {
+                before += list_len[w];
+                w++;
+            }
+            fw = w;
+            fo = (int)(e_lo - before);
+        }
+    }
     uint32_t *bw = tiles_lds[wave];
     const uint8_t *cells = reinterpret_cast<const uint8_t *>(bw);
     constexpr int kW1[2] = {kA1W, kC1W}, kB1[2] = {kA1B, kC1B};
@@ -319,24 +368,56 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
 
     const int64_t n_tiles = (rows + 15) / 16;
     const int64_t stride = (int64_t)gridDim.x * kTrainWaves;
-    int64_t tile = (int64_t)blockIdx.x * kTrainWaves + wave;
+    int32_t *my_list = list + 2 * qw * cap;   // entries (tile, any logit near its boundary)
+    int n_flag = 0;                       // hot pass: tiles put on the list (wave-uniform)
+    // fix pass: the entry being processed (cur_near) and the next one's position (fw, fo)
+    auto fix_entry = [&]() -> int2 {
+        const int2 v = *reinterpret_cast<const int2 *>(list + 2 * ((int64_t)fw * cap + fo));
+        if (++fo >= list_len[fw]) {
+            fo = 0;
+            do
+                fw++;
+            while (fw < n_waves && list_len[fw] == 0);
+        }
+        return v;
+    };
+    int cur_near = 0, nxt_near = 0;
+    int64_t tile = qw;
+    if (FIX) {
+        const int2 v = e_lo < e_hi ? fix_entry() : make_int2((int)(n_tiles - 1), 0);
+        tile = v.x;
+        nxt_near = v.y;
+    }
     // one wave per SIMD hides no load latency: row r0 + j's inputs arrive a tile ahead
     // the counts row of training row r is r mod n_boards (rows are step-major, t * n_boards + board):
     // kept incrementally as the lane's row advances by 16 * stride (a prefetch past the end, clamped
-    // to the last tile, reads a valid counts row it never uses)
+    // to the last tile, reads a valid counts row it never uses); the fix pass computes it per tile
     int64_t bnext = REF ? (std::min<int64_t>(tile, n_tiles - 1) * 16 + j) % n_boards : 0;
     const int64_t bstep = REF ? (stride * 16) % n_boards : 0;
     RowIn next = fetch_row<REF>(std::min<int64_t>(tile, n_tiles - 1) * 16 + j, rows, bnext, boards, actions, targets,
                                 wn, cm, counts);
-    for (; tile < n_tiles; tile += stride) {
+    for (int64_t e = e_lo; FIX ? e < e_hi : tile < n_tiles; e++) {
         // ---------------- inputs: row r0 + j in the four lanes j + 16g
         const RowIn in = next;
-        if (REF) {
-            bnext += bstep;
-            bnext -= bnext >= n_boards ? n_boards : 0;
+        int64_t tnext;
+        if (FIX) {
+            cur_near = nxt_near;
+            tnext = tile;
+            if (e + 1 < e_hi) {
+                const int2 v = fix_entry();
+                tnext = v.x;
+                nxt_near = v.y;
+            }
+            if (REF)
+                bnext = (tnext * 16 + j) % n_boards;
+        } else {
+            tnext = std::min<int64_t>(tile + stride, n_tiles - 1);
+            if (REF) {
+                bnext += bstep;
+                bnext -= bnext >= n_boards ? n_boards : 0;
+            }
         }
-        next = fetch_row<REF>(std::min<int64_t>(tile + stride, n_tiles - 1) * 16 + j, rows, bnext, boards, actions,
-                              targets, wn, cm, counts);
+        next = fetch_row<REF>(tnext * 16 + j, rows, bnext, boards, actions, targets, wn, cm, counts);
         const uint4 bv = in.b;
         const uint32_t bwd[4] = {bv.x, bv.y, bv.z, bv.w};
         float xa[4];   // A operands of layer 1: x[r0 + j][4s + g]
@@ -384,10 +465,12 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
                 acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[3], wb.w, acc, 0, 0, 0);
                 pre[net][ub] = acc;
             }
+        bool edge_any = false;
         // ---------------- ReLU6 decisions 0 < a < 6, i.e. |a - 3| < 3; within the fp32 error bound
         // of 0 or 6 (min(|a|, |a - 6|) = ||a - 3| - 3|) the pre-activation is redone in fp64
         // (the hot path takes the fp32 decision where it uses a mask and only asks whether any of
         // the tile's 512 pre-activations is near a boundary; the fix-up below finds which)
+        if (!FIX) {   // (the fix pass tests each unit itself)
         float bound[2][4];
 #pragma unroll
         for (int net = 0; net < 2; net++)
@@ -395,7 +478,6 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
             for (int i = 0; i < 4; i++)
                 bound[net][i] = fmaf(s1[net], xm[i], e1[net]);
         // (per row and net: the nearest of the lane's 4 units against the row's bound)
-        bool edge_any = false;
 #pragma unroll
         for (int net = 0; net < 2; net++)
 #pragma unroll
@@ -406,6 +488,7 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
                     dn[ub] = fabsf(fabsf(pre[net][ub][i] - 3.0f) - 3.0f);
                 edge_any |= fminf(fminf(dn[0], dn[1]), fminf(dn[2], dn[3])) < bound[net][i];
             }
+        }
         // ---------------- per row i of the lane group (rows 4g + i): layer 2 (the group's 16 lanes
         // add up), the loss (every lane of the group computes it; counted once) -- the same code on
         // the hot path and in the exact-decision fix-up below, so the same values
@@ -482,71 +565,90 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
                 reinterpret_cast<float4 *>(acc)[2 * ub + 1] = a1;
             }
         };
-        // hot path: fp32 decisions everywhere. Layer 2 of the lane group's rows; then the loss with
-        // lane 4r + k on logit k of tile row r (the row's DPP quad does the sums over k), rows whose
-        // logit lies within its fp32 error bound of 0 flagged in `near_rows` (bit 4r + k); then the
-        // backward
-        {
+        // layer 2 of the lane group's rows into the tile area: pre-ReLU logits (kTZr) and value (kTV)
+        auto layer2_lds = [&]() {
             float zq[4], vq;
             layer2(zq, vq);
             if ((j & 3) == 0) {   // the four lanes of a row hold the bitwise same sums
                 *reinterpret_cast<float4 *>(bw + kTZr + 4 * (4 * g + lrow)) = make_float4(zq[0], zq[1], zq[2], zq[3]);
                 bw[kTV + 4 * g + lrow] = __float_as_uint(vq);
             }
-        }
-        wave_lds_sync();
-        uint64_t near_rows;
-        {
+            wave_lds_sync();
+        };
+        // lane 4r + k: is logit k of tile row r within its fp32 error bound of the logits' ReLU
+        // boundary (bit 4r + k of the ballot); from the tile area after layer2_lds
+        auto near_ballot = [&]() -> uint64_t {
             const int r = lane >> 2;
             const float zr = __uint_as_float(bw[kTZr + lane]);
-            const float v = __uint_as_float(bw[kTV + r]);
-            const float wt = __uint_as_float(bw[kTWt + r]);
-            const float tgt = __uint_as_float(bw[kTTg + r]);
-            const float z = fmaxf(zr, 0.0f);                               // the logits' ReLU (a3c.py:153)
-            const float mz = quad_max(z);
-            float p = __expf(z - mz);
-            const float se = quad_sum(p);
-            const float inv = __builtin_amdgcn_rcpf(se), lse = mz + kLn2 * __builtin_amdgcn_logf(se);
-            p *= inv;
-            const float lq = kLn2 * __builtin_amdgcn_logf(p + kEntropyEps);
-            const float hk = -p * lq;                                       // logit k's term of the entropy
-            const float gr = -(lq + p * __builtin_amdgcn_rcpf(p + kEntropyEps));   // dH/dp_k
-            const float gbar = quad_sum(p * gr);
-            const float td = tgt - v;
-            float dz, la;
-            if (REF) {   // reference: -beta wn H - cm sum_k c_k log p_k  (losses.py, a3c.py:110-116)
-                const float c = __uint_as_float(bw[kTCm + r]);
-                const float ck = __uint_as_float(bw[kTCn + lane]);
-                const float C = quad_sum(ck);
-                dz = -beta * wt * p * (gr - gbar) - c * (ck - p * C);
-                la = -beta * wt * hk - c * (ck * (z - lse));
-            } else {     // textbook: -wn (beta H + td log p[a]), td constant for the actor
-                const bool act = lk == (int)bw[kTAc + r];
-                dz = -wt * (beta * p * (gr - gbar) + td * ((act ? 1.0f : 0.0f) - p));
-                la = -wt * (beta * hk + (act ? td * (z - lse) : 0.0f));
-            }
-            const float dv = -2.0f * wt * td;                               // critic = wn td^2
             const float xml = __uint_as_float(bw[kTXm + r]);
-            near_rows = __builtin_amdgcn_ballot_w64(fabsf(zr) < zedge_l + zcarry_l * (hb + hw * xml));
-            const float dzm = zr > 0.0f ? dz : 0.0f;
-            gb2l += dzm;
-            loss_a += la;
-            if (lk == 0) {   // the row's terms once
-                gbc2 += dv;
-                loss_c += wt * td * td;
-                bw[kTDv + r] = __float_as_uint(dv);
-            }
-            bw[kTDz + lane] = __float_as_uint(dzm);
-            bw[kTDu + lane] = __float_as_uint(dz);
-        }
-        wave_lds_sync();
-        // this lane group's rows 4g + i near a logit boundary (bit i)
-        const uint32_t near_q = (uint32_t)(near_rows >> (16 * g)) & 0xFFFFu;
-        uint32_t near = 0;
+            return __builtin_amdgcn_ballot_w64(fabsf(zr) < zedge_l + zcarry_l * (hb + hw * xml));
+        };
+        // this lane group's rows 4g + i with a logit near the boundary (bit i)
+        auto group_rows = [&](uint64_t near_rows) {
+            const uint32_t near_q = (uint32_t)(near_rows >> (16 * g)) & 0xFFFFu;
+            uint32_t near = 0;
 #pragma unroll
-        for (int i = 0; i < 4; i++)
-            near |= ((near_q >> (4 * i)) & 0xFu) != 0 ? 1u << i : 0u;
-        {
+            for (int i = 0; i < 4; i++)
+                near |= ((near_q >> (4 * i)) & 0xFu) != 0 ? 1u << i : 0u;
+            return near;
+        };
+        // the loss with lane 4r + k on logit k of tile row r (the row's DPP quad does the sums over k):
+        // dz through the logits' ReLU (kTDz), before it (kTDu), dv (kTDv) into the tile area; the hot
+        // pass also sums db2, dbc2 and the losses
+        auto loss_lds = [&]() {
+            {
+                const int r = lane >> 2;
+                const float zr = __uint_as_float(bw[kTZr + lane]);
+                const float v = __uint_as_float(bw[kTV + r]);
+                const float wt = __uint_as_float(bw[kTWt + r]);
+                const float tgt = __uint_as_float(bw[kTTg + r]);
+                const float z = fmaxf(zr, 0.0f);                               // the logits' ReLU (a3c.py:153)
+                const float mz = quad_max(z);
+                float p = __expf(z - mz);
+                const float se = quad_sum(p);
+                const float inv = __builtin_amdgcn_rcpf(se), lse = mz + kLn2 * __builtin_amdgcn_logf(se);
+                p *= inv;
+                const float lq = kLn2 * __builtin_amdgcn_logf(p + kEntropyEps);
+                const float hk = -p * lq;                                       // logit k's term of the entropy
+                const float gr = -(lq + p * __builtin_amdgcn_rcpf(p + kEntropyEps));   // dH/dp_k
+                const float gbar = quad_sum(p * gr);
+                const float td = tgt - v;
+                float dz, la;
+                if (REF) {   // reference: -beta wn H - cm sum_k c_k log p_k  (losses.py, a3c.py:110-116)
+                    const float c = __uint_as_float(bw[kTCm + r]);
+                    const float ck = __uint_as_float(bw[kTCn + lane]);
+                    const float C = quad_sum(ck);
+                    dz = -beta * wt * p * (gr - gbar) - c * (ck - p * C);
+                    la = -beta * wt * hk - c * (ck * (z - lse));
+                } else {     // textbook: -wn (beta H + td log p[a]), td constant for the actor
+                    const bool act = lk == (int)bw[kTAc + r];
+                    dz = -wt * (beta * p * (gr - gbar) + td * ((act ? 1.0f : 0.0f) - p));
+                    la = -wt * (beta * hk + (act ? td * (z - lse) : 0.0f));
+                }
+                const float dv = -2.0f * wt * td;                               // critic = wn td^2
+                const float dzm = zr > 0.0f ? dz : 0.0f;
+                if (!FIX) {      // the fix pass adds only differences
+                    gb2l += dzm;
+                    loss_a += la;
+                }
+                if (lk == 0) {   // the row's terms once
+                    if (!FIX) {
+                        gbc2 += dv;
+                        loss_c += wt * td * td;
+                    }
+                    bw[kTDv + r] = __float_as_uint(dv);
+                }
+                bw[kTDz + lane] = __float_as_uint(dzm);
+                bw[kTDu + lane] = __float_as_uint(dz);
+            }
+            wave_lds_sync();
+        };
+        if (!FIX) {
+            // ---------------- hot pass: fp32 decisions everywhere
+            layer2_lds();
+            const uint64_t near_rows = near_ballot();
+            loss_lds();
+            const uint32_t near = group_rows(near_rows);
             float dz[4][4], dv[4];
 #pragma unroll
             for (int i = 0; i < 4; i++) {
@@ -555,7 +657,7 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
                 dv[i] = __uint_as_float(bw[kTDv + 4 * g + i]);
             }
             // W2^T dz on the MFMA: A = dz (lane j + 16g: row j, logit g), B = W2[g][16ub + j], D = [row
-            // 4g + i][unit 16ub + j] -- the same k-ordered fmaf chain as the fix-up's VALU form
+            // 4g + i][unit 16ub + j] -- the same k-ordered fmaf chain as the fix pass's VALU form
             const float adz = __uint_as_float(bw[kTDz + 4 * j + g]);
             const float4 w2g = wl[23];
             const float w2b[4] = {w2g.x, w2g.y, w2g.z, w2g.w};
@@ -563,18 +665,17 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
             for (int ub = 0; ub < 4; ub++)
                 sdhm[ub] = __builtin_amdgcn_mfma_f32_16x16x4f32(adz, w2b[ub], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
             rows_backward(dz, dv, 0xFu, false, 0u, false);
-        }
-        // ---------------- exact decisions (rare: the whole wave enters, lanes pick their own rows):
-        // for a flagged row, the exact logits' ReLU and hidden masks, and the row's backward run again
-        // on the differences (exact minus what the hot path accumulated, from the hot path's dz in LDS)
-        if (__builtin_amdgcn_ballot_w64(edge_any || near != 0)) {
-            // opaque copies of the tile's pre-activations: the fix-up reads them from registers the
-            // hot path is done with
-#pragma unroll
-            for (int net = 0; net < 2; net++)
-#pragma unroll
-                for (int ub = 0; ub < 4; ub++)
-                    asm volatile("" : "+v"(pre[net][ub]));
+            // a tile with any decision within its bound goes on the list: (tile, any logit near)
+            if (__builtin_amdgcn_ballot_w64(edge_any || near != 0)) {
+                if (lane == 0)
+                    *reinterpret_cast<int2 *>(my_list + 2 * n_flag) = make_int2((int)tile, near_rows != 0 ? 1 : 0);
+                n_flag++;
+            }
+        } else {
+            // ---------------- fix pass (the whole wave; lanes pick their own rows): the exact hidden
+            // masks of the units within their bound (fp64), the exact logits' ReLU of the rows near
+            // it (fp64, when the hot pass saw any), and only where a decision differs from the hot
+            // path's: the loss (the hot path's dz) and the row's backward on the differences
             uint32_t mask = 0, edge = 0;   // fp32 decisions and flags, bit 16 net + 4 ub + i
 #pragma unroll
             for (int net = 0; net < 2; net++)
@@ -585,8 +686,7 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
                         const float d = fabsf(pre[net][ub][i] - 3.0f);
                         const uint32_t bit = 1u << (16 * net + 4 * ub + i);
                         mask |= d < 3.0f ? bit : 0u;
-                        // (the bound again, from the row's max input in LDS: not kept live across the tile)
-                        edge |= fabsf(d - 3.0f) < fmaf(s1[net], __uint_as_float(bw[kTXm + 4 * g + i]), e1[net]) ? bit : 0u;
+                        edge |= fabsf(d - 3.0f) < fmaf(s1[net], xm[i], e1[net]) ? bit : 0u;
                     }
             uint32_t mx = mask;   // exact hidden masks
             for (uint32_t m = edge; m; m &= m - 1) {
@@ -594,22 +694,19 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
                 const double ad = preact64<MODE>(&w1x_lds[net][16 * ub + j][0], cells + 16 * (4 * g + i));
                 mx = (ad > 0.0 && ad < 6.0) ? (mx | (1u << bit)) : (mx & ~(1u << bit));
             }
+            uint32_t near = 0, posb = 0, chg = 0;   // per row i: near / exact logit decisions (bit 4i + k) / changed
+            const bool have_z = cur_near != 0;      // wave-uniform: the hot pass saw a logit near its boundary
+            if (have_z) {
+                layer2_lds();
+                near = group_rows(near_ballot());
+            }
 #pragma unroll
             for (int i = 0; i < 4; i++) {
-                if (!__builtin_amdgcn_ballot_w64((((edge >> i) & 0x1111u) | ((edge >> (16 + i)) & 0x1111u) | ((near >> i) & 1u)) != 0))
-                    continue;
-                const int ri = 4 * g + i;
-                const float4 z4 = *reinterpret_cast<const float4 *>(bw + kTZr + 4 * ri);
-                const float4 m4 = *reinterpret_cast<const float4 *>(bw + kTDz + 4 * ri);
-                const float4 u4 = *reinterpret_cast<const float4 *>(bw + kTDu + 4 * ri);
-                const float zr[4] = {z4.x, z4.y, z4.z, z4.w}, dzm[4] = {m4.x, m4.y, m4.z, m4.w},
-                            dzu[4] = {u4.x, u4.y, u4.z, u4.w};
-                const float dv = __uint_as_float(bw[kTDv + ri]);
-                float pos[4];   // exact logits' ReLU decisions (1 / 0)
-#pragma unroll
-                for (int k = 0; k < 4; k++)
-                    pos[k] = zr[k] > 0.0f ? 1.0f : 0.0f;
-                if ((near >> i) & 1u) {   // the group's lanes together (DPP sums within the group)
+                bool changed = (((mx ^ mask) >> i) & 0x11111111u) != 0;
+                if (__builtin_amdgcn_ballot_w64((near >> i) & 1u)) {   // the group's lanes together (DPP sums)
+                    const int ri = 4 * g + i;
+                    const float4 z4 = *reinterpret_cast<const float4 *>(bw + kTZr + 4 * ri);
+                    const float zr[4] = {z4.x, z4.y, z4.z, z4.w};
                     const uint8_t *rc = cells + 16 * ri;
                     double pk[4] = {0.0, 0.0, 0.0, 0.0};
                     for (int ub = 0; ub < 4; ub++) {
@@ -620,35 +717,56 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
                             pk[k] = __builtin_fma((double)w1_lds[lane][40 + 4 * ub + k], h, pk[k]);
                     }
 #pragma unroll
-                    for (int k = 0; k < 4; k++)
-                        pos[k] = (double)b2[k] + row_sum16_d(pk[k]) > 0.0 ? 1.0f : 0.0f;
+                    for (int k = 0; k < 4; k++) {
+                        const bool pos = (double)b2[k] + row_sum16_d(pk[k]) > 0.0;
+                        posb |= pos ? 1u << (4 * i + k) : 0u;
+                        changed |= ((near >> i) & 1u) && pos != (zr[k] > 0.0f);
+                    }
                 }
-                // nothing to correct where every exact decision equals the hot path's (nearly always:
-                // the bounds flag ~7 % of the tiles, ~1e-3 of the flagged decisions flip)
-                bool changed = (((mx ^ mask) >> i) & 0x11111111u) != 0;
+                chg |= changed ? 1u << i : 0u;
+            }
+            // nothing to correct where every exact decision equals the hot path's (nearly always:
+            // the bounds flag ~7 % of the tiles, ~1e-3 of the flagged decisions flip)
+            if (__builtin_amdgcn_ballot_w64(chg != 0)) {
+                if (!have_z)
+                    layer2_lds();
+                loss_lds();
 #pragma unroll
-                for (int k = 0; k < 4; k++)
-                    changed |= (pos[k] != 0.0f) != (zr[k] > 0.0f);
-                if (!__builtin_amdgcn_ballot_w64(changed))
-                    continue;
-                // the hot path's terms with its decisions, then the exact ones: backward(exact) -
-                // backward(hot) is linear in dz and dv, so run the difference on each mask set
-                float ndz[4][4] = {}, pdz[4][4] = {}, dv4[4] = {};
+                for (int i = 0; i < 4; i++) {
+                    if (!__builtin_amdgcn_ballot_w64((chg >> i) & 1u))
+                        continue;
+                    const bool changed = (chg >> i) & 1u;
+                    const int ri = 4 * g + i;
+                    const float4 z4 = *reinterpret_cast<const float4 *>(bw + kTZr + 4 * ri);
+                    const float4 m4 = *reinterpret_cast<const float4 *>(bw + kTDz + 4 * ri);
+                    const float4 u4 = *reinterpret_cast<const float4 *>(bw + kTDu + 4 * ri);
+                    const float zr[4] = {z4.x, z4.y, z4.z, z4.w}, dzm[4] = {m4.x, m4.y, m4.z, m4.w},
+                                dzu[4] = {u4.x, u4.y, u4.z, u4.w};
+                    const float dv = __uint_as_float(bw[kTDv + ri]);
+                    // the hot path's terms with its decisions, then the exact ones: backward(exact) -
+                    // backward(hot) is linear in dz and dv, so run the difference on each mask set. A
+                    // lane whose row and units kept every decision adds exact zeros (its two terms
+                    // would cancel only up to rounding)
+                    float ndz[4][4] = {}, pdz[4][4] = {}, dv4[4] = {}, ndv4[4] = {};
 #pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    ndz[i][k] = -dzm[k];
-                    pdz[i][k] = pos[k] != 0.0f ? dzu[k] : 0.0f;
+                    for (int k = 0; k < 4; k++) {
+                        const bool pos = (near >> i) & 1u ? ((posb >> (4 * i + k)) & 1u) != 0 : zr[k] > 0.0f;
+                        ndz[i][k] = changed ? -dzm[k] : 0.0f;
+                        pdz[i][k] = changed && pos ? dzu[k] : 0.0f;
+                    }
+                    dv4[i] = changed ? dv : 0.0f;
+                    ndv4[i] = changed ? -dv : 0.0f;
+                    rows_backward(ndz, ndv4, 1u << i, true, mask, true);
+                    rows_backward(pdz, dv4, 1u << i, true, mx, true);
                 }
-                dv4[i] = dv;
-                float ndv4[4] = {};
-                ndv4[i] = -dv;
-                rows_backward(ndz, ndv4, 1u << i, true, mask, true);
-                rows_backward(pdz, dv4, 1u << i, true, mx, true);
             }
         }
+        tile = FIX ? tnext : tile + stride;
     }
+    if (!FIX && lane == 0)
+        list_len[qw] = n_flag;
     // ---------------- this wave's record (FlatParams order)
-    float *rec = partials + ((int64_t)blockIdx.x * kTrainWaves + wave) * kRec;
+    float *rec = partials + qw * kRec;
 #pragma unroll
     for (int ub = 0; ub < 4; ub++) {
         const int u = 16 * ub + j;
@@ -744,11 +862,18 @@ int launched(const char *what)
 
 extern "C" {
 
-/* workspace floats of r48_mlp_train_grad: the per-wave records + the first reduction pass's groups */
-int64_t r48_mlp_train_workspace_floats(void)
+/* workspace of r48_mlp_train_grad over `rows` training rows (4-byte words): the per-wave records of
+ * both passes, the first reduction pass's groups, then the flag lists (one slot per tile of a wave)
+ * and their lengths */
+constexpr int64_t kTrainRecs = (int64_t)kTrainGroups * kTrainWaves;
+constexpr int64_t kRecFloats = (2 * kTrainRecs + (2 * kTrainRecs + kRedGroup - 1) / kRedGroup) * kRec;
+static int64_t list_cap(int64_t rows) { return std::max<int64_t>(1, ((rows + 15) / 16 + kTrainRecs - 1) / kTrainRecs); }
+
+int64_t r48_mlp_train_workspace_floats(int64_t rows)
 {
-    const int64_t recs = (int64_t)kTrainGroups * kTrainWaves;
-    return (recs + (recs + kRedGroup - 1) / kRedGroup) * kRec;
+    if (rows < 1)
+        return fail(R48_EINVAL, "r48_mlp_train_workspace_floats: rows < 1");
+    return kRecFloats + 2 * kTrainRecs * list_cap(rows) + kTrainRecs;
 }
 
 int r48_mlp_train_grad(const int8_t *boards, int64_t rows, int64_t n_boards, const int8_t *actions,
@@ -761,16 +886,25 @@ int r48_mlp_train_grad(const int8_t *boards, int64_t rows, int64_t n_boards, con
     if ((reinterpret_cast<uintptr_t>(boards) | reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(counts) |
          reinterpret_cast<uintptr_t>(workspace) | reinterpret_cast<uintptr_t>(grad)) & 15u)
         return fail(R48_EINVAL, "r48_mlp_train_grad: boards, w, counts, workspace and grad must be 16-byte aligned");
-    const int n_rec = kTrainGroups * kTrainWaves, n_grp = (n_rec + kRedGroup - 1) / kRedGroup;
+    const int n_rec = 2 * kTrainRecs, n_grp = (n_rec + kRedGroup - 1) / kRedGroup;
+    const int64_t cap = list_cap(rows);
+    int32_t *list = reinterpret_cast<int32_t *>(workspace + kRecFloats);
+    int32_t *list_len = list + 2 * kTrainRecs * cap;
     hipStream_t s = (hipStream_t)stream;
-    auto go = [&](auto kern) {
-        hipLaunchKernelGGL(kern, dim3(kTrainGroups), dim3(64 * kTrainWaves), 0, s, boards, rows, n_boards, actions,
-                           targets, wn, cm, counts, beta, w, workspace);
+    // hot pass (records 0 .. kTrainRecs - 1, the flag lists), then the fix pass over the lists (records
+    // kTrainRecs ..): one stream, so the fix pass sees the hot pass's lists
+    auto go = [&](auto hot, auto fix) {
+        hipLaunchKernelGGL(hot, dim3(kTrainGroups), dim3(64 * kTrainWaves), 0, s, boards, rows, n_boards, actions,
+                           targets, wn, cm, counts, beta, w, workspace, list, list_len, cap);
+        hipLaunchKernelGGL(fix, dim3(kTrainGroups), dim3(64 * kTrainWaves), 0, s, boards, rows, n_boards, actions,
+                           targets, wn, cm, counts, beta, w, workspace + kTrainRecs * kRec, list, list_len, cap);
     };
     if (mode == R48_FEAT_VALUES)
-        cm ? go(k_mlp_train<R48_FEAT_VALUES, true>) : go(k_mlp_train<R48_FEAT_VALUES, false>);
+        cm ? go(k_mlp_train<R48_FEAT_VALUES, true, false>, k_mlp_train<R48_FEAT_VALUES, true, true>)
+           : go(k_mlp_train<R48_FEAT_VALUES, false, false>, k_mlp_train<R48_FEAT_VALUES, false, true>);
     else
-        cm ? go(k_mlp_train<R48_FEAT_EXPONENTS, true>) : go(k_mlp_train<R48_FEAT_EXPONENTS, false>);
+        cm ? go(k_mlp_train<R48_FEAT_EXPONENTS, true, false>, k_mlp_train<R48_FEAT_EXPONENTS, true, true>)
+           : go(k_mlp_train<R48_FEAT_EXPONENTS, false, false>, k_mlp_train<R48_FEAT_EXPONENTS, false, true>);
     float4 *groups = reinterpret_cast<float4 *>(workspace + (int64_t)n_rec * kRec);
     constexpr int q = kRec / 4;
     hipLaunchKernelGGL(k_mlp_reduce1, dim3((q * n_grp + 255) / 256), dim3(256), 0, s, (const float4 *)workspace, n_rec,

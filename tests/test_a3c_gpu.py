@@ -555,13 +555,15 @@ def test_mlp_rollout_megakernel_equals_per_step_kernels(mode, n):
     assert all(np.isfinite(out[k]) for k in ("actor_loss", "critic_loss"))
 
 
+@pytest.mark.parametrize("exponents", [False, True])                      # R48_FEAT_VALUES / _EXPONENTS
 @pytest.mark.parametrize("T,n", [(1, 5), (3, 10_007), (4, 262_154)])   # one padded tile; 30,021 rows; 2^20 + 40 rows
 @pytest.mark.parametrize("mode", ["textbook", "reference"])                # (>= 32 tiles per wave)
-def test_fused_mlp_update_gradients_match_torch(mode, T, n):
+def test_fused_mlp_update_gradients_match_torch(mode, T, n, exponents):
     """r48_mlp_train_grad (fp32, one pass: forward + loss + backward, weight gradients accumulated per
     hidden unit) vs PyTorch autograd of the trainer's own loss (losses.chunk_loss) on the reference
     network in float64: per parameter tensor the max error relative to the tensor's scale is within
-    2x (+1e-5) of PyTorch's own fp32 autograd error; the losses agree to 1e-5."""
+    2x (+1e-5) of PyTorch's own fp32 autograd error; the losses agree to 1e-5. Both input encodings:
+    raw tile values (the reference's, a3c.py:139) and exponents (the textbook path)."""
     from rein48_amd.a3c import kernels as K
     from rein48_amd.a3c.fused import mlp_train_grad
     from rein48_amd.a3c.losses import chunk_loss, segment_stats
@@ -574,7 +576,7 @@ def test_fused_mlp_update_gradients_match_torch(mode, T, n):
     targets = torch.from_numpy(rng.normal(scale=2.0, size=(T, n)).astype(np.float32)).to(DEV)
     lengths = torch.from_numpy(rng.integers(1, T + 1, size=n)).to(DEV)
     mask = (torch.arange(T, device=DEV)[:, None] < lengths[None, :])
-    x = K.board_features(boards.view(-1, 16), exponents=False)
+    x = K.board_features(boards.view(-1, 16), exponents=exponents)
     with torch.no_grad():
         _, v = net(x)
     stats = segment_stats(v.view(T, n), targets, actions, mask)
@@ -599,7 +601,8 @@ def test_fused_mlp_update_gradients_match_torch(mode, T, n):
         cm = ((stats["td_sum"] / (4.0 * stats["B"] ** 2))[None, :] * m / n).contiguous()
         counts = stats["counts"].float().contiguous()
     gf, af, cf = mlp_train_grad(net, boards.view(-1, 16), actions.view(-1).contiguous(), targets.view(-1).contiguous(),
-                                wn.view(-1), None if cm is None else cm.view(-1), counts, n_boards=n)
+                                wn.view(-1), None if cm is None else cm.view(-1), counts, n_boards=n,
+                                exponents=exponents)
     off = 0
     for (name, p), r64, r32 in zip(net.named_parameters(), g64, g32):
         f = gf[off:off + p.numel()].double().view_as(r64)
@@ -610,8 +613,89 @@ def test_fused_mlp_update_gradients_match_torch(mode, T, n):
     np.testing.assert_allclose([float(af), float(cf)], [a64, c64], rtol=1e-5, atol=1e-9)
     # deterministic (fixed-order reduction)
     gf2, _, _ = mlp_train_grad(net, boards.view(-1, 16), actions.view(-1).contiguous(), targets.view(-1).contiguous(),
-                               wn.view(-1), None if cm is None else cm.view(-1), counts, n_boards=n)
+                               wn.view(-1), None if cm is None else cm.view(-1), counts, n_boards=n,
+                               exponents=exponents)
     assert torch.equal(gf, gf2)
+
+
+@pytest.mark.parametrize("mode", ["textbook", "reference"])
+def test_fused_mlp_update_exact_decisions_fix_flipped_relus(mode):
+    """The exact-decision pass of r48_mlp_train_grad (the fix kernel over the hot pass's flagged
+    tiles) on a network built so that fp32 decides two ReLUs the wrong way on every row:
+      hidden unit 5 (actor layer 1, ReLU6 at 0): weights 1 + 2^-23, -1, 3, -3 on cells 0, 1, 4, 8
+      holding 2^3, 2^3, 2^17, 2^17 (three MFMA k-steps) -- fp32 loses the 2^-20 against 3 * 2^17 and
+      gets exactly 0 (inactive), the exact pre-activation is 2^-20 (active);
+      logit 0 (the logits' ReLU at 0): units 0, 16, 32 saturate at 6 and W2[0] holds (2^24, 2^-24,
+      -2^24) on them in the lane's chain order -- fp32 gets 0, exactly 6 * 2^-24 > 0.
+    (The exact values are tiny, so the fp32 value error they leave is far below the tolerance; the
+    flipped decisions are not.)
+    The fused gradient must equal the float64 autograd gradient (which decides both exactly) to 1e-5
+    of each tensor's scale, while the same net with the two tiny terms removed (what fp32 decided)
+    has a gradient far from it -- so the test fails if the flips are not corrected."""
+    from rein48_amd.a3c import kernels as K
+    from rein48_amd.a3c.fused import mlp_train_grad
+    from rein48_amd.a3c.losses import chunk_loss, segment_stats
+    import torch.nn.functional as F
+
+    def build(tiny):
+        net = _mlp_net(5)
+        with torch.no_grad():
+            net.a1.weight[5].zero_()
+            net.a1.weight[5, :4] = torch.tensor([1.0 + 2.0 ** -23 if tiny else 1.0, -1.0, 0.0, 0.0])
+            net.a1.weight[5, 4], net.a1.weight[5, 8] = 3.0, -3.0
+            net.a1.bias[5] = 0.0
+            for u in (0, 16, 32):
+                net.a1.weight[u].zero_()
+                net.a1.bias[u] = 100.0
+            net.a2.weight[0].zero_()
+            net.a2.weight[0, 0], net.a2.weight[0, 16], net.a2.weight[0, 32] = 2.0 ** 24, 2.0 ** -24 if tiny else 0.0, -2.0 ** 24
+            net.a2.bias[0] = 0.0
+        return net
+
+    T, n = 1, 4099
+    rng = np.random.default_rng(21)
+    b = rng.integers(0, 6, size=(T, n, 16)).astype(np.int8)
+    b[..., [0, 1]] = 3                        # unit 5's inputs: 2^3, 2^3, 2^17, 2^17
+    b[..., [4, 8]] = 17
+    boards = torch.from_numpy(b).to(DEV)
+    actions = torch.from_numpy(rng.integers(0, 4, size=(T, n)).astype(np.int8)).to(DEV)
+    targets = torch.from_numpy(rng.normal(scale=2.0, size=(T, n)).astype(np.float32)).to(DEV)
+    mask = torch.ones((T, n), dtype=torch.bool, device=DEV)
+    x = K.board_features(boards.view(-1, 16), exponents=False)
+    net = build(True)
+    with torch.no_grad():
+        _, v = net(x)
+    stats = segment_stats(v.view(T, n), targets, actions, mask)
+
+    def grads64(m):
+        m = copy.deepcopy(m).double()
+        xd = x.double()
+        lg = F.relu(F.linear(F.relu6(F.linear(xd, m.a1.weight, m.a1.bias)), m.a2.weight, m.a2.bias))
+        val = F.linear(F.relu6(F.linear(xd, m.c1.weight, m.c1.bias)), m.c2.weight, m.c2.bias)[:, 0]
+        st = {k: (t.double() if t.is_floating_point() else t) for k, t in stats.items()}
+        a, c = chunk_loss(lg.view(T, n, 4), val.view(T, n), actions, targets.double(), mask, st, mode=mode)
+        (a + c).backward()
+        return [p.grad.detach() for p in m.parameters()], lg
+
+    g64, lg64 = grads64(net)
+    assert bool((lg64[:, 0] > 0).all())                                  # exactly: logit 0 active
+    gwrong, _ = grads64(build(False))                                    # fp32's decisions
+    wn = (mask.float() / stats["B"][None, :] / n).contiguous()
+    cm = counts = None
+    if mode == "reference":
+        cm = ((stats["td_sum"] / (4.0 * stats["B"] ** 2))[None, :] * mask.float() / n).contiguous()
+        counts = stats["counts"].float().contiguous()
+    gf, _, _ = mlp_train_grad(net, boards.view(-1, 16), actions.view(-1).contiguous(), targets.view(-1).contiguous(),
+                              wn.view(-1), None if cm is None else cm.view(-1), counts, n_boards=n)
+    off, far = 0, []
+    for (name, p), r64, rw in zip(net.named_parameters(), g64, gwrong):
+        f = gf[off:off + p.numel()].double().view_as(r64)
+        off += p.numel()
+        scale = float(r64.abs().max()) + 1e-30
+        e_f = float((f - r64).abs().max()) / scale
+        far.append(float((rw - r64).abs().max()) / scale)
+        assert e_f <= 1e-5, (name, e_f)
+    assert max(far[0], far[1]) > 1e-2 and max(far[2], far[3]) > 1e-2, far   # a1 and a2 both moved by the flips
 
 
 @pytest.mark.parametrize("mode", ["textbook", "reference"])

@@ -25,7 +25,7 @@ def counting_grad(net, boards, actions, targets, wn, cm=None, counts=None, beta=
     dev = boards.device
     rows = boards.numel() // 16
     w = fused.pack_mlp(net) if w is None else w
-    ws = torch.empty(int(L.r48_mlp_train_workspace_floats()), dtype=torch.float32, device=dev)
+    ws = torch.empty(int(L.r48_mlp_train_workspace_floats(rows)), dtype=torch.float32, device=dev)
     out = torch.zeros(2512, dtype=torch.float32, device=dev)
     p = lambda t: C.c_void_p(0 if t is None else t.data_ptr())
     rc = L.r48_mlp_train_grad(p(boards), rows, int(n_boards or rows), p(actions), p(targets), p(wn), p(cm), p(counts),

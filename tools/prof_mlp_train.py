@@ -23,7 +23,7 @@ wn = torch.full((rows,), 1.0 / rows, device=dev)
 torch.manual_seed(0)
 net = ActorCriticMLP().to(dev)
 w = pack_mlp(net)
-ws = torch.empty(int(_lib.load().r48_mlp_train_workspace_floats()), dtype=torch.float32, device=dev)
+ws = torch.empty(int(_lib.load().r48_mlp_train_workspace_floats(rows)), dtype=torch.float32, device=dev)
 for _ in range(iters + 1):
     mlp_train_grad(net, boards, actions, targets, wn, beta=0.01, exponents=True, n_boards=1 << 20, w=w, workspace=ws)
 torch.cuda.synchronize()
