@@ -23,9 +23,10 @@ Extra objects on the JSON line:
                 profiles/<round>/pmc_k_step_n.json together with the hash of the kernel sources it
                 was made from) x board-steps / the SAME wall time as `value` -> frac; frac_device
                 uses the HIP-event dispatch time of the same region instead; peak = one issue cycle
-                per SIMD per clock (1024 SIMDs x 2.4 GHz). `hbm_def` prices the same rate at
-                SURVEY.md 8(d)'s 34 B per board-step against 8 TB/s (k_step_n makes no per-step HBM
-                round trip, so that fraction may exceed 1). If the committed profile's source hash
+                per SIMD per clock (1024 SIMDs x 2.4 GHz). `hbm_def` expresses the same rate in GB/s
+                at SURVEY.md 8(d)'s 34 B per board-step -- not a roofline fraction: k_step_n makes
+                no per-step HBM round trip; the HBM roofline point is hbm.k_step_2p26 below. If the
+                committed profile's source hash
                 differs from the tree's, the profile-derived fields are null and `profile_stale`
                 says so. `valu_instr_rate` gives the plain instruction-rate fraction.
                 `hbm` holds the single-step kernel k_step (boards through HBM every step, 34
@@ -260,9 +261,11 @@ def roofline_step_n(n, wall_s, dev_ms, steps):
     pmc_k_step_n.json, made by tools/make_profiles.py from build/r48_env.s and the instruction-rate
     table); peak = one issue cycle per SIMD per clock (1024 SIMDs x 2.4 GHz). frac uses the same
     wall time as `value`, frac_device the HIP-event dispatch time of the region, frac_trace the
-    committed kernel trace of the driver's command. hbm_def: the same board-step rate at 34 B per
-    board-step against 8 TB/s. Profile-derived fields are null when the profile
-    was made from other kernel sources than the tree's (profile_stale)."""
+    committed kernel trace of the driver's command. hbm_def: the same board-step rate expressed as
+    GB/s at 34 B per board-step -- an equivalent rate, not a roofline fraction (the
+    HBM roofline point is the single-step kernel at 2^26 boards, roofline.hbm.k_step_2p26).
+    Profile-derived fields are null when the profile was made from other kernel sources than the
+    tree's (profile_stale)."""
     prof = _load_profile("pmc_k_step_n.json")
     trace = _load_profile("roofline_from_trace.json")
     sha = env_source_sha16()
@@ -270,10 +273,11 @@ def roofline_step_n(n, wall_s, dev_ms, steps):
     bsteps = n * steps
     rate_wall = bsteps / wall_s
     rate_dev = bsteps / (dev_ms * 1e-3)
-    hbm = {"bytes_per_board_step": ALGO_BYTES, "achieved": rate_wall * ALGO_BYTES / 1e9, "peak": HBM_PEAK_GBS,
-           "unit": "GB/s", "frac": rate_wall * ALGO_BYTES / 1e9 / HBM_PEAK_GBS,
-           "note": "SURVEY.md 8(d)'s 34 B per board-step priced at the wall rate of `value`; k_step_n reads and "
-                   "writes each board once per call (no per-step HBM round trip), so this may exceed 1"}
+    hbm = {"bytes_per_board_step": ALGO_BYTES, "equivalent_gbs": rate_wall * ALGO_BYTES / 1e9,
+           "note": "SURVEY.md 8(d)'s 34 B per board-step priced at the wall rate of `value`: NOT a fraction of the HBM "
+                   "roofline -- k_step_n reads and writes each board once per call (no per-step HBM round trip), so "
+                   "the kernel is VALU-bound, not HBM-bound. The HBM roofline point is roofline.hbm.k_step_2p26 "
+                   "(one step per launch through HBM, 2^26 boards past the Infinity Cache)"}
     out = {"bound": "valu", "unit": "G VALU issue-cycles/s", "peak": VALU_ISSUE_PEAK_G,
            "achieved": None, "frac": None, "frac_device": None, "achieved_is": "modelled",
            "hbm_def": hbm, "board_steps_timed": bsteps, "wall_ms_timed": wall_s * 1e3, "device_ms_timed": dev_ms,

@@ -803,3 +803,44 @@ def test_resnet_train_step_bn_fold_is_bit_identical(B):
     for k, (u, v) in enumerate(zip(sa, sb)):
         assert torch.equal(u, v), ("running stats", k)
     assert torch.equal(ga, gb)
+
+
+def test_dqn_trainer_at_the_config5_per_gpu_slice():
+    """DQNTrainer at the bench's per-GPU slice of BASELINE config 5 (16M boards over 8 GPUs): 2^21
+    boards acting, a 2^25-slot HBM ring, 64K-board minibatches, for three train steps.
+      - acting: one fused launch over all 2^21 boards (the trainer's act) equals 2^18-board chunks
+        keyed by their global board ids (Q bit-identical, epsilon-greedy actions identical);
+      - the ring: sampled transitions are consistent with the oracle move (a not-done row's
+        next_state is the moved state plus at most one spawned 2/4 in an empty cell; a done row's
+        next_state is a reset board: exactly one tile, 2 or 4), actions in 0..3;
+      - the updates' losses and the flat parameters stay finite."""
+    from rein48_amd.dqn import DQNConfig, DQNTrainer
+    from rein48_amd.dqn.fused import resnet_q_forward
+    n, cap, B = 1 << 21, 1 << 25, 1 << 16
+    tr = DQNTrainer(DQNConfig(n_boards=n, replay_capacity=cap, batch=B, learn_start=B, seed=7), device=DEV)
+    assert tr.use_fused
+    losses = [tr.train_step()["loss"] for _ in range(3)]
+    assert len(tr.replay) == 3 * n and all(np.isfinite(losses)), losses
+    assert bool(torch.isfinite(tr.flat.data).all())
+    # acting: one launch == 2^18-board chunks (same Philox keys: global board id, step counter)
+    blob = tr.packed(tr.net)
+    eps, ctr = 0.3, 11
+    q1, a1 = resnet_q_forward(tr.env.boards, blob, q=True, actions=True, eps=eps, seed=5, ctr=ctr, gid0=0)
+    for s in range(0, n, 1 << 18):
+        qc, ac = resnet_q_forward(tr.env.boards[s:s + (1 << 18)].contiguous(), blob, q=True, actions=True, eps=eps,
+                                  seed=5, ctr=ctr, gid0=s)
+        assert torch.equal(qc, q1[s:s + (1 << 18)]) and torch.equal(ac, a1[s:s + (1 << 18)]), s
+    # the ring's rows: oracle move of (state, action) vs next_state
+    out = tr.replay.sample(1 << 16)
+    st, a, s2, d = (out[k][:6000].cpu().numpy() for k in ("state", "action", "next_state", "done"))
+    assert ((a >= 0) & (a < 4)).all()
+    for i in range(st.shape[0]):
+        if d[i]:
+            nz = s2[i][s2[i] != 0]
+            assert nz.size == 1 and nz[0] in (1, 2), (i, s2[i])
+            continue
+        moved = O.move(st[i], int(a[i]))[0]
+        diff = moved != s2[i]
+        assert diff.sum() <= 1, i
+        if diff.any():
+            assert moved[diff][0] == 0 and s2[i][diff][0] in (1, 2), i

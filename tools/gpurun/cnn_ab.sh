@@ -5,7 +5,7 @@
 set -o pipefail
 O=gpurun_out/$1; shift; mkdir -p $O
 R48_LIB=$1 timeout -k 10 600 python -u -m pytest tests/test_a3c_gpu.py -m gpu -x -q --timeout 300 --timeout-method thread -k "rollout or fused_cnn or trainer_fused_update" > $O/pytest.log 2>&1; rc=$?; tail -1 $O/pytest.log; [ $rc -eq 0 ] || exit $rc
-for i in 1 2; do for L in "$@"; do
+for i in $(seq ${N:-2}); do for L in "$@"; do
 R48_LIB=$L timeout -k 10 300 python -u -c "
 import os, torch, bench
 d = torch.device('cuda', 0)

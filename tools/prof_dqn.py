@@ -14,7 +14,9 @@ from rein48_amd.dqn import DQNConfig, DQNTrainer  # noqa: E402
 
 if __name__ == "__main__":
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 5
-    cfg = DQNConfig(n_boards=1 << 18, replay_capacity=1 << 22, batch=1 << 16, learn_start=1, seed=0)
+    what = sys.argv[2] if len(sys.argv) > 2 else "update"     # "update" | "act" (2^21 boards, bench slice)
+    boards = 1 << 21 if what == "act" else 1 << 18
+    cfg = DQNConfig(n_boards=boards, replay_capacity=1 << 22, batch=1 << 16, learn_start=1, seed=0)
     tr = DQNTrainer(cfg, device="cuda:0")
     for _ in range(3):
         tr.train_step()
@@ -22,7 +24,7 @@ if __name__ == "__main__":
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     ev[0].record()
     for _ in range(n):
-        tr.update()
+        tr.update() if what == "update" else tr.act()
     ev[1].record()
     torch.cuda.synchronize()
-    print("update ms", ev[0].elapsed_time(ev[1]) / n, "updates", n, flush=True)
+    print(what, "ms", ev[0].elapsed_time(ev[1]) / n, what + "s", n, flush=True)

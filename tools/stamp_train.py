@@ -5,8 +5,8 @@ the cycles spent in each phase (summed over its tiles) over the first 8 words of
 Phases: 0 tile head (inputs, Xt), 1 forward, 2 loss, 3 dh2 + dWh + dh2^T + db2, 5 position loop.
 
     python tools/stamp_train.py [source.hip [out.hip]] && tools/build_variant.sh \\
-        build/var/r48_a3c_train_stamp.hip r48_a3c_train build/lib_train_stamp.so -mllvm -amdgpu-mfma-vgpr-form=1
-    python tools/exp_train_stamps.py build/lib_train_stamp.so      (on the GPU)"""
+        build/var/r48_a3c_train_stamp.hip r48_a3c_train build/ab/lib_train_stamp.so -mllvm -amdgpu-mfma-vgpr-form=1
+    python tools/exp_train_stamps.py build/ab/lib_train_stamp.so      (on the GPU)"""
 import os
 import sys
 
@@ -18,7 +18,7 @@ MARKS = [
     ("        // ---------------- forward (", 0),
     ("        // ---------------- loss gradient per row", 1),
     ("        // ---------------- dh2 = Wh^T dout", 2),
-    ("            fwd_conv2_heads_", 6),
+    ("            fwd_conv2_heads_grouped(w, bl", 6),
     ("        // ---------------- per conv1 position R", 3),
     ("        const RowIn in = next;", 5),
 ]
