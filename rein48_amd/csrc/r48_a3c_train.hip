@@ -304,84 +304,6 @@ __device__ __forceinline__ void fwd_conv2_heads_chain(const uint4 *w, const floa
     }
 }
 
-// conv2 + heads in the inference kernels' fragment-grouped order (r48_cnn_common.h
-// cnn_conv2_heads_grouped: each W2 fragment read once per tile feeds the 4 positions' independent
-// accumulators of its output half, so no conv2 MFMA waits on the previous one; 41 fragment reads
-// per tile instead of 89), with the training kernel's extras: h2 kept (the ReLU' mask) and stored
-// to the image as formed (dWh's and the mask's h2^T), and the heads in three accumulators -- half
-// 0's under half 1's conv2, half 1's per output position as its epilogue completes, s = 0 and
-// s = 1 in separate chains -- summed at the end (rows 0..4: logits and value).
-#ifndef R48_TRAIN_GROUPED
-#define R48_TRAIN_GROUPED 1
-#endif
-__device__ __forceinline__ void fwd_conv2_heads_grouped(const uint4 *w, const float *b, int lane, int h,
-                                                        const bf16x8 (&h1)[9][2], WStream &ws,
-                                                        bf16x8 (&h2)[4][2][2], f32x16 &out, uint16_t *img,
-                                                        const LaneAddr &la)
-{
-    auto next = [&](int i) { return ws.step(w, fwd_grouped_frag(i + 2 < kFwdGroupedReads ? i + 2 : 0), lane); };
-    f32x16 acc[4];
-    int i = 9;
-    {
-        const f32x16 b2 = load_bias(b + 32, h);
-#pragma unroll
-        for (int u = 0; u < 8; u++, i++) {
-            const bf16x8 wa = next(i);
-            wfence();
-#pragma unroll
-            for (int p = 0; p < 4; p++)
-                acc[p] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, h1[kP2[p][u >> 1]][u & 1], u ? acc[p] : b2, 0, 0,
-                                                                 0);
-            wfence();
-        }
-    }
-#pragma unroll
-    for (int p = 0; p < 4; p++) {
-#pragma unroll
-        for (int s = 0; s < 2; s++) {
-            h2[p][0][s] = acc_to_frag_relu(acc[p], s);
-            store_frag(img, la, 64 * p + 16 * s, h2[p][0][s]);
-        }
-    }
-    f32x16 o0 = f32x16{}, o1 = f32x16{}, o2 = f32x16{};
-    {
-        const f32x16 b2 = load_bias(b + 64, h);
-#pragma unroll
-        for (int u = 0; u < 8; u++) {
-            const bf16x8 wa = next(i++);
-            wfence();
-#pragma unroll
-            for (int p = 0; p < 4; p++)
-                acc[p] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, h1[kP2[p][u >> 1]][u & 1], u ? acc[p] : b2, 0, 0,
-                                                                 0);
-            wfence();
-            const bf16x8 wh = next(i++);
-            wfence();
-            o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, h2[u >> 1][0][u & 1], o0, 0, 0, 0);
-            wfence();
-        }
-    }
-#pragma unroll
-    for (int p = 0; p < 4; p++) {
-#pragma unroll
-        for (int s = 0; s < 2; s++) {
-            h2[p][1][s] = acc_to_frag_relu(acc[p], s);
-            store_frag(img, la, 64 * p + 32 + 16 * s, h2[p][1][s]);
-            const bf16x8 wh = next(i++);
-            wfence();
-            if (s == 0)
-                o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, h2[p][1][s], o1, 0, 0, 0);
-            else
-                o2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, h2[p][1][s], o2, 0, 0, 0);
-            wfence();
-        }
-    }
-    out = o0;
-#pragma unroll
-    for (int r = 0; r < 4; r++)   // rows 0..3 (lane half 0) and 4 (half 1, register 0): the heads
-        out[r] = (o0[r] + o1[r]) + o2[r];
-}
-
 template <int MODE>
 __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
     const int8_t *__restrict__ boards, int64_t rows, int64_t n_boards, const int8_t *__restrict__ actions,
@@ -489,15 +411,9 @@ __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
         {
             bf16x8 h1[9][2];
             WStream ws;
-#if R48_TRAIN_GROUPED
-            ws.start(w, fwd_grouped_frag(0), fwd_grouped_frag(1), lane);
-            fwd_conv1(w, bl, lane, h, x, ws, h1, fwd_grouped_frag(9), fwd_grouped_frag(10));
-            fwd_conv2_heads_grouped(w, bl, lane, h, h1, ws, h2, out, my, la);
-#else
             ws.start(w, fwd_frag(0), fwd_frag(1), lane);
             fwd_conv1(w, bl, lane, h, x, ws, h1, fwd_frag(9), fwd_frag(10));
             fwd_conv2_heads_chain(w, bl, lane, h, h1, ws, h2, out, my, la);
-#endif
         }
         // ---------------- loss gradient per row (lane half 0: logits rows 0..3; value in lane + 32)
         // the value (row 4 = lane half 1's first register) into lane half 0: v_permlane32_swap, no LDS
@@ -568,66 +484,67 @@ __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
             uint32_t pk[4] = {h == 0 ? d0 : 0u, h == 0 ? d1 : 0u, h == 0 ? d2 : 0u, 0u};
             __builtin_memcpy(&dout, pk, 16);
         }
-        // ---------------- dh2 = Wh^T dout . [h2 > 0] in BOTH orientations, straight from the MFMA:
-        //   orientation 1 (features in registers, the dh1 chain's A operand): A = Wh^T fragment m,
-        //     B = dout; masked with h2 (registers)
-        //   orientation 2 (rows in registers, dW2's and db2's A operand): the same two operands
-        //     swapped, A = dout, B = Wh^T fragment m; masked with h2^T read back transposed from the
-        //     image -- the reads dWh needs anyway -- so dh2 makes no LDS round trip
-        //   dWh[o][f] += sum over rows of h2^T[f] dout[o]  (A = h2^T, B = Dt with the column
-        //     selector; 16x16x32, 8 feature tiles x 2 row steps)
-        //   db2 += row sums of dh2^T (16x16x32 with a selector B), one block behind
-        // Per step m (= 2p + g = feature block): both dh2 MFMAs of m + 1, the two dWh MFMAs of m, the
-        // db2 MFMAs of m - 1, then the epilogues of m (bf16 pack + ReLU') -- the pipe runs under
-        // every epilogue.
+        // ---------------- dh2 = Wh^T dout . [h2 > 0] (orientation 1; h2 dies here), and under it:
+        //   dWh[o][f] += sum over rows of h2^T[f] dout[o]  (A = h2^T read back transposed from the
+        //     image, B = Dt with the column selector; 16x16x32, 8 feature tiles x 2 row steps)
+        //   the dh2 image, block m written over h2 block m once its last dWh read is issued (one
+        //     wave's LDS operations execute in order), then read back transposed: dh2^T (AGPRs)
+        //   db2 += row sums of dh2^T (16x16x32 with a selector B), two blocks behind
+        // Per step m (= 2p + g = feature block): dh2 MFMA m + 1, two dWh MFMAs (their h2^T operands
+        // read two MFMAs ahead), two db2 MFMAs, then the epilogue of m (bf16 pack + ReLU') -- the
+        // pipe runs under every epilogue.
         bf16x8 dh2[4][2][2];
         bf16x8 dh2t[4][2][2];
         {
             const bf16x8 sel0 = splat_frag(n16 == (g16 & 1) ? one2 : 0u);
             const bf16x8 sel1 = splat_frag(n16 == 2 + (g16 & 1) ? one2 : 0u);
             const bf16x8 bd0 = lds_frag(my + la.dr), bd1 = lds_frag(my + la.dr + 16);
-            bf16x8 A[2] = {trr(my, la, 0, 0), trr(my, la, 0, 1)};
-            bf16x8 wq = frag_at(w, kOffWhT, lane);
-            f32x16 acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wq, dout, zero, 0, 0, 0);
-            f32x16 acc2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(dout, wq, zero, 0, 0, 0);
-            wq = frag_at(w, kOffWhT + 1, lane);
+            bf16x8 A = trr(my, la, 0, 0), A1 = trr(my, la, 0, 1);
+            f32x16 acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_at(w, kOffWhT, lane), dout, zero, 0, 0, 0);
+            bf16x8 q = frag_at(w, kOffWhT + 1, lane);
 #pragma unroll
-            for (int m = 0; m <= 8; m++) {              // m = 2p + g = the feature block
-                f32x16 nxt1 = acc1, nxt2 = acc2;
-                bf16x8 An[2] = {A[0], A[1]};
+            for (int m = 0; m <= 9; m++) {              // m = 2p + g = the feature block
+                f32x16 nxt = acc;
                 if (m + 1 < 8) {
-                    const bf16x8 wa = wq;
+                    const bf16x8 wa = q;
                     if (m + 2 < 8)
-                        wq = frag_at(w, kOffWhT + m + 2, lane);
-                    An[0] = trr(my, la, m + 1, 0);
-                    An[1] = trr(my, la, m + 1, 1);
+                        q = frag_at(w, kOffWhT + m + 2, lane);
                     wfence();
-                    nxt1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, dout, zero, 0, 0, 0);
-                    nxt2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(dout, wa, zero, 0, 0, 0);
+                    nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, dout, zero, 0, 0, 0);
                 }
                 if (m < 8) {
-                    acc16_lds(dwh[m], A[0], bd0);
-                    acc16_lds(dwh[m], A[1], bd1);
-                }
-                if (m >= 1) {                           // db2 of block m - 1 (its epilogue ran at step m - 1)
-                    const int b = m - 1;
 #pragma unroll
-                    for (int s = 0; s < 2; s++)   // (the block's epilogue has just written its operands)
-                        acc16_av(db2, dh2t[b >> 1][b & 1][s], (b & 1) ? sel1 : sel0);
+                    for (int k = 2 * m; k < 2 * m + 2; k++) {
+                        const bf16x8 An = k + 2 < 16 ? trr(my, la, (k + 2) >> 1, (k + 2) & 1) : A;
+                        acc16_lds(dwh[m], A, (k & 1) ? bd1 : bd0);
+                        A = A1;
+                        A1 = An;
+                    }
+                }
+                if (m >= 2) {                           // db2 of block m - 2 (read at step m - 2)
+                    const int b = m - 2;
+#pragma unroll
+                    for (int s = 0; s < 2; s++) {
+                        if (b == 0 && s == 0)
+                            acc16_av(db2, dh2t[b >> 1][b & 1][s], sel0);
+                        else if (b == 1 && s == 0)
+                            acc16_av(db2, dh2t[b >> 1][b & 1][s], sel1);
+                        else
+                            acc16_a(db2, dh2t[b >> 1][b & 1][s], (b & 1) ? sel1 : sel0);
+                    }
                 }
                 __builtin_amdgcn_sched_barrier(0);
                 if (m < 8) {
                     const int p = m >> 1, g = m & 1;
-                    dh2[p][g][0] = mask_pk(acc_to_frag(acc1, 0), h2[p][g][0]);
-                    dh2[p][g][1] = mask_pk(acc_to_frag(acc1, 1), h2[p][g][1]);
-                    dh2t[p][g][0] = mask_pk(acc_to_frag(acc2, 0), A[0]);
-                    dh2t[p][g][1] = mask_pk(acc_to_frag(acc2, 1), A[1]);
+                    dh2[p][g][0] = mask_pk(acc_to_frag(acc, 0), h2[p][g][0]);
+                    dh2[p][g][1] = mask_pk(acc_to_frag(acc, 1), h2[p][g][1]);
+                    store_frag(my, la, 64 * p + 32 * g, dh2[p][g][0]);
+                    store_frag(my, la, 64 * p + 32 * g + 16, dh2[p][g][1]);
+                    dh2t[p][g][0] = trr(my, la, m, 0);
+                    dh2t[p][g][1] = trr(my, la, m, 1);
                     __builtin_amdgcn_sched_barrier(0);
                 }
-                acc1 = nxt1;
-                acc2 = nxt2;
-                A[0] = An[0];
-                A[1] = An[1];
+                acc = nxt;
             }
         }
         // ---------------- per conv1 position R: h1^T_R, dh1^T_R, dW2, dW1. Software-pipelined: the

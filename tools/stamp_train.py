@@ -18,7 +18,7 @@ MARKS = [
     ("        // ---------------- forward (", 0),
     ("        // ---------------- loss gradient per row", 1),
     ("        // ---------------- dh2 = Wh^T dout", 2),
-    ("            fwd_conv2_heads_grouped(w, bl", 6),
+    ("            fwd_conv2_heads_", 6),
     ("        // ---------------- per conv1 position R", 3),
     ("        const RowIn in = next;", 5),
 ]
@@ -35,6 +35,8 @@ def main():
     assert loop in s
     s = s.replace(loop, "    unsigned long long st_acc[8] = {}, st_last = __builtin_amdgcn_s_memtime();\n" + loop, 1)
     for mark, k in MARKS:
+        if s.count(mark) > 1:   # a source with #if alternatives of the call: stamp the first
+            mark = mark + s.split(mark, 2)[1].split("(", 1)[0] + "("
         assert s.count(mark) == 1, mark
         s = s.replace(mark, "        R48_STAMP(%d)\n%s" % (k, mark), 1)
     end = "        rec[kOffLoss + 1] = red[6];\n    }\n"
