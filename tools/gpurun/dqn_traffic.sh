@@ -6,4 +6,4 @@ export TMPDIR=/tmp
 O=${1:-gpurun_out/dqn_traffic}; mkdir -p $O
 timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch -o pmc -- python3 tools/prof_dqn.py 2 > $O/fetch.log 2>&1 \
 && timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write -o pmc -- python3 tools/prof_dqn.py 2 > $O/write.log 2>&1 \
-&& python3 tools/dqn_traffic.py $O 2 | tee $O/traffic.txt
+&& python3 tools/dqn_traffic.py $O 3 | tee $O/traffic.txt
