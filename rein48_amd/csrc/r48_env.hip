@@ -25,7 +25,10 @@ using r48::Board;
 namespace {
 
 constexpr int kBlock = 256;
-constexpr int kStepNP = 1;   // board pairs per lane in k_step_n
+#ifndef R48_STEPN_NP
+#define R48_STEPN_NP 1
+#endif
+constexpr int kStepNP = R48_STEPN_NP;   // board pairs per lane in k_step_n (A/B builds: -DR48_STEPN_NP=2)
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -324,7 +327,7 @@ template <bool RANDOM, bool AUTO_RESET, bool REWARD, int NP, bool TRAJ = false>
 // The read-ahead below needs ~62 VGPRs; waves_per_eu(8) holds the allocator to the 64 that keep the
 // 8 waves per SIMD the VALU issue bound needs. The merge-reward variants need more than 64 (they
 // spilled 28-48 B per lane to scratch under the cap), so they keep the plain launch bounds.
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(REWARD ? 1 : 8, 8))) void k_step_n(int8_t *boards, int64_t n, int64_t gid0, uint32_t k0, uint32_t k1,
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(REWARD ? 1 : 8 / NP, 8 / NP))) void k_step_n(int8_t *boards, int64_t n, int64_t gid0, uint32_t k0, uint32_t k1,
                                                    uint32_t step0, int32_t n_steps, int8_t *__restrict__ actions,
                                                    uint8_t *__restrict__ done, uint8_t *__restrict__ changed,
                                                    int32_t *__restrict__ reward, int32_t *__restrict__ score,
