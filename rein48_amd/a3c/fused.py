@@ -83,13 +83,13 @@ def pack_cnn(net):
 
 
 @torch.no_grad()
-def pack_cnn_train(net):
+def pack_cnn_train(net, fwd=None):
     """-> (wfrag bf16 [65, 64, 8], bias f32 [104]): pack_cnn's 41 forward fragments followed by
-    the 8 Wh^T and 16 W2^T fragments of the fused update."""
+    the 8 Wh^T and 16 W2^T fragments of the fused update. fwd: pack_cnn(net) if already made."""
     global _MAPS_BWD
     if _MAPS_BWD is None:
         _MAPS_BWD = _index_maps_backward()
-    wfrag, bias = pack_cnn(net)
+    wfrag, bias = pack_cnn(net) if fwd is None else fwd
     dev = net.conv1.weight.device
     wht_idx, w2t_idx = _on_device("bwd", _MAPS_BWD, dev)
     hw = torch.cat([net.heads.weight.reshape(-1), torch.zeros(1, device=dev)])

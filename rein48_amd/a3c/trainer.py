@@ -75,6 +75,11 @@ class A3CTrainer:
         self.rewards = torch.zeros((T, n), dtype=torch.float32, device=self.device)
         self.sample_ctr = 0
         self.updates = 0
+        # weight epoch: rollout() starts one (the weights may have been set from outside since the
+        # last step), the optimizer step of update() ends it; the kernels' packed weight images are
+        # made once per epoch (_packed)
+        self._wepoch = 0
+        self._packs = {}
         self._rollout_v = None       # ([T + 1, n] V(boards[t]) slab of the last megakernel rollout, updates)
         self._mask = None            # [T, n] valid-step mask of the last rollout, formed on first use
         # before the first rollout every step is valid (a full-length segment for every board)
@@ -89,9 +94,26 @@ class A3CTrainer:
         return self.net(x)  # bf16 (MFMA) or fp32 compute per cfg.bf16; outputs fp32
 
     # ------------------------------------------------------------------ rollout (a3c.py:194-212)
+    def _packed(self, kind):
+        """The packed weight image `kind` ("cnn": pack_cnn, "cnn_train": pack_cnn_train, "mlp":
+        pack_mlp) of the current weights, made once per weight epoch."""
+        c = self._packs.get(kind)
+        if c is None or c[0] != self._wepoch:
+            if kind == "cnn":
+                v = pack_cnn(self.net)
+            elif kind == "cnn_train":
+                from .fused import pack_cnn_train
+                v = pack_cnn_train(self.net, fwd=self._packed("cnn"))
+            else:
+                from .fused import pack_mlp
+                v = pack_mlp(self.net, out=c[1] if c is not None else None)
+            c = self._packs[kind] = (self._wepoch, v)
+        return c[1]
+
     @torch.no_grad()
     def rollout(self):
         cfg, env = self.cfg, self.env
+        self._wepoch += 1
         env.reset()
         self._rollout_v = None
         merge = cfg.mode == "textbook"
@@ -99,7 +121,7 @@ class A3CTrainer:
             self.rewards.zero_()  # GameClient.py:138: reward is always 0
         fused = cfg.net == "cnn" and cfg.bf16 and cfg.fused_policy
         if fused:
-            wfrag, bias = pack_cnn(self.net)   # weights are fixed for the whole rollout
+            wfrag, bias = self._packed("cnn")   # weights are fixed for the whole rollout
         mlp_mega = self._mlp_fused() and cfg.fused_rollout
         mega = (fused and cfg.fused_rollout) or mlp_mega
         if merge and not mega and getattr(self, "_rewards_i32", None) is None:
@@ -173,9 +195,7 @@ class A3CTrainer:
         return cfg.net == "mlp" and not cfg.bf16 and cfg.fused_policy and self.device.type == "cuda"
 
     def _mlp_weights(self):
-        from .fused import pack_mlp
-        self._mlp_w = pack_mlp(self.net, out=getattr(self, "_mlp_w", None))
-        return self._mlp_w
+        return self._packed("mlp")
 
     def _rollout_megakernel(self, wfrag, bias, merge, mlp=False):
         """r48_cnn_rollout (or, mlp=True, r48_mlp_rollout with the reference network): the T policy
@@ -226,7 +246,7 @@ class A3CTrainer:
         fused = cfg.net == "cnn" and cfg.bf16 and cfg.fused_policy
         with torch.no_grad():
             if fused:   # values of all T*n training states in one fused MFMA launch
-                wfrag, bias = pack_cnn(self.net)
+                wfrag, bias = self._packed("cnn")
                 value = lambda b: cnn_forward(b.reshape(-1, 16), wfrag, bias, exponents=cfg.features == "exponents",
                                               logits=False, value=True)[1]
             elif self._mlp_fused():   # the reference MLP: one fp32 VALU launch (r48_mlp_policy_forward)
@@ -242,23 +262,26 @@ class A3CTrainer:
             need_values = not (fused_upd and cfg.mode == "textbook")
             v_all = None
             rv = self._rollout_v
+            v_T = None   # V(boards[T])
             if need_values and rv is not None and rv[1] == self.updates and cfg.mode == "reference":
                 # V(boards[t]) from the rollout (rows 0..T-1 of a [T + 1, n] slab); the reference
                 # states are boards[1..T], so V(boards[T]) -- never a rollout input -- takes one
                 # forward into row T and the values are the view of rows 1..T (no copy)
                 rv[0][T] = value(self.boards[T]).view(n)
                 v_all = rv[0][1:T + 1]
+                v_T = rv[0][T]
             elif need_values:
                 v_all = torch.empty((T, n), dtype=torch.float32, device=self.device)
                 ch = T if (fused or self._mlp_fused()) else cfg.update_chunk   # no activations kept
                 for t0 in range(0, T, ch):
                     t1 = min(T, t0 + ch)
                     v_all[t0:t1] = value(states[t0:t1].contiguous()).view(t1 - t0, n)
-            # last post-step state of each segment = boards[len]
-            idx = self.lengths.long().view(1, n, 1).expand(1, n, 16)
-            last = self.boards.gather(0, idx)[0].contiguous()
-            v_last = value(last)
-            boot = torch.where(self.finished, torch.zeros_like(v_last), v_last.view(n)).float().contiguous()
+            # the bootstrap V(s_last) (a3c.py:218-223) counts only for segments that did not finish,
+            # and such a segment ran all T steps: its last post-step state is boards[T] (= boards[len]
+            # for every board that needs it; no gather, and in reference mode the row-T value above)
+            if v_T is None:
+                v_T = value(self.boards[T]).view(n)
+            boot = torch.where(self.finished, torch.zeros_like(v_T), v_T).float().contiguous()
             targets = K.discounted_returns(self.rewards, self.lengths, boot, cfg.gamma,
                                            drop_last=cfg.mode == "reference")
             if self.actions.is_cuda:    # one launch (r48_a3c_segment_stats) for the masked sums + counts
@@ -270,13 +293,15 @@ class A3CTrainer:
         if fused_upd:
             # pass 2 as ONE fused kernel over all T x n states (no activation hits HBM): MFMA for the
             # CNN (r48_a3c_train.hip), fp32 MFMA + VALU for the reference MLP (r48_mlp_train.hip)
-            actor_total, critic_total = self._fused_gradient(states, targets, stats)
+            actor, critic = self._fused_gradient(states, targets, stats)
             self.flat.allreduce_grad(self.group)
             self.opt.step()
             self.updates += 1
-            return {"actor_loss": actor_total, "critic_loss": critic_total,
-                    "mean_length": float(self.lengths.float().mean()),
-                    "finished": float(self.finished.float().mean())}
+            self._wepoch += 1
+            # the reported scalars in ONE device-to-host transfer (one synchronisation)
+            a, c, ml, fin = torch.stack([actor.float(), critic.float(), self.lengths.float().mean(),
+                                         self.finished.float().mean()]).tolist()
+            return {"actor_loss": a, "critic_loss": c, "mean_length": ml, "finished": fin}
         # pass 2: chunked forward/backward, gradients accumulate in the flat buffer
         self.flat.zero_grad()
         actor_total, critic_total = 0.0, 0.0
@@ -291,6 +316,7 @@ class A3CTrainer:
         self.flat.allreduce_grad(self.group)   # RCCL across GPUs (a3c.py:79-80's push, synchronous)
         self.opt.step()                        # fused TF1 RMSProp (a3c.py:264-265)
         self.updates += 1
+        self._wepoch += 1
         return {"actor_loss": actor_total, "critic_loss": critic_total,
                 "mean_length": float(self.lengths.float().mean()),
                 "finished": float(self.finished.float().mean())}
@@ -299,7 +325,7 @@ class A3CTrainer:
         """Per-row weights of losses.chunk_loss for r48_cnn_train_grad: wn = mask / (B n) and, in
         reference mode, cm = (td_sum / (4 B^2)) mask / n with the per-segment action counts;
         the kernel's gradient lands in the flat gradient buffer (parameters() order)."""
-        from .fused import cnn_train_grad, pack_cnn_train
+        from .fused import cnn_train_grad
         cfg = self.cfg
         n = cfg.n_boards
         ref = cfg.mode == "reference"
@@ -317,18 +343,18 @@ class A3CTrainer:
                 wn.view(-1), None if cm is None else cm.view(-1), counts, beta=cfg.beta,
                 exponents=cfg.features == "exponents", n_boards=n, w=self._mlp_weights(), workspace=self._mlp_ws)
             self.flat.grad.copy_(g)
-            return float(actor), float(critic)
+            return actor, critic
         if getattr(self, "_train_ws", None) is None:
             self._train_ws = torch.empty(_lib_workspace_floats(), dtype=torch.float32, device=self.device)
         grads, actor, critic = cnn_train_grad(
             self.net, states.reshape(-1, 16), self.actions.reshape(-1), targets.reshape(-1).contiguous(),
             wn.view(-1), None if cm is None else cm.view(-1), counts, beta=cfg.beta,
-            exponents=cfg.features == "exponents", n_boards=n, packed=pack_cnn_train(self.net),
+            exponents=cfg.features == "exponents", n_boards=n, packed=self._packed("cnn_train"),
             workspace=self._train_ws)
         with torch.no_grad():
             for p, g in zip(self.net.parameters(), grads):
                 p.grad.copy_(g.view_as(p))
-        return float(actor), float(critic)
+        return actor, critic
 
     def train_step(self):
         self.rollout()

@@ -143,6 +143,7 @@ def load(trainer, path):
             _load_env(trainer.env, st["env"])
             trainer.sample_ctr = st["sample_ctr"]
             trainer._rollout_v = None            # the rollout's values belong to the old weights
+            trainer._wepoch += 1                 # repack the kernels' weight images
             trainer._mask = None
         else:
             trainer.target.load_state_dict(st["target"])
