@@ -29,10 +29,11 @@ def test_board_features_exact():
     np.testing.assert_array_equal(bf, R.board_values(b).astype(np.float32))  # powers of two are exact in bf16
 
 
-def test_sample_actions_match_choose_action():
+@pytest.mark.parametrize("ctr", [5, 0xFFFFFFFF])
+def test_sample_actions_match_choose_action(ctr):
     from rein48_amd.a3c import kernels as K
     rng = np.random.default_rng(1)
-    n, seed, ctr, gid0 = 200_000, 77, 5, 1000
+    n, seed, gid0 = 200_000, 77, 1000
     logits = rng.normal(scale=2.0, size=(n, 4)).astype(np.float32)
     act, logp, ent = K.sample_actions(torch.from_numpy(logits).to(DEV), seed, ctr, gid0=gid0, want_logp=True,
                                       want_entropy=True)
