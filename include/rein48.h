@@ -221,6 +221,17 @@ int r48_a3c_segment_stats(const float *values, const float *targets, const int8_
  * order (and fp32 reciprocal) of the tensor form in rein48_amd/a3c/trainer.py, bit-identical to it. */
 int r48_a3c_row_weights(const int32_t *lengths, const float *B, const float *td_sum, int32_t T, int64_t n, float *wn,
                         float *cm, void *stream);
+/* The update's per-board pass in one launch (the fused update's inputs without any [T][n] weight rows):
+ * targets float[T][n] exactly as r48_discounted_returns (same arguments), and per segment
+ * seg float[n][4] = {w0, c0, L, 0} (16-byte aligned; L = clamp(lengths[i], 0, T) as int32 bits) with
+ * w0 = (1 / B) (1 / n) and c0 = (td_sum / ((4 B) B)) (1 / n), B = max(L, 1) -- r48_a3c_row_weights' wn
+ * and cm at every row t < L, bit for bit given the same td_sum. counts (nullable, 16-byte aligned;
+ * the reference loss): float[n][4] action counts over t < L, as r48_a3c_segment_stats, and c0 from
+ * td_sum = sum over t < L of targets - values (values float[T][n], actions int8[T][n] needed then),
+ * summed from t = L - 1 down (the returns scan's order); without counts c0 = 0. */
+int r48_a3c_segments(const float *rewards, const float *values, const int8_t *actions, const int32_t *lengths,
+                     const float *bootstrap, int32_t T, int64_t n, float gamma, int32_t drop_last, float *targets,
+                     float *seg, float *counts, void *stream);
 
 /* tf.train.RMSPropOptimizer(lr) (a3c.py:264-265; TF1 semantics: ms slot starts at ONES, eps
  * inside the sqrt, momentum 0 by default) over one flat float32 parameter buffer of n values. */
@@ -289,6 +300,12 @@ int64_t r48_mlp_train_workspace_floats(int64_t rows);
 int r48_mlp_train_grad(const int8_t *boards, int64_t rows, int64_t n_boards, const int8_t *actions,
                        const float *targets, const float *wn, const float *cm, const float *counts, float beta,
                        int32_t mode, const float *w, float *workspace, float *grad, void *stream);
+/* The same with per-board weights: seg float[n_boards][4] of r48_a3c_segments (16-byte aligned) instead
+ * of wn / cm -- row r = t n_boards + b weighs seg[b].w0 (and seg[b].c0) when t < seg[b].L, else 0;
+ * the reference loss when counts != NULL. Equals r48_mlp_train_grad on the expanded rows bit for bit. */
+int r48_mlp_train_grad_seg(const int8_t *boards, int64_t rows, int64_t n_boards, const int8_t *actions,
+                           const float *targets, const float *seg, const float *counts, float beta, int32_t mode,
+                           const float *w, float *workspace, float *grad, void *stream);
 
 /* Fused A3C update for the CNN (configs 3-4; rein48_amd/a3c/losses.py restating a3c.py:99-123):
  * the gradient of (actor + critic) over `rows` training states w.r.t. every ActorCriticCNN
@@ -303,6 +320,11 @@ int r48_cnn_train_grad(const int8_t *boards, int64_t rows, int64_t n_boards, con
                        const float *targets, const float *wn, const float *cm, const float *counts,
                        float beta, int32_t mode, const void *wfrag, const float *bias, float *workspace,
                        float *grad, void *stream);
+/* The same with per-board weights (seg of r48_a3c_segments, as r48_mlp_train_grad_seg; n_boards < 2^31):
+ * bit for bit r48_cnn_train_grad on the expanded rows. */
+int r48_cnn_train_grad_seg(const int8_t *boards, int64_t rows, int64_t n_boards, const int8_t *actions,
+                           const float *targets, const float *seg, const float *counts, float beta, int32_t mode,
+                           const void *wfrag, const float *bias, float *workspace, float *grad, void *stream);
 int64_t r48_cnn_train_workspace_floats(void);
 int64_t r48_cnn_train_grad_floats(void);
 

@@ -28,6 +28,7 @@ DRAW_CONTRACT = 3          # R48_DRAW_CONTRACT (include/rein48.h); test_abi chec
 _P, _I32, _I64, _U32, _U64 = C.c_void_p, C.c_int32, C.c_int64, C.c_uint32, C.c_uint64
 SIGNATURES = {
     "r48_cnn_train_grad": (C.c_int, [_P, _I64, _I64, _P, _P, _P, _P, _P, C.c_float, _I32, _P, _P, _P, _P, _P]),
+    "r48_cnn_train_grad_seg": (C.c_int, [_P, _I64, _I64, _P, _P, _P, _P, C.c_float, _I32, _P, _P, _P, _P, _P]),
     "r48_cnn_train_workspace_floats": (_I64, []),
     "r48_cnn_train_grad_floats": (_I64, []),
     "r48_resnet_q_forward": (C.c_int, [_P, _I64, _P, _P, _P, C.c_float, _U64, _I64, _U32, _P]),
@@ -101,6 +102,7 @@ SIGNATURES = {
     "r48_discounted_returns": (C.c_int, [_P, _P, _P, _I32, _I64, C.c_float, _I32, _P, _P]),
     "r48_a3c_segment_stats": (C.c_int, [_P, _P, _P, _P, _I32, _I64, _P, _P, _P, _P]),
     "r48_a3c_row_weights": (C.c_int, [_P, _P, _P, _I32, _I64, _P, _P, _P]),
+    "r48_a3c_segments": (C.c_int, [_P, _P, _P, _P, _P, _I32, _I64, C.c_float, _I32, _P, _P, _P, _P]),
     "r48_rmsprop_tf1": (C.c_int, [_P, _P, _P, _P, _I64, C.c_float, C.c_float, C.c_float, C.c_float, _P]),
     "r48_cnn_rollout": (C.c_int, [_P, _I64, _I32, _P, _P, _I32, _P, _P, _P, _P, _P, _P, _U64, _I64, _U32, _U64,
                                   _U32, _U32, _P]),
@@ -111,6 +113,7 @@ SIGNATURES = {
                                   _U32, _P]),
     "r48_mlp_train_workspace_floats": (_I64, [_I64]),
     "r48_mlp_train_grad": (C.c_int, [_P, _I64, _I64, _P, _P, _P, _P, _P, C.c_float, _I32, _P, _P, _P, _P]),
+    "r48_mlp_train_grad_seg": (C.c_int, [_P, _I64, _I64, _P, _P, _P, _P, C.c_float, _I32, _P, _P, _P, _P]),
     "r48_conv3x3_bn_in": (C.c_int, [_P, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "r48_bn_finish": (C.c_int, [_P, _I32, _I64, _I32, _P, _P, _P, _P, C.c_float, C.c_float, _P, _P, _P]),
     "r48_last_error": (C.c_char_p, []),

@@ -101,30 +101,50 @@ def pack_cnn_train(net, fwd=None):
 GRAD_FLOATS = 9703   # r48_cnn_train_grad's record: dW2 [64][128] | db2 [64] | dW1 [32][5] | dWh [5][257] | losses [2]
 
 
-def cnn_train_grad(net, boards, actions, targets, wn, cm=None, counts=None, beta=0.001, exponents=False,
-                   n_boards=None, packed=None, workspace=None):
+def _check_weights(wn, cm, counts, seg):
+    """wn [+ cm + counts] per row, or seg [+ counts] per board (r48_a3c_segments)."""
+    if seg is not None:
+        if wn is not None or cm is not None:
+            raise ValueError("per-board weights (seg) replace wn / cm")
+        if not seg.is_cuda or seg.dtype != torch.float32 or not seg.is_contiguous() or seg.shape[-1] != 4:
+            raise ValueError("seg must be a contiguous float32 GPU tensor [n_boards, 4]")
+        return
+    if wn is None or not wn.is_cuda or wn.dtype != torch.float32 or not wn.is_contiguous():
+        raise ValueError("wn must be a contiguous float32 GPU tensor")
+    if (cm is None) != (counts is None):
+        raise ValueError("reference mode needs both cm and counts")
+
+
+def cnn_train_grad(net, boards, actions, targets, wn=None, cm=None, counts=None, beta=0.001, exponents=False,
+                   n_boards=None, packed=None, workspace=None, seg=None):
     """Gradient of the A3C loss (rein48_amd/a3c/losses.py) over `rows` training states in ONE fused
     pass (r48_cnn_train_grad). boards int8 [rows, 16]; actions int8 [rows]; targets, wn (= mask /
     (B * n)) f32 [rows]; reference mode: cm (= coef * mask / n) f32 [rows] and counts f32
-    [n_boards, 4] (row r belongs to board r % n_boards). Returns (grads in net.parameters()
-    order, actor loss, critic loss)."""
+    [n_boards, 4] (row r belongs to board r % n_boards). Or, instead of wn / cm, the per-board
+    weights seg f32 [n_boards, 4] of kernels.segments (r48_cnn_train_grad_seg; reference mode iff
+    counts is given). Returns (grads in net.parameters() order, actor loss, critic loss)."""
     L = _lib.load()
     rows = boards.numel() // 16
     dev = boards.device
     for name, t, dt in (("boards", boards, torch.int8), ("actions", actions, torch.int8),
-                        ("targets", targets, torch.float32), ("wn", wn, torch.float32)):
+                        ("targets", targets, torch.float32)):
         if not t.is_cuda or t.dtype != dt or not t.is_contiguous():
             raise ValueError("%s must be a contiguous %s GPU tensor" % (name, dt))
-    if (cm is None) != (counts is None):
-        raise ValueError("reference mode needs both cm and counts")
+    _check_weights(wn, cm, counts, seg)
     wfrag, bias = packed if packed is not None else pack_cnn_train(net)
     if workspace is None:
         workspace = torch.empty(L.r48_cnn_train_workspace_floats(), dtype=torch.float32, device=dev)
     out = torch.empty(GRAD_FLOATS, dtype=torch.float32, device=dev)
-    check(L.r48_cnn_train_grad(ptr(boards), rows, int(n_boards or rows), ptr(actions), ptr(targets), ptr(wn), ptr(cm),
-                               ptr(counts), float(beta), _lib.FEAT_EXPONENTS if exponents else _lib.FEAT_VALUES,
-                               ptr(wfrag), ptr(bias), ptr(workspace), ptr(out),
-                               C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)))
+    mode = _lib.FEAT_EXPONENTS if exponents else _lib.FEAT_VALUES
+    stream = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    if seg is not None:
+        check(L.r48_cnn_train_grad_seg(ptr(boards), rows, int(n_boards or rows), ptr(actions), ptr(targets), ptr(seg),
+                                       ptr(counts), float(beta), mode, ptr(wfrag), ptr(bias), ptr(workspace), ptr(out),
+                                       stream))
+    else:
+        check(L.r48_cnn_train_grad(ptr(boards), rows, int(n_boards or rows), ptr(actions), ptr(targets), ptr(wn),
+                                   ptr(cm), ptr(counts), float(beta), mode, ptr(wfrag), ptr(bias), ptr(workspace),
+                                   ptr(out), stream))
     dw2 = out[:64 * 128].view(64, 128)
     db2 = out[8192:8256]
     dw1 = out[8256:8416].view(32, 5)
@@ -198,25 +218,30 @@ def mlp_forward(boards, w, exponents=False, logits=True, value=True, actions=Fal
 MLP_GRAD_FLOATS = 2501   # r48_mlp_train_grad's gradient (FlatParams order), then actor + critic loss
 
 
-def mlp_train_grad(net, boards, actions, targets, wn, cm=None, counts=None, beta=0.001, exponents=False,
-                   n_boards=None, w=None, workspace=None):
+def mlp_train_grad(net, boards, actions, targets, wn=None, cm=None, counts=None, beta=0.001, exponents=False,
+                   n_boards=None, w=None, workspace=None, seg=None):
     """r48_mlp_train_grad: the A3C loss gradient (losses.chunk_loss's per-row weights wn / cm /
-    counts, as cnn_train_grad) of every ActorCriticMLP parameter over `rows` training states in one
-    fp32 pass -> (flat gradient [2501] in parameters() order, actor loss, critic loss) as device
-    tensors (0-d for the losses)."""
+    counts, or the per-board seg, as cnn_train_grad) of every ActorCriticMLP parameter over `rows`
+    training states in one fp32 pass -> (flat gradient [2501] in parameters() order, actor loss,
+    critic loss) as device tensors (0-d for the losses)."""
     rows = boards.numel() // 16
     dev = boards.device
-    for t, name in ((boards, "boards"), (actions, "actions"), (targets, "targets"), (wn, "wn")):
+    for t, name in ((boards, "boards"), (actions, "actions"), (targets, "targets")):
         if not t.is_cuda or not t.is_contiguous():
             raise ValueError("%s must be a contiguous GPU tensor" % name)
+    _check_weights(wn, cm, counts, seg)
     if w is None:
         w = pack_mlp(net)
     L = _lib.load()
     if workspace is None:
         workspace = torch.empty(int(L.r48_mlp_train_workspace_floats(rows)), dtype=torch.float32, device=dev)
     out = torch.empty(2504, dtype=torch.float32, device=dev)
-    check(L.r48_mlp_train_grad(ptr(boards), rows, int(n_boards or rows), ptr(actions), ptr(targets), ptr(wn), ptr(cm),
-                               ptr(counts), float(beta), _lib.FEAT_EXPONENTS if exponents else _lib.FEAT_VALUES,
-                               ptr(w), ptr(workspace), ptr(out),
-                               C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)))
+    mode = _lib.FEAT_EXPONENTS if exponents else _lib.FEAT_VALUES
+    stream = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    if seg is not None:
+        check(L.r48_mlp_train_grad_seg(ptr(boards), rows, int(n_boards or rows), ptr(actions), ptr(targets), ptr(seg),
+                                       ptr(counts), float(beta), mode, ptr(w), ptr(workspace), ptr(out), stream))
+    else:
+        check(L.r48_mlp_train_grad(ptr(boards), rows, int(n_boards or rows), ptr(actions), ptr(targets), ptr(wn),
+                                   ptr(cm), ptr(counts), float(beta), mode, ptr(w), ptr(workspace), ptr(out), stream))
     return out[:MLP_GRAD_FLOATS], out[MLP_GRAD_FLOATS], out[MLP_GRAD_FLOATS + 1]

@@ -94,6 +94,30 @@ def row_weights(lengths, B, T, td_sum=None):
     return wn, cm
 
 
+def segments(rewards, lengths, bootstrap, gamma=0.9, drop_last=True, values=None, actions=None):
+    """The fused update's per-board pass (r48_a3c_segments), one launch: targets [T, n] exactly as
+    discounted_returns, seg [n, 4] = (w0, c0, L as int32 bits, 0) -- row_weights' wn / cm at every row
+    t < L -- and, with values + actions (the reference loss), counts [n, 4] and c0 from the td sum.
+    -> (targets, seg, counts or None)."""
+    _dev(rewards, "rewards", torch.float32)
+    _dev(lengths, "lengths", torch.int32)
+    _dev(bootstrap, "bootstrap", torch.float32)
+    if (values is None) != (actions is None):
+        raise ValueError("values and actions go together (the reference loss)")
+    if values is not None:
+        _dev(values, "values", torch.float32)
+        _dev(actions, "actions", torch.int8)
+    T, n = rewards.shape
+    dev = rewards.device
+    targets = torch.empty_like(rewards)
+    seg = torch.empty((n, 4), dtype=torch.float32, device=dev)
+    counts = torch.empty((n, 4), dtype=torch.float32, device=dev) if values is not None else None
+    check(_lib.load().r48_a3c_segments(ptr(rewards), ptr(values), ptr(actions), ptr(lengths), ptr(bootstrap), T, n,
+                                       float(gamma), 1 if drop_last else 0, ptr(targets), ptr(seg), ptr(counts),
+                                       _stream(rewards)))
+    return targets, seg, counts
+
+
 def rmsprop_tf1_(var, grad, ms, mom, lr, decay=0.9, momentum=0.0, eps=1e-10):
     """In-place TF1 RMSProp step on flat float32 buffers."""
     for t, name in ((var, "var"), (grad, "grad"), (ms, "ms"), (mom, "mom")):

@@ -282,14 +282,23 @@ class A3CTrainer:
             if v_T is None:
                 v_T = value(self.boards[T]).view(n)
             boot = torch.where(self.finished, torch.zeros_like(v_T), v_T).float().contiguous()
-            targets = K.discounted_returns(self.rewards, self.lengths, boot, cfg.gamma,
-                                           drop_last=cfg.mode == "reference")
-            if self.actions.is_cuda:    # one launch (r48_a3c_segment_stats) for the masked sums + counts
-                stats = K.segment_stats(self.actions, self.lengths, v_all, None if v_all is None else targets)
-            elif v_all is not None:
-                stats = segment_stats(v_all, targets, self.actions, self.mask)
+            if fused_upd:
+                # returns, per-board loss weights and (reference loss) action counts in ONE launch
+                # (r48_a3c_segments): the fused kernels expand the weights per row themselves
+                ref = cfg.mode == "reference"
+                targets, seg, counts = K.segments(self.rewards, self.lengths, boot, cfg.gamma, drop_last=ref,
+                                                  values=v_all if ref else None,
+                                                  actions=self.actions if ref else None)
+                stats = {"seg": seg, "counts": counts}
             else:
-                stats = {"B": self.mask.float().sum(0).clamp(min=1.0)}
+                targets = K.discounted_returns(self.rewards, self.lengths, boot, cfg.gamma,
+                                               drop_last=cfg.mode == "reference")
+                if self.actions.is_cuda:    # one launch (r48_a3c_segment_stats) for the masked sums + counts
+                    stats = K.segment_stats(self.actions, self.lengths, v_all, None if v_all is None else targets)
+                elif v_all is not None:
+                    stats = segment_stats(v_all, targets, self.actions, self.mask)
+                else:
+                    stats = {"B": self.mask.float().sum(0).clamp(min=1.0)}
         if fused_upd:
             # pass 2 as ONE fused kernel over all T x n states (no activation hits HBM): MFMA for the
             # CNN (r48_a3c_train.hip), fp32 MFMA + VALU for the reference MLP (r48_mlp_train.hip)
@@ -329,10 +338,14 @@ class A3CTrainer:
         cfg = self.cfg
         n = cfg.n_boards
         ref = cfg.mode == "reference"
-        # wn = mask / (B n), cm = (td_sum / (4 B^2)) mask / n as one launch (r48_a3c_row_weights)
-        wn, cm = K.row_weights(self.lengths, stats["B"].contiguous(), cfg.max_steps,
-                               stats["td_sum"].contiguous() if ref else None)
-        counts = stats["counts"].float().contiguous() if ref else None
+        if "seg" in stats:   # per-board weights (r48_a3c_segments): no [T][n] weight rows
+            wn = cm = None
+            seg, counts = stats["seg"], stats["counts"]
+        else:
+            # wn = mask / (B n), cm = (td_sum / (4 B^2)) mask / n as one launch (r48_a3c_row_weights)
+            wn, cm = K.row_weights(self.lengths, stats["B"].contiguous(), cfg.max_steps,
+                                   stats["td_sum"].contiguous() if ref else None)
+            seg, counts = None, stats["counts"].float().contiguous() if ref else None
         if self._mlp_fused():
             from .fused import mlp_train_grad
             if getattr(self, "_mlp_ws", None) is None:
@@ -340,17 +353,18 @@ class A3CTrainer:
                                            device=self.device)
             g, actor, critic = mlp_train_grad(
                 self.net, states.reshape(-1, 16), self.actions.reshape(-1), targets.reshape(-1).contiguous(),
-                wn.view(-1), None if cm is None else cm.view(-1), counts, beta=cfg.beta,
-                exponents=cfg.features == "exponents", n_boards=n, w=self._mlp_weights(), workspace=self._mlp_ws)
+                None if wn is None else wn.view(-1), None if cm is None else cm.view(-1), counts, beta=cfg.beta,
+                exponents=cfg.features == "exponents", n_boards=n, w=self._mlp_weights(), workspace=self._mlp_ws,
+                seg=seg)
             self.flat.grad.copy_(g)
             return actor, critic
         if getattr(self, "_train_ws", None) is None:
             self._train_ws = torch.empty(_lib_workspace_floats(), dtype=torch.float32, device=self.device)
         grads, actor, critic = cnn_train_grad(
             self.net, states.reshape(-1, 16), self.actions.reshape(-1), targets.reshape(-1).contiguous(),
-            wn.view(-1), None if cm is None else cm.view(-1), counts, beta=cfg.beta,
+            None if wn is None else wn.view(-1), None if cm is None else cm.view(-1), counts, beta=cfg.beta,
             exponents=cfg.features == "exponents", n_boards=n, packed=self._packed("cnn_train"),
-            workspace=self._train_ws)
+            workspace=self._train_ws, seg=seg)
         with torch.no_grad():
             for p, g in zip(self.net.parameters(), grads):
                 p.grad.copy_(g.view_as(p))

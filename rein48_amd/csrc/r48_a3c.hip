@@ -296,6 +296,67 @@ __global__ __launch_bounds__(kBlock) void k_row_weights(const int32_t *__restric
         cm[r] = ((td_sum[i] / ((4.0f * b) * b)) * m) * inv_n;
 }
 
+// The update's per-board pass in one launch (trainer.A3CTrainer.update with the fused gradient):
+// the discounted returns of k_returns (same recurrence, same instruction per step: identical
+// targets), and per board seg = {w0, c0, L, 0} -- the per-row weights of k_row_weights at every row
+// t < L (w0 = (1 / B) (1 / n), c0 = (td_sum / ((4 B) B)) (1 / n), B = max(L, 1), L as int bits),
+// which the train kernels expand themselves -- plus, with TD (the reference loss), td_sum over
+// t < L of targets - values (summed from t = L - 1 down: the scan's order, not k_segment_stats')
+// and the action counts. One lane per board, the T rows coalesced across lanes, 8 rows of loads in
+// flight.
+template <bool DROP_LAST, bool TD>
+__global__ __launch_bounds__(kBlock) void k_segments(const float *__restrict__ rewards, const float *__restrict__ values,
+                                                     const int8_t *__restrict__ actions, const int32_t *__restrict__ len,
+                                                     const float *__restrict__ bootstrap, int32_t T, int64_t n, float gamma,
+                                                     float *__restrict__ out, float4 *__restrict__ seg,
+                                                     float4 *__restrict__ counts)
+{
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n)
+        return;
+    const int32_t L = min(max(len[i], 0), T);
+    float g = bootstrap[i], td = 0.0f, c[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    constexpr int kAhead = 8;
+    for (int32_t t0 = T - 1; t0 >= 0; t0 -= kAhead) {
+        float r[kAhead], v[kAhead];
+        int a[kAhead];
+#pragma unroll
+        for (int k = 0; k < kAhead; k++) {
+            const int32_t t = t0 - k;
+            const int64_t o = (int64_t)max(t, 0) * n + i;
+            r[k] = rewards[o];
+            v[k] = TD ? values[o] : 0.0f;
+            a[k] = TD ? actions[o] & 3 : 0;
+        }
+#pragma unroll
+        for (int k = 0; k < kAhead; k++) {
+            const int32_t t = t0 - k;
+            if (t < 0)
+                break;
+            float o;
+            if (t >= L) {
+                o = 0.0f;
+            } else if (DROP_LAST && t == L - 1) {
+                o = g;
+            } else {
+                g = r[k] + gamma * g;
+                o = g;
+            }
+            out[(int64_t)t * n + i] = o;
+            if (TD && t < L) {
+                td += o - v[k];
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+                    c[q] += a[k] == q ? 1.0f : 0.0f;
+            }
+        }
+    }
+    const float b = (float)max(L, 1), inv_n = 1.0f / (float)n;
+    seg[i] = make_float4((1.0f / b) * inv_n, TD ? ((td / ((4.0f * b) * b)) * 1.0f) * inv_n : 0.0f, __int_as_float(L), 0.0f);
+    if (TD)
+        counts[i] = make_float4(c[0], c[1], c[2], c[3]);
+}
+
 }  // namespace
 
 extern "C" {
@@ -403,6 +464,24 @@ int r48_a3c_row_weights(const int32_t *lengths, const float *B, const float *td_
                        (hipStream_t)stream, lengths, B,
                        td_sum, T, n, wn, cm);
     return launched("k_row_weights");
+}
+
+int r48_a3c_segments(const float *rewards, const float *values, const int8_t *actions, const int32_t *lengths,
+                     const float *bootstrap, int32_t T, int64_t n, float gamma, int32_t drop_last, float *targets,
+                     float *seg, float *counts, void *stream)
+{
+    const bool td = counts != nullptr;
+    if (!rewards || !lengths || !bootstrap || !targets || !seg || T < 1 || n < 0 || (td && (!values || !actions)) ||
+        ((reinterpret_cast<uintptr_t>(seg) | reinterpret_cast<uintptr_t>(counts)) & 15))
+        return fail(R48_EINVAL, "r48_a3c_segments: NULL argument (values/actions needed with counts), T < 1, n < 0 "
+                                "or seg/counts not 16-byte aligned");
+    if (n == 0)
+        return R48_OK;
+    auto kern = drop_last ? (td ? k_segments<true, true> : k_segments<true, false>)
+                          : (td ? k_segments<false, true> : k_segments<false, false>);
+    hipLaunchKernelGGL(kern, grid_for(n), dim3(kBlock), 0, (hipStream_t)stream, rewards, values, actions, lengths,
+                       bootstrap, T, n, gamma, targets, reinterpret_cast<float4 *>(seg), reinterpret_cast<float4 *>(counts));
+    return launched("k_segments");
 }
 
 }  // extern "C"

@@ -304,11 +304,13 @@ __device__ __forceinline__ void fwd_conv2_heads_chain(const uint4 *w, const floa
     }
 }
 
-template <int MODE>
+// SEG: the row weights come per board (seg[b] = {w0, c0, L, 0} of r48_a3c_segments, row t * n_boards + b
+// weighted iff t < L; reference loss iff counts != NULL) instead of per row (wn, cm)
+template <int MODE, bool SEG>
 __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
     const int8_t *__restrict__ boards, int64_t rows, int64_t n_boards, const int8_t *__restrict__ actions,
     const float *__restrict__ targets, const float *__restrict__ wn, const float *__restrict__ cm,
-    const float *__restrict__ counts, float beta, const uint4 *__restrict__ wfrag,
+    const float4 *__restrict__ seg, const float *__restrict__ counts, float beta, const uint4 *__restrict__ wfrag,
     const float *__restrict__ bias, float *__restrict__ partials)
 {
     extern __shared__ uint4 lds[];
@@ -362,24 +364,51 @@ __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
         float wt, tgt, c;
         int act;
         float4 cnt;
+        uint32_t t, L;   // SEG: the row's step (UINT32_MAX when not live) and its segment length
     };
+    // SEG: (step, board) of the lane's unclamped row tile * 32 + col, advanced by 32 stride rows per
+    // fetch without a division (rows of a prefetch past the end are not live; their board index stays
+    // in range)
+    const uint32_t nb = (uint32_t)n_boards;
+    uint32_t seg_t = 0, seg_b = 0, seg_dt = 0, seg_db = 0;
+    if (SEG) {
+        const uint32_t u0 = (uint32_t)(first * 32 + col), du = (uint32_t)(stride * 32);
+        seg_t = u0 / nb, seg_b = u0 % nb, seg_dt = du / nb, seg_db = du % nb;
+    }
+    const bool ref = SEG ? counts != nullptr : cm != nullptr;   // wave-uniform
     auto fetch = [&](int64_t tile) {
         RowIn in;
         const int64_t r = std::min<int64_t>(tile, n_tiles - 1) * 32 + col;
         const bool live = r < rows && tile < n_tiles;
         const int64_t rr = r < rows ? r : rows - 1;     // padding lanes compute on a valid row, weight 0
         in.raw = *reinterpret_cast<const uint2 *>(boards + 16 * rr + 8 * h);
-        const float wt = wn[rr];
-        in.wt = live ? wt : 0.0f;
         in.tgt = targets[rr];
         in.act = actions[rr] & 3;
         in.c = 0.f, in.cnt = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (cm) {   // wave-uniform
-            const float c = cm[rr];
-            in.c = live ? c : 0.0f;
-            // row rr belongs to board rr % n_boards (rows are [T][n_boards]); 32-bit when it fits
-            const int64_t bidx = rows <= 0xFFFFFFFFll ? (int64_t)((uint32_t)rr % (uint32_t)n_boards) : rr % n_boards;
-            in.cnt = *reinterpret_cast<const float4 *>(counts + 4 * bidx);
+        if (SEG) {   // raw per-board values: the step test waits for the load in the loss, not here
+            const float4 sg = seg[seg_b];
+            in.wt = sg.x;
+            in.L = (uint32_t)__float_as_int(sg.z);
+            in.t = live ? seg_t : 0xFFFFFFFFu;
+            if (ref) {
+                in.c = sg.y;
+                in.cnt = *reinterpret_cast<const float4 *>(counts + 4 * (int64_t)seg_b);
+            }
+            seg_b += seg_db;
+            seg_t += seg_dt;
+            if (seg_b >= nb)
+                seg_b -= nb, seg_t++;
+        } else {
+            const float wt = wn[rr];
+            in.wt = live ? wt : 0.0f;
+            if (ref) {
+                const float c = cm[rr];
+                in.c = live ? c : 0.0f;
+                // row rr belongs to board rr % n_boards (rows are [T][n_boards]); 32-bit when it fits
+                const int64_t bidx =
+                    rows <= 0xFFFFFFFFll ? (int64_t)((uint32_t)rr % (uint32_t)n_boards) : rr % n_boards;
+                in.cnt = *reinterpret_cast<const float4 *>(counts + 4 * bidx);
+            }
         }
         return in;
     };
@@ -422,7 +451,8 @@ __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
                         bl[100];
         float dz[4] = {0.f, 0.f, 0.f, 0.f}, dv = 0.f;
         if (h == 0) {
-            const float wt = in.wt;
+            const bool on = !SEG || in.t < in.L;
+            const float wt = on ? in.wt : 0.0f;
             float z[4], p[4], gr[4];
 #pragma unroll
             for (int k = 0; k < 4; k++)
@@ -447,8 +477,8 @@ __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
             }
             const float td = in.tgt - v;
             const int a = in.act;
-            if (cm) {   // reference: -beta wn H - cm sum_k c_k log p_k  (losses.py, a3c.py:110-116)
-                const float c = in.c;
+            if (ref) {   // reference: -beta wn H - cm sum_k c_k log p_k  (losses.py, a3c.py:110-116)
+                const float c = on ? in.c : 0.0f;
                 const float4 cnt = in.cnt;
                 const float ck[4] = {cnt.x, cnt.y, cnt.z, cnt.w}, C = cnt.x + cnt.y + cnt.z + cnt.w;
                 float sa = 0.f;
@@ -716,6 +746,28 @@ int fail(int code, const std::string &msg)
 // per-wave record workspace (r48_cnn_train_workspace_floats) and the launch always agree
 constexpr int grid_size() { return 256; }
 
+int cnn_train_launch(const int8_t *boards, int64_t rows, int64_t n_boards, const int8_t *actions, const float *targets,
+                     const float *wn, const float *cm, const float *seg, const float *counts, float beta, int32_t mode,
+                     const void *wfrag, const float *bias, float *workspace, float *grad, void *stream)
+{
+    const int grid = grid_size();
+    const size_t lds = kLds;
+    // one instantiation per input encoding (no per-cell branch); each needs the LDS opt-in once
+    auto kern = seg ? (mode == R48_FEAT_VALUES ? k_cnn_train<R48_FEAT_VALUES, true> : k_cnn_train<R48_FEAT_EXPONENTS, true>)
+                    : (mode == R48_FEAT_VALUES ? k_cnn_train<R48_FEAT_VALUES, false> : k_cnn_train<R48_FEAT_EXPONENTS, false>);
+    r48::ensure_dynamic_lds(reinterpret_cast<const void *>(kern), (int)lds, r48::stream_device((hipStream_t)stream));
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), lds, (hipStream_t)stream, boards, rows, n_boards, actions,
+                       targets, wn, cm, (const float4 *)seg, counts, beta, (const uint4 *)wfrag, bias, workspace);
+    // the group sums go after the records in the workspace (r48_cnn_train_workspace_floats)
+    float *group_sums = workspace + (int64_t)grid * kWaves * kPartial;
+    hipLaunchKernelGGL(k_reduce_groups, dim3((kPartial + 255) / 256, kGroups), dim3(256), 0, (hipStream_t)stream,
+                       workspace, (int64_t)grid * kWaves, group_sums);
+    hipLaunchKernelGGL(k_reduce, dim3((kPartial + 255) / 256), dim3(256), 0, (hipStream_t)stream, group_sums, grad);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess)
+        return fail(R48_EHIP, std::string("k_cnn_train: ") + hipGetErrorString(e));
+    return R48_OK;
+}
 }  // namespace
 
 extern "C" {
@@ -736,22 +788,22 @@ int r48_cnn_train_grad(const int8_t *boards, int64_t rows, int64_t n_boards, con
     if ((reinterpret_cast<uintptr_t>(boards) | reinterpret_cast<uintptr_t>(wfrag) |
          reinterpret_cast<uintptr_t>(counts)) & 15u)
         return fail(R48_EINVAL, "boards, wfrag and counts must be 16-byte aligned");
-    const int grid = grid_size();
-    const size_t lds = kLds;
-    // one instantiation per input encoding (no per-cell branch); each needs the LDS opt-in once
-    auto kern = mode == R48_FEAT_VALUES ? k_cnn_train<R48_FEAT_VALUES> : k_cnn_train<R48_FEAT_EXPONENTS>;
-    r48::ensure_dynamic_lds(reinterpret_cast<const void *>(kern), (int)lds, r48::stream_device((hipStream_t)stream));
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), lds, (hipStream_t)stream, boards, rows, n_boards, actions,
-                       targets, wn, cm, counts, beta, (const uint4 *)wfrag, bias, workspace);
-    // the group sums go after the records in the workspace (r48_cnn_train_workspace_floats)
-    float *group_sums = workspace + (int64_t)grid * kWaves * kPartial;
-    hipLaunchKernelGGL(k_reduce_groups, dim3((kPartial + 255) / 256, kGroups), dim3(256), 0, (hipStream_t)stream,
-                       workspace, (int64_t)grid * kWaves, group_sums);
-    hipLaunchKernelGGL(k_reduce, dim3((kPartial + 255) / 256), dim3(256), 0, (hipStream_t)stream, group_sums, grad);
-    const hipError_t e = hipGetLastError();
-    if (e != hipSuccess)
-        return fail(R48_EHIP, std::string("k_cnn_train: ") + hipGetErrorString(e));
-    return R48_OK;
+    return cnn_train_launch(boards, rows, n_boards, actions, targets, wn, cm, nullptr, counts, beta, mode, wfrag, bias,
+                            workspace, grad, stream);
+}
+
+int r48_cnn_train_grad_seg(const int8_t *boards, int64_t rows, int64_t n_boards, const int8_t *actions,
+                           const float *targets, const float *seg, const float *counts, float beta, int32_t mode,
+                           const void *wfrag, const float *bias, float *workspace, float *grad, void *stream)
+{
+    if (!boards || !actions || !targets || !seg || !wfrag || !bias || !workspace || !grad || rows < 1 ||
+        n_boards < 1 || n_boards > 0x7FFFFFFF || (mode != R48_FEAT_VALUES && mode != R48_FEAT_EXPONENTS))
+        return fail(R48_EINVAL, "NULL argument, rows/n_boards < 1, n_boards >= 2^31 or bad mode");
+    if ((reinterpret_cast<uintptr_t>(boards) | reinterpret_cast<uintptr_t>(wfrag) | reinterpret_cast<uintptr_t>(seg) |
+         reinterpret_cast<uintptr_t>(counts)) & 15u)
+        return fail(R48_EINVAL, "boards, wfrag, seg and counts must be 16-byte aligned");
+    return cnn_train_launch(boards, rows, n_boards, actions, targets, nullptr, nullptr, seg, counts, beta, mode, wfrag,
+                            bias, workspace, grad, stream);
 }
 
 }  // extern "C"

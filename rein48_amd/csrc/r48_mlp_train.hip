@@ -178,36 +178,48 @@ struct RowIn {
     float wt, tgt, c;
     int a;
     float4 cnt;
+    int32_t t, L;   // SEG: the row's step (INT32_MAX when not live) and its segment length
 };
 
-template <bool REF>
-__device__ __forceinline__ RowIn fetch_row(int64_t r, int64_t rows, int64_t bidx, const int8_t *boards,
+// SEG: the row weights per board (seg[bidx] = {w0, c0, L, 0} of r48_a3c_segments; the row is weighted
+// iff its step tidx < L) instead of per row (wn, cm)
+template <bool REF, bool SEG>
+__device__ __forceinline__ RowIn fetch_row(int64_t r, int64_t rows, int64_t bidx, int64_t tidx, const int8_t *boards,
                                            const int8_t *actions, const float *targets, const float *wn,
-                                           const float *cm, const float *counts)
+                                           const float *cm, const float4 *seg, const float *counts)
 {
     const bool live = r < rows;
     const int64_t rr = live ? r : rows - 1;   // padding rows: a valid row with weight 0
     RowIn x;
     x.b = *reinterpret_cast<const uint4 *>(boards + 16 * rr);
-    x.wt = live ? wn[rr] : 0.0f;
     x.tgt = targets[rr];
     x.a = actions[rr] & 3;
     x.c = 0.0f;
     x.cnt = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (REF) {
-        x.c = live ? cm[rr] : 0.0f;
-        x.cnt = *reinterpret_cast<const float4 *>(counts + 4 * bidx);
+    if (SEG) {   // raw per-board values: the step test waits for the load where the row is used
+        const float4 sg = seg[bidx];
+        x.wt = sg.x;
+        x.c = sg.y;
+        x.L = __float_as_int(sg.z);
+        x.t = live ? (int32_t)tidx : 0x7FFFFFFF;
+    } else {
+        x.wt = live ? wn[rr] : 0.0f;
+        if (REF)
+            x.c = live ? cm[rr] : 0.0f;
     }
+    if (REF)
+        x.cnt = *reinterpret_cast<const float4 *>(counts + 4 * bidx);
     return x;
 }
 
 // flag list of hot wave q: int2 entries (tile, any logit near its boundary) at list[2 q cap ..], its
 // length in list_len[q]; cap >= the wave's tile count
-template <int MODE, bool REF, bool FIX>
+template <int MODE, bool REF, bool FIX, bool SEG>
 __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_eu(2))) void k_mlp_train(
     const int8_t *__restrict__ boards, int64_t rows, int64_t n_boards, const int8_t *__restrict__ actions,
     const float *__restrict__ targets, const float *__restrict__ wn, const float *__restrict__ cm,
-    const float *__restrict__ counts, float beta, const float *__restrict__ w, float *__restrict__ partials,
+    const float4 *__restrict__ seg, const float *__restrict__ counts, float beta, const float *__restrict__ w,
+    float *__restrict__ partials,
     int32_t *__restrict__ list, int32_t *__restrict__ list_len, int64_t cap)
 {
     // per wave: the tile's 16 boards (64 words) and each row's largest input; per workgroup: the
@@ -392,10 +404,15 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
     // the counts row of training row r is r mod n_boards (rows are step-major, t * n_boards + board):
     // kept incrementally as the lane's row advances by 16 * stride (a prefetch past the end, clamped
     // to the last tile, reads a valid counts row it never uses); the fix pass computes it per tile
-    int64_t bnext = REF ? (std::min<int64_t>(tile, n_tiles - 1) * 16 + j) % n_boards : 0;
-    const int64_t bstep = REF ? (stride * 16) % n_boards : 0;
-    RowIn next = fetch_row<REF>(std::min<int64_t>(tile, n_tiles - 1) * 16 + j, rows, bnext, boards, actions, targets,
-                                wn, cm, counts);
+    // SEG: the step of the row as well (tnext_t, with bnext: the row's (step, board)), both advanced
+    // without a division in the hot pass
+    const int64_t r0 = (SEG ? tile : std::min<int64_t>(tile, n_tiles - 1)) * 16 + j;
+    int64_t bnext = REF || SEG ? r0 % n_boards : 0;
+    int64_t tnext_t = SEG ? r0 / n_boards : 0;   // < 2^31: rows / n_boards steps
+    const int64_t bstep = REF || SEG ? (stride * 16) % n_boards : 0;
+    const int64_t tstep = SEG ? (stride * 16) / n_boards : 0;
+    RowIn next = fetch_row<REF, SEG>(std::min<int64_t>(tile, n_tiles - 1) * 16 + j, rows, bnext, tnext_t, boards, actions,
+                                     targets, wn, cm, seg, counts);
     for (int64_t e = e_lo; FIX ? e < e_hi : tile < n_tiles; e++) {
         // ---------------- inputs: row r0 + j in the four lanes j + 16g
         const RowIn in = next;
@@ -408,16 +425,20 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
                 tnext = v.x;
                 nxt_near = v.y;
             }
-            if (REF)
+            if (REF || SEG)
                 bnext = (tnext * 16 + j) % n_boards;
+            if (SEG)
+                tnext_t = (tnext * 16 + j) / n_boards;
         } else {
             tnext = std::min<int64_t>(tile + stride, n_tiles - 1);
-            if (REF) {
+            if (REF || SEG) {
                 bnext += bstep;
-                bnext -= bnext >= n_boards ? n_boards : 0;
+                tnext_t += tstep;
+                if (bnext >= n_boards)
+                    bnext -= n_boards, tnext_t++;
             }
         }
-        next = fetch_row<REF>(tnext * 16 + j, rows, bnext, boards, actions, targets, wn, cm, counts);
+        next = fetch_row<REF, SEG>(tnext * 16 + j, rows, bnext, tnext_t, boards, actions, targets, wn, cm, seg, counts);
         const uint4 bv = in.b;
         const uint32_t bwd[4] = {bv.x, bv.y, bv.z, bv.w};
         float xa[4];   // A operands of layer 1: x[r0 + j][4s + g]
@@ -434,11 +455,12 @@ __global__ __launch_bounds__(64 * kTrainWaves) __attribute__((amdgpu_waves_per_e
         if (g == 0) {
             *reinterpret_cast<uint4 *>(bw + kTB + 4 * j) = bv;
             bw[kTXm + j] = __float_as_uint(cell_input<MODE>(mb));
-            bw[kTWt + j] = __float_as_uint(in.wt);
+            const bool on = !SEG || in.t < in.L;
+            bw[kTWt + j] = __float_as_uint(on ? in.wt : 0.0f);
             bw[kTTg + j] = __float_as_uint(in.tgt);
             bw[kTAc + j] = (uint32_t)in.a;
             if (REF) {
-                bw[kTCm + j] = __float_as_uint(in.c);
+                bw[kTCm + j] = __float_as_uint(on ? in.c : 0.0f);
                 *reinterpret_cast<float4 *>(bw + kTCn + 4 * j) = in.cnt;
             }
         }
@@ -876,6 +898,51 @@ int64_t r48_mlp_train_workspace_floats(int64_t rows)
     return kRecFloats + 2 * kTrainRecs * list_cap(rows) + kTrainRecs;
 }
 
+static int mlp_train_launch(const int8_t *boards, int64_t rows, int64_t n_boards, const int8_t *actions,
+                            const float *targets, const float *wn, const float *cm, const float *seg, const float *counts,
+                            float beta, int32_t mode, const float *w, float *workspace, float *grad, void *stream)
+{
+    const int n_rec = 2 * kTrainRecs, n_grp = (n_rec + kRedGroup - 1) / kRedGroup;
+    const int64_t cap = list_cap(rows);
+    int32_t *list = reinterpret_cast<int32_t *>(workspace + kRecFloats);
+    int32_t *list_len = list + 2 * kTrainRecs * cap;
+    hipStream_t s = (hipStream_t)stream;
+    const float4 *sg = reinterpret_cast<const float4 *>(seg);
+    // hot pass (records 0 .. kTrainRecs - 1, the flag lists), then the fix pass over the lists (records
+    // kTrainRecs ..): one stream, so the fix pass sees the hot pass's lists
+    auto go = [&](auto hot, auto fix) {
+        hipLaunchKernelGGL(hot, dim3(kTrainGroups), dim3(64 * kTrainWaves), 0, s, boards, rows, n_boards, actions,
+                           targets, wn, cm, sg, counts, beta, w, workspace, list, list_len, cap);
+        hipLaunchKernelGGL(fix, dim3(kTrainGroups), dim3(64 * kTrainWaves), 0, s, boards, rows, n_boards, actions,
+                           targets, wn, cm, sg, counts, beta, w, workspace + kTrainRecs * kRec, list, list_len, cap);
+    };
+    // the reference loss: cm (per row) or counts with seg (per board)
+    const bool ref = seg ? counts != nullptr : cm != nullptr;
+    constexpr int V = R48_FEAT_VALUES, E = R48_FEAT_EXPONENTS;
+    if (seg) {
+        if (mode == V)
+            ref ? go(k_mlp_train<V, true, false, true>, k_mlp_train<V, true, true, true>)
+                : go(k_mlp_train<V, false, false, true>, k_mlp_train<V, false, true, true>);
+        else
+            ref ? go(k_mlp_train<E, true, false, true>, k_mlp_train<E, true, true, true>)
+                : go(k_mlp_train<E, false, false, true>, k_mlp_train<E, false, true, true>);
+    } else {
+        if (mode == V)
+            ref ? go(k_mlp_train<V, true, false, false>, k_mlp_train<V, true, true, false>)
+                : go(k_mlp_train<V, false, false, false>, k_mlp_train<V, false, true, false>);
+        else
+            ref ? go(k_mlp_train<E, true, false, false>, k_mlp_train<E, true, true, false>)
+                : go(k_mlp_train<E, false, false, false>, k_mlp_train<E, false, true, false>);
+    }
+    float4 *groups = reinterpret_cast<float4 *>(workspace + (int64_t)n_rec * kRec);
+    constexpr int q = kRec / 4;
+    hipLaunchKernelGGL(k_mlp_reduce1, dim3((q * n_grp + 255) / 256), dim3(256), 0, s, (const float4 *)workspace, n_rec,
+                       groups);
+    hipLaunchKernelGGL(k_mlp_reduce2, dim3((q + 255) / 256), dim3(256), 0, s, (const float4 *)groups, n_grp,
+                       (float4 *)grad);
+    return launched("k_mlp_train");
+}
+
 int r48_mlp_train_grad(const int8_t *boards, int64_t rows, int64_t n_boards, const int8_t *actions,
                        const float *targets, const float *wn, const float *cm, const float *counts, float beta,
                        int32_t mode, const float *w, float *workspace, float *grad, void *stream)
@@ -886,32 +953,24 @@ int r48_mlp_train_grad(const int8_t *boards, int64_t rows, int64_t n_boards, con
     if ((reinterpret_cast<uintptr_t>(boards) | reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(counts) |
          reinterpret_cast<uintptr_t>(workspace) | reinterpret_cast<uintptr_t>(grad)) & 15u)
         return fail(R48_EINVAL, "r48_mlp_train_grad: boards, w, counts, workspace and grad must be 16-byte aligned");
-    const int n_rec = 2 * kTrainRecs, n_grp = (n_rec + kRedGroup - 1) / kRedGroup;
-    const int64_t cap = list_cap(rows);
-    int32_t *list = reinterpret_cast<int32_t *>(workspace + kRecFloats);
-    int32_t *list_len = list + 2 * kTrainRecs * cap;
-    hipStream_t s = (hipStream_t)stream;
-    // hot pass (records 0 .. kTrainRecs - 1, the flag lists), then the fix pass over the lists (records
-    // kTrainRecs ..): one stream, so the fix pass sees the hot pass's lists
-    auto go = [&](auto hot, auto fix) {
-        hipLaunchKernelGGL(hot, dim3(kTrainGroups), dim3(64 * kTrainWaves), 0, s, boards, rows, n_boards, actions,
-                           targets, wn, cm, counts, beta, w, workspace, list, list_len, cap);
-        hipLaunchKernelGGL(fix, dim3(kTrainGroups), dim3(64 * kTrainWaves), 0, s, boards, rows, n_boards, actions,
-                           targets, wn, cm, counts, beta, w, workspace + kTrainRecs * kRec, list, list_len, cap);
-    };
-    if (mode == R48_FEAT_VALUES)
-        cm ? go(k_mlp_train<R48_FEAT_VALUES, true, false>, k_mlp_train<R48_FEAT_VALUES, true, true>)
-           : go(k_mlp_train<R48_FEAT_VALUES, false, false>, k_mlp_train<R48_FEAT_VALUES, false, true>);
-    else
-        cm ? go(k_mlp_train<R48_FEAT_EXPONENTS, true, false>, k_mlp_train<R48_FEAT_EXPONENTS, true, true>)
-           : go(k_mlp_train<R48_FEAT_EXPONENTS, false, false>, k_mlp_train<R48_FEAT_EXPONENTS, false, true>);
-    float4 *groups = reinterpret_cast<float4 *>(workspace + (int64_t)n_rec * kRec);
-    constexpr int q = kRec / 4;
-    hipLaunchKernelGGL(k_mlp_reduce1, dim3((q * n_grp + 255) / 256), dim3(256), 0, s, (const float4 *)workspace, n_rec,
-                       groups);
-    hipLaunchKernelGGL(k_mlp_reduce2, dim3((q + 255) / 256), dim3(256), 0, s, (const float4 *)groups, n_grp,
-                       (float4 *)grad);
-    return launched("k_mlp_train");
+    return mlp_train_launch(boards, rows, n_boards, actions, targets, wn, cm, nullptr, counts, beta, mode, w, workspace,
+                            grad, stream);
+}
+
+int r48_mlp_train_grad_seg(const int8_t *boards, int64_t rows, int64_t n_boards, const int8_t *actions,
+                           const float *targets, const float *seg, const float *counts, float beta, int32_t mode,
+                           const float *w, float *workspace, float *grad, void *stream)
+{
+    if (!boards || !actions || !targets || !seg || !w || !workspace || !grad || rows < 1 || n_boards < 1 ||
+        (mode != R48_FEAT_VALUES && mode != R48_FEAT_EXPONENTS))
+        return fail(R48_EINVAL, "r48_mlp_train_grad_seg: NULL argument, rows/n_boards < 1 or bad mode");
+    if ((reinterpret_cast<uintptr_t>(boards) | reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(seg) |
+         reinterpret_cast<uintptr_t>(counts) | reinterpret_cast<uintptr_t>(workspace) |
+         reinterpret_cast<uintptr_t>(grad)) & 15u)
+        return fail(R48_EINVAL, "r48_mlp_train_grad_seg: boards, w, seg, counts, workspace and grad must be 16-byte "
+                                "aligned");
+    return mlp_train_launch(boards, rows, n_boards, actions, targets, nullptr, nullptr, seg, counts, beta, mode, w,
+                            workspace, grad, stream);
 }
 
 }  // extern "C"

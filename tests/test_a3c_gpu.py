@@ -475,6 +475,94 @@ def test_segment_stats_and_row_weights_match_tensor_forms():
     assert torch.equal(cm, (got["td_sum"] / (4.0 * got["B"] * got["B"]))[None, :] * m / n)
 
 
+@pytest.mark.parametrize("n", [70001, 4096])
+@pytest.mark.parametrize("reference", [False, True])
+def test_segments_equal_returns_stats_and_row_weights(reference, n):
+    """r48_a3c_segments (the fused update's one per-board pass) vs the three kernels it replaces on
+    ragged segment lengths 0..T (and one past T): targets bit-identical to r48_discounted_returns
+    (both drop_last modes, n = 4096 takes its float4 kernel), counts equal to r48_a3c_segment_stats',
+    w0 / c0 / L equal to r48_a3c_row_weights' wn / cm at every row t < L -- w0 bit for bit, c0 to the
+    fp32 rounding of the td sum's order (the segment pass sums from t = L - 1 down)."""
+    from rein48_amd.a3c import kernels as K
+    T = 100
+    g = torch.Generator(device="cpu").manual_seed(12)
+    lengths = torch.randint(1, T + 1, (n,), generator=g, dtype=torch.int32)
+    lengths[:6] = torch.tensor([1, T, 2, T - 1, 0, T + 3], dtype=torch.int32)
+    lengths = lengths.to(DEV)
+    rewards = (torch.randn(T, n, generator=g) * 4).to(DEV)
+    values = torch.randn(T, n, generator=g).to(DEV)
+    actions = torch.randint(0, 4, (T, n), generator=g, dtype=torch.int8).to(DEV)
+    boot = torch.randn(n, generator=g).to(DEV)
+    tg, seg, counts = K.segments(rewards, lengths, boot, 0.9, drop_last=reference,
+                                 values=values if reference else None, actions=actions if reference else None)
+    want = K.discounted_returns(rewards, lengths, boot, 0.9, drop_last=reference)
+    assert torch.equal(tg, want)
+    L = lengths.clamp(0, T)
+    assert torch.equal(seg[:, 2].view(torch.int32), L) and bool((seg[:, 3] == 0).all())
+    st = K.segment_stats(actions, lengths, values, want)
+    wn, cm = K.row_weights(L, st["B"], T, st["td_sum"])
+    valid = torch.arange(T, device=DEV)[:, None] < L[None, :]
+    assert torch.equal(torch.where(valid, seg[None, :, 0].expand(T, n), torch.zeros_like(wn)), wn)
+    if reference:
+        assert torch.equal(counts, st["counts"])
+        got_cm = torch.where(valid, seg[None, :, 1].expand(T, n), torch.zeros_like(cm))
+        mag = ((want - values).abs() * valid).sum(0) / (4.0 * st["B"] * st["B"]) / n
+        assert bool(((got_cm - cm).abs() <= 1e-5 * mag[None, :] + 1e-30).all())
+    else:
+        assert counts is None and bool((seg[:, 1] == 0).all())
+
+
+def _seg_case(T, n, seed, reference):
+    """Random training rows [T][n] with ragged segments and their per-board weights (r48_a3c_segments),
+    plus the same weights expanded per row (wn, cm) for the per-row entry points."""
+    from rein48_amd.a3c import kernels as K
+    rng = np.random.default_rng(seed)
+    b = rng.integers(1, 10, size=(T, n, 16)).astype(np.int8)
+    b[rng.random((T, n, 16)) < 0.4] = 0
+    boards = torch.from_numpy(b).to(DEV)
+    actions = torch.from_numpy(rng.integers(0, 4, size=(T, n)).astype(np.int8)).to(DEV)
+    rewards = torch.from_numpy(rng.normal(scale=2.0, size=(T, n)).astype(np.float32)).to(DEV)
+    values = torch.from_numpy(rng.normal(size=(T, n)).astype(np.float32)).to(DEV)
+    lengths = torch.from_numpy(rng.integers(1, T + 1, size=n).astype(np.int32)).to(DEV)
+    boot = torch.from_numpy(rng.normal(size=n).astype(np.float32)).to(DEV)
+    targets, seg, counts = K.segments(rewards, lengths, boot, 0.9, drop_last=reference,
+                                      values=values if reference else None, actions=actions if reference else None)
+    valid = torch.arange(T, device=DEV)[:, None] < lengths[None, :]
+    wn = torch.where(valid, seg[None, :, 0].expand(T, n), torch.zeros(())).contiguous()
+    cm = torch.where(valid, seg[None, :, 1].expand(T, n), torch.zeros(())).contiguous() if reference else None
+    return boards, actions, targets, seg, counts, wn, cm
+
+
+@pytest.mark.parametrize("T,n", [(37, 5003), (100, (1 << 18) + 7)])
+@pytest.mark.parametrize("mode", ["textbook", "reference"])
+def test_train_grad_per_board_weights_equal_per_row(mode, T, n):
+    """r48_cnn_train_grad_seg / r48_mlp_train_grad_seg (per-board weights, the row's step and board
+    tracked in-kernel) == r48_cnn_train_grad / r48_mlp_train_grad on the same weights expanded per
+    row, bit for bit (gradient and losses); a ragged row count (partial last tile) and, at 2^18 + 7
+    boards x 100 steps, many tiles per wave (the incremental step / board across tiles)."""
+    from rein48_amd.a3c.fused import cnn_train_grad, mlp_train_grad, pack_cnn_train
+    from rein48_amd.a3c.nets import ActorCriticCNN
+    ref = mode == "reference"
+    boards, actions, targets, seg, counts, wn, cm = _seg_case(T, n, 21, ref)
+    bv, av, tv = boards.view(-1, 16), actions.view(-1).contiguous(), targets.view(-1).contiguous()
+    torch.manual_seed(7)
+    net = ActorCriticCNN().to(DEV)
+    packed = pack_cnn_train(net)
+    for exponents in (False, True):
+        a = cnn_train_grad(net, bv, av, tv, wn.view(-1), None if cm is None else cm.view(-1), counts, exponents=exponents,
+                           n_boards=n, packed=packed)
+        b = cnn_train_grad(net, bv, av, tv, counts=counts, exponents=exponents, n_boards=n, packed=packed, seg=seg)
+        for x, y in zip(a[0] + [a[1], a[2]], b[0] + [b[1], b[2]]):
+            assert torch.equal(x, y)
+    mnet = _mlp_net()
+    for exponents in (False, True):
+        a = mlp_train_grad(mnet, bv, av, tv, wn.view(-1), None if cm is None else cm.view(-1), counts,
+                           exponents=exponents, n_boards=n)
+        b = mlp_train_grad(mnet, bv, av, tv, counts=counts, exponents=exponents, n_boards=n, seg=seg)
+        for x, y in zip(a, b):
+            assert torch.equal(x, y)
+
+
 # ---------------------------------------------------------------- the reference MLP, fused (r48_mlp.hip)
 def _mlp_net(seed=3):
     from rein48_amd.a3c.nets import ActorCriticMLP
