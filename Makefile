@@ -19,6 +19,9 @@ FLAGS_r48_policy ?= -mllvm -amdgpu-sched-strategy=max-ilp
 # the cell-grouped ResNet kernel keeps its 16 x 4 live accumulators in VGPRs (the epilogue reads
 # them without v_accvgpr_read) and the block input in AGPRs
 FLAGS_r48_resnet ?= -mllvm -amdgpu-mfma-vgpr-form=1
+# the MLP policy: its layer-1 f32 MFMA results stay in VGPRs for the VALU layer 2 (rollout 6.24 -> 5.90 ms
+# reference, 3.49 -> 3.39 ms textbook vs the AGPR form, profiles/r05/a3c/mlp_policy_f32_mfma_ab.txt)
+FLAGS_r48_mlp ?= -mllvm -amdgpu-mfma-vgpr-form=1
 # the MLP update: no SLP packing of its scalar f32 adds / FMAs (packed f32 VALU issues at half rate)
 FLAGS_r48_mlp_train ?= -fno-slp-vectorize
 

@@ -1,13 +1,14 @@
 // r48_mlp.hip -- the reference's own A3C network (algorithm/a3c/a3c.py:136-169, fp32) fused on gfx950.
 //
 // ActorCriticMLP (rein48_amd/a3c/nets.py): actor 16 -> 64 ReLU6 -> 4 ReLU (-> softmax), critic
-// 16 -> 64 ReLU6 -> 1, on the 16 raw tile values (a3c.py:37-39,139) or exponents. The network is
-// tiny (2,501 parameters, ~2.4 k FMAs per board) and fp32 like the reference, so it runs on the
-// VALU with ONE BOARD PER LANE: the weights are wave-uniform and come through the scalar cache into
-// SGPRs (s_load), the activations never leave the lane, and every FMA is a v_pk_fma_f32 over two
-// hidden units. No MFMA: an fp32 16x64 layer has no bf16 form that keeps the reference's fp32
-// numbers, and at one board per lane no data moves between lanes. (The fused update, which has
-// row contractions to do, is in r48_mlp_train.hip.)
+// 16 -> 64 ReLU6 -> 1, on the 16 raw tile values (a3c.py:37-39,139) or exponents, fp32 like the
+// reference. ONE BOARD PER LANE, 64 boards per wave: both 16 -> 64 layers (86 % of the FMAs) run on the
+// f32 MFMA (v_mfma_f32_32x32x2_f32: exact f32, bit for bit the k-ordered fmaf chain, at twice the rate
+// a packed-f32 VALU kernel reaches, and beside the VALU), the 64 -> 4 / 64 -> 1 layers, the draw and the
+// env step on the VALU (mlp_forward below). Round 4 ran everything as v_pk_fma_f32 chains with the
+// weights in SGPRs: rollout 6.68 -> 5.90 ms (reference loss, with V(s_t)), 3.92 -> 3.39 ms (textbook)
+// per 100 steps of 2^20 boards (profiles/r05/a3c/mlp_policy_f32_mfma_ab.txt). (The fused update, which
+// has row contractions to do, is in r48_mlp_train.hip.)
 //
 // k_mlp_forward   logits (post-ReLU, a3c.py:153), value, and the choose_action draw (a3c.py:89-93:
 //                 softmax + Philox inverse CDF, the r48_sample_actions contract) of every board
@@ -18,10 +19,8 @@
 //
 // Weight blob (rein48_amd/a3c/fused.py pack_mlp, 2,504 floats), grouped by hidden-unit PAIR p
 // (units 2p, 2p + 1): a1 [32 p][16 in][2] | a1.b [64] | a2 [32 p][4 out][2] | a2.b [4] |
-// c1 [32 p][16 in][2] | c1.b [64] | c2 [64] | c2.b [1] | pad -- one pair's weights are contiguous
-// (s_load_dwordx16 twice for its 32 layer-1 weights) and every SGPR pair feeds one packed FMA. The
-// pair loop is NOT unrolled: the scalar loads then stay next to their use instead of being
-// scheduled together (2,500 weights do not fit the SGPRs; they spilled into VGPR lanes).
+// c1 [32 p][16 in][2] | c1.b [64] | c2 [64] | c2.b [1] | pad; each kernel gathers the layer-1 A
+// operands of its lanes from it once (36 VGPRs) and stages the layer-2 weights in LDS by lane half.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -38,7 +37,7 @@ void set_last_error(const std::string &msg);
 
 namespace {
 
-typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int kBlock = 256;
 constexpr uint32_t kSampleTag = 0xA3Cu;   // r48_a3c.hip k_sample's draw tag
@@ -53,80 +52,105 @@ __device__ __forceinline__ void board_inputs(const r48::Board &b, float (&x)[16]
         x[c] = cell_input<MODE>((w[c >> 2] >> (8 * (c & 3))) & 0xFFu);
 }
 
-__device__ __forceinline__ f32x2 pair_at(const float *__restrict__ w, int off)
-{
-    return *reinterpret_cast<const f32x2 *>(w + off);
-}
-
 __device__ __forceinline__ float relu6(float a) { return fminf(fmaxf(a, 0.0f), 6.0f); }
 
-// One 16 -> 64 ReLU6 layer folded straight into its consumer: hidden units are formed two at a time
-// (one packed FMA chain per pair, inputs in order 0..15 after the bias) and immediately contracted
-// into the NO outputs as per-parity partial sums acc[k] = (sum over even units, sum over odd units).
-template <int NO>
-__device__ __forceinline__ void hidden_into(const float *__restrict__ w, int w1, int b1, int w2, const float (&x)[16],
-                                            f32x2 (&acc)[NO])
+// ---- the policy of a wave's 64 boards (lane l holds board l) ----
+// Layer 1 (16 -> 64 actor, 16 -> 64 critic) on the f32 MFMA: D[unit][board] = W1 . [1; x] per unit block
+// m (0, 1: actor units 32m..32m+31; 2, 3: critic) and board block nb (boards 32nb..32nb+31 of the wave),
+// nine v_mfma_f32_32x32x2_f32 K-steps: step 0 the bias (A = b1 in lane half 0, B = 1), step s >= 1
+// inputs 2(s-1) + h. An f32 MFMA is bit for bit the k-ordered fmaf chain, so every hidden unit is
+// fma(w15, x15, ... fma(w0, x0, b1)) -- one chain in input order. Layer 2 (64 -> 4 actor, 64 -> 1
+// critic) on the VALU: a lane holds 16 units of each block for one board (D rows 8(r >> 2) + 4h +
+// (r & 3)), contracts them with its half's layer-2 weights (LDS), and one v_permlane32_swap + add per
+// output sums the two halves into the lane that owns the board.
+
+// A operands: a[m][s] = W1[unit 32(m & 1) + (lane & 31) of net m >> 1][input 2(s - 1) + h], a[m][0] =
+// the bias in lane half 0 -- loaded once per kernel (36 VGPRs)
+__device__ __forceinline__ void load_layer1(const float *__restrict__ w, int lane, float (&a)[4][9])
 {
+    const int h = lane >> 5;
 #pragma unroll
-    for (int k = 0; k < NO; k++)
-        acc[k] = f32x2{0.0f, 0.0f};
-#pragma unroll 1
-    for (int p = 0; p < 32; p++) {
-        // four independent FMA chains over inputs f = q mod 4 (the bias starts chain 0), summed in a
-        // fixed order: a 16-long dependent chain per pair left the VALU waiting on its latency
-        f32x2 c4[4] = {pair_at(w, b1 + 2 * p), f32x2{0.0f, 0.0f}, f32x2{0.0f, 0.0f}, f32x2{0.0f, 0.0f}};
+    for (int m = 0; m < 4; m++) {
+        const int u = 32 * (m & 1) + (lane & 31), w1 = m < 2 ? kA1W : kC1W, b1 = m < 2 ? kA1B : kC1B;
+        a[m][0] = h ? 0.0f : w[b1 + u];
 #pragma unroll
-        for (int f = 0; f < 16; f++)
-            c4[f & 3] = __builtin_elementwise_fma(pair_at(w, w1 + 32 * p + 2 * f), f32x2{x[f], x[f]}, c4[f & 3]);
-        const f32x2 a = (c4[0] + c4[1]) + (c4[2] + c4[3]);
-        const f32x2 h = f32x2{relu6(a.x), relu6(a.y)};
-#pragma unroll
-        for (int k = 0; k < NO; k++)
-            acc[k] = __builtin_elementwise_fma(pair_at(w, w2 + (NO == 1 ? 2 * p : 8 * p + 2 * k)), h, acc[k]);
+        for (int s = 1; s < 9; s++)
+            a[m][s] = w[w1 + 32 * (u >> 1) + 2 * (2 * (s - 1) + h) + (u & 1)];
     }
 }
 
-// hidden_into for the actor (4 outputs) and the critic (1 output) in ONE pair loop: two independent
-// FMA chains per trip under one round of scalar loads (the update's forward, where the latency of the
-// loads is exposed at two waves per SIMD)
-__device__ __forceinline__ void hidden_both(const float *__restrict__ w, const float (&x)[16], f32x2 (&acc)[4], f32x2 &cv)
+// layer-2 weights by lane half h, actor block mm and D register r (unit u = 32 mm + 8(r >> 2) + 4h + (r & 3)):
+// a2l[(2h + mm) 16 + r] = a2[0..3][u], c2l[(2h + mm) 16 + r] = c2[u]; filled by the whole block
+__device__ __forceinline__ void stage_layer2(const float *__restrict__ w, float4 *a2l, float *c2l)
 {
-#pragma unroll
-    for (int k = 0; k < 4; k++)
-        acc[k] = f32x2{0.0f, 0.0f};
-    cv = f32x2{0.0f, 0.0f};
-#pragma unroll 1
-    for (int p = 0; p < 32; p++) {
-        f32x2 ca[4] = {pair_at(w, kA1B + 2 * p), f32x2{0.0f, 0.0f}, f32x2{0.0f, 0.0f}, f32x2{0.0f, 0.0f}};
-        f32x2 cc[4] = {pair_at(w, kC1B + 2 * p), f32x2{0.0f, 0.0f}, f32x2{0.0f, 0.0f}, f32x2{0.0f, 0.0f}};
-#pragma unroll
-        for (int f = 0; f < 16; f++) {
-            ca[f & 3] = __builtin_elementwise_fma(pair_at(w, kA1W + 32 * p + 2 * f), f32x2{x[f], x[f]}, ca[f & 3]);
-            cc[f & 3] = __builtin_elementwise_fma(pair_at(w, kC1W + 32 * p + 2 * f), f32x2{x[f], x[f]}, cc[f & 3]);
-        }
-        const f32x2 a = (ca[0] + ca[1]) + (ca[2] + ca[3]), c = (cc[0] + cc[1]) + (cc[2] + cc[3]);
-        const f32x2 h = f32x2{relu6(a.x), relu6(a.y)}, hc = f32x2{relu6(c.x), relu6(c.y)};
-#pragma unroll
-        for (int k = 0; k < 4; k++)
-            acc[k] = __builtin_elementwise_fma(pair_at(w, kA2W + 8 * p + 2 * k), h, acc[k]);
-        cv = __builtin_elementwise_fma(pair_at(w, kC2W + 2 * p), hc, cv);
+    const int t = threadIdx.x;
+    if (t < 64) {
+        const int h = t >> 5, mm = (t >> 4) & 1, r = t & 15;
+        const int u = 32 * mm + 8 * (r >> 2) + 4 * h + (r & 3), p = u >> 1, e = u & 1;
+        a2l[t] = make_float4(w[kA2W + 8 * p + e], w[kA2W + 8 * p + 2 + e], w[kA2W + 8 * p + 4 + e],
+                             w[kA2W + 8 * p + 6 + e]);
+        c2l[t] = w[kC2W + u];
     }
 }
 
-// logits z (post-ReLU) and, when VALUE, the critic's value of one board's inputs
+__device__ __forceinline__ float2 swap32(float lo, float hi)
+{
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(lo), __float_as_uint(hi), false, false);
+    return make_float2(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+
+// logits z (post-ReLU, a3c.py:153) and, when VALUE, the critic's value of the lane's board; every lane of
+// the wave must be active (padding lanes run on a valid duplicate board)
 template <bool VALUE>
-__device__ __forceinline__ void mlp_forward(const float *__restrict__ w, const float (&x)[16], float (&z)[4], float &v)
+__device__ __forceinline__ void mlp_forward(const float *__restrict__ w, const float (&a)[4][9], const float4 *a2l,
+                                            const float *c2l, int h, const float (&x)[16], float (&z)[4], float &v)
 {
-    f32x2 acc[4];
-    hidden_into<4>(w, kA1W, kA1B, kA2W, x, acc);
+    // B operands of board block 0 / 1: one swap per K-step turns the lanes' own inputs (2j, 2j + 1)
+    // into [own x_2j | partner's x_2j+1] and [partner's x_2j | own x_2j+1]
+    float b0[9], b1[9];
+    b0[0] = b1[0] = h ? 0.0f : 1.0f;
 #pragma unroll
-    for (int k = 0; k < 4; k++)
-        z[k] = fmaxf(w[kA2B + k] + (acc[k].x + acc[k].y), 0.0f);
+    for (int s = 1; s < 9; s++) {
+        const float2 q = swap32(x[2 * (s - 1)], x[2 * (s - 1) + 1]);
+        b0[s] = q.x;
+        b1[s] = q.y;
+    }
+    float zp[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}}, vp[2] = {0.f, 0.f};
+    constexpr int kM = VALUE ? 4 : 2;
+#pragma unroll
+    for (int m = 0; m < kM; m++) {
+        f32x16 d0 = {}, d1 = {};
+#pragma unroll
+        for (int s = 0; s < 9; s++) {
+            d0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[m][s], b0[s], d0, 0, 0, 0);
+            d1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[m][s], b1[s], d1, 0, 0, 0);
+        }
+        const int base = (2 * h + (m & 1)) * 16;
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+            const float h0 = relu6(d0[r]), h1 = relu6(d1[r]);
+            if (m < 2) {
+                const float4 wk = a2l[base + r];
+                zp[0][0] = fmaf(wk.x, h0, zp[0][0]), zp[1][0] = fmaf(wk.x, h1, zp[1][0]);
+                zp[0][1] = fmaf(wk.y, h0, zp[0][1]), zp[1][1] = fmaf(wk.y, h1, zp[1][1]);
+                zp[0][2] = fmaf(wk.z, h0, zp[0][2]), zp[1][2] = fmaf(wk.z, h1, zp[1][2]);
+                zp[0][3] = fmaf(wk.w, h0, zp[0][3]), zp[1][3] = fmaf(wk.w, h1, zp[1][3]);
+            } else {
+                const float wc = c2l[base + r];
+                vp[0] = fmaf(wc, h0, vp[0]), vp[1] = fmaf(wc, h1, vp[1]);
+            }
+        }
+    }
+    // the board's two halves: lanes 0-31 own block 0's boards, lanes 32-63 block 1's; half 0's part first
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const float2 q = swap32(zp[0][k], zp[1][k]);
+        z[k] = fmaxf(w[kA2B + k] + (q.x + q.y), 0.0f);
+    }
     v = 0.0f;
     if (VALUE) {
-        f32x2 c[1];
-        hidden_into<1>(w, kC1W, kC1B, kC2W, x, c);
-        v = w[kC2B] + (c[0].x + c[0].y);
+        const float2 q = swap32(vp[0], vp[1]);
+        v = w[kC2B] + (q.x + q.y);
     }
 }
 
@@ -161,15 +185,26 @@ __global__ __launch_bounds__(kBlock) void k_mlp_forward(const int8_t *__restrict
                                                         float *__restrict__ value, int8_t *__restrict__ actions,
                                                         int64_t gid0, uint32_t pk0, uint32_t pk1, uint32_t ctr)
 {
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n)
-        return;
+    __shared__ float4 a2l[64];
+    __shared__ float c2l[64];
+    stage_layer2(w, a2l, c2l);
+    __syncthreads();
+    const int lane = threadIdx.x & 63, h = lane >> 5;
+    const int64_t i0 = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if ((i0 & ~63ll) >= n)
+        return;   // a whole wave past the end (wave-uniform)
+    const bool live = i0 < n;
+    const int64_t i = live ? i0 : n - 1;   // padding lanes: a valid duplicate, nothing stored
+    float a[4][9];
+    load_layer1(w, lane, a);
     float x[16], z[4], v;
     board_inputs<MODE>(load_board(boards, i), x);
-    if (value)
-        mlp_forward<true>(w, x, z, v);
+    if (value)   // wave-uniform
+        mlp_forward<true>(w, a, a2l, c2l, h, x, z, v);
     else
-        mlp_forward<false>(w, x, z, v);
+        mlp_forward<false>(w, a, a2l, c2l, h, x, z, v);
+    if (!live)
+        return;
     if (logits)
         *reinterpret_cast<float4 *>(logits + 4 * i) = make_float4(z[0], z[1], z[2], z[3]);
     if (value)
@@ -189,35 +224,49 @@ __global__ __launch_bounds__(kBlock) void k_mlp_rollout(int8_t *__restrict__ boa
                                                         uint32_t pk1, uint32_t ctr0, uint32_t ek0, uint32_t ek1,
                                                         uint32_t step0)
 {
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n)
-        return;
+    __shared__ float4 a2l[64];
+    __shared__ float c2l[64];
+    stage_layer2(w, a2l, c2l);
+    __syncthreads();
+    const int lane = threadIdx.x & 63, h = lane >> 5;
+    const int64_t i0 = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if ((i0 & ~63ll) >= n)
+        return;   // a whole wave past the end (wave-uniform)
+    const bool live = i0 < n;
+    const int64_t i = live ? i0 : n - 1;   // padding lanes step a valid duplicate and store nothing
+    float a[4][9];
+    load_layer1(w, lane, a);
     const uint64_t gid = (uint64_t)(gid0 + i);
     r48::Board b = load_board(boards, i);
     int32_t len = T;
     for (int32_t t = 0; t < T; t++) {
         const int64_t at = (int64_t)t * n + i;
-        store_board(traj, at, b);
+        if (live)
+            store_board(traj, at, b);
         float x[16], z[4], v;
         board_inputs<MODE>(b, x);
-        mlp_forward<VALUES>(w, x, z, v);
-        if (VALUES)
-            values[at] = v;
+        mlp_forward<VALUES>(w, a, a2l, c2l, h, x, z, v);
         const uint32_t act = sample_action(z, gid, ctr0 + (uint32_t)t, pk0, pk1);
         uint32_t dx, dy;
         r48::step_draw(gid, step0 + (uint32_t)t, ek0, ek1, dx, dy);
         const r48::StepOut o = r48::step_board<REWARD, false, true>(b, act, dy, (dx & 0x3FFFFFFFu) < r48::kFourThresh30);
-        actions[at] = (int8_t)act;
-        done[at] = (uint8_t)o.done;
-        if (reward)   // merge reward as fp32 (exact: < 2^24)
-            reward[at] = REWARD ? (float)o.reward : 0.0f;
+        if (live) {
+            if (VALUES)
+                values[at] = v;
+            actions[at] = (int8_t)act;
+            done[at] = (uint8_t)o.done;
+            if (reward)   // merge reward as fp32 (exact: < 2^24)
+                reward[at] = REWARD ? (float)o.reward : 0.0f;
+        }
         if (o.done && len == T)
             len = t + 1;   // through the first done step (a3c.py:201)
     }
-    store_board(traj, (int64_t)T * n + i, b);
-    store_board(boards, i, b);
-    if (lengths)
-        lengths[i] = len;
+    if (live) {
+        store_board(traj, (int64_t)T * n + i, b);
+        store_board(boards, i, b);
+        if (lengths)
+            lengths[i] = len;
+    }
 }
 
 
