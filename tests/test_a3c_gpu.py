@@ -96,10 +96,12 @@ def test_discounted_returns_vector_path_equals_scalar_path(drop_last):
     assert torch.equal(out4, out1)
 
 
-def test_discounted_returns_match_reference_golden():
-    """r48_discounted_returns (drop-last mode) vs the reference's own _get_target_value_list
-    outputs (tests/golden/a3c_golden.json, made by executing a3c.py:246-256), all 48 cases in
-    one launch, fp32 tolerance rtol=1e-5."""
+@pytest.mark.parametrize("segments", [False, True])
+def test_discounted_returns_match_reference_golden(segments):
+    """r48_discounted_returns (drop-last mode) -- and the fused update's segment pass r48_a3c_segments,
+    whose targets must be the same -- vs the reference's own _get_target_value_list outputs
+    (tests/golden/a3c_golden.json, made by executing a3c.py:246-256), all 48 cases in one launch, fp32
+    tolerance rtol=1e-5; the segment pass's per-board weights at those lengths as well."""
     import json
     import os
     from rein48_amd.a3c import kernels as K
@@ -110,8 +112,16 @@ def test_discounted_returns_match_reference_golden():
         rewards[:len(c["rewards"]), i] = c["rewards"]
     lengths = np.array([len(c["rewards"]) for c in g], np.int32)
     boot = np.array([c["last_target_value"] for c in g], np.float32)
-    out = K.discounted_returns(torch.from_numpy(rewards).to(DEV), torch.from_numpy(lengths).to(DEV),
-                               torch.from_numpy(boot).to(DEV), 0.9, drop_last=True).cpu().numpy()
+    args = (torch.from_numpy(rewards).to(DEV), torch.from_numpy(lengths).to(DEV), torch.from_numpy(boot).to(DEV), 0.9)
+    if segments:
+        out, seg, _ = K.segments(*args, drop_last=True)
+        seg = seg.cpu()
+        assert torch.equal(seg[:, 2].view(torch.int32), torch.from_numpy(lengths))
+        w0 = (1.0 / torch.from_numpy(lengths).float()) * torch.tensor(1.0 / n, dtype=torch.float32)
+        assert torch.equal(seg[:, 0], w0)
+        out = out.cpu().numpy()
+    else:
+        out = K.discounted_returns(*args, drop_last=True).cpu().numpy()
     for i, c in enumerate(g):
         L = lengths[i]
         np.testing.assert_allclose(out[:L, i], c["targets"], rtol=1e-5, atol=1e-4)
