@@ -616,6 +616,30 @@ def test_fused_mlp_forward_matches_torch_and_oracle(exponents):
     assert torch.equal(a, act)
 
 
+@pytest.mark.parametrize("exponents", [False, True])
+def test_fused_mlp_forward_is_per_board(exponents):
+    """The MFMA policy works on 64-board waves (lane l = board l, padding lanes on a duplicate board):
+    every output must still depend on its own board only -- the first k boards of a batch give the
+    same logits, values and draws bit for bit as the whole batch, for k = 1 (63 padding lanes), 63,
+    64, 65 and a ragged 4,099, at any board offset (gid0 keys the draws)."""
+    from rein48_amd.a3c.fused import mlp_forward, pack_mlp
+    net = _mlp_net(5)
+    rng = np.random.default_rng(9)
+    b = rng.integers(1, 12, size=(5000, 16)).astype(np.int8)
+    b[rng.random((5000, 16)) < 0.4] = 0
+    boards = torch.from_numpy(b).to(DEV)
+    w = pack_mlp(net)
+    full = mlp_forward(boards, w, exponents=exponents, actions=True, seed=3, ctr=7, gid0=100)
+    for k in (1, 63, 64, 65, 4099):
+        part = mlp_forward(boards[:k].contiguous(), w, exponents=exponents, actions=True, seed=3, ctr=7, gid0=100)
+        for x, y in zip(part, full):
+            assert torch.equal(x, y[:k]), k
+    # an offset slice: boards 37.. keyed from gid0 = 137
+    part = mlp_forward(boards[37:37 + 200].contiguous(), w, exponents=exponents, actions=True, seed=3, ctr=7, gid0=137)
+    for x, y in zip(part, full):
+        assert torch.equal(x, y[37:237])
+
+
 @pytest.mark.parametrize("mode,n", [("textbook", 5003), ("reference", 4099), ("textbook", (1 << 20) + 3)])
 def test_mlp_rollout_megakernel_equals_per_step_kernels(mode, n):
     """r48_mlp_rollout (all T steps of every board in one launch) == T x (r48_mlp_policy_forward +
