@@ -20,7 +20,8 @@
 // Weight blob (rein48_amd/a3c/fused.py pack_mlp, 2,504 floats), grouped by hidden-unit PAIR p
 // (units 2p, 2p + 1): a1 [32 p][16 in][2] | a1.b [64] | a2 [32 p][4 out][2] | a2.b [4] |
 // c1 [32 p][16 in][2] | c1.b [64] | c2 [64] | c2.b [1] | pad; each kernel gathers the layer-1 A
-// operands of its lanes from it once (36 VGPRs) and stages the layer-2 weights in LDS by lane half.
+// operands of its lanes from it once (32 VGPRs) and stages the layer-1 biases and layer-2 weights in
+// LDS by lane half.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -55,35 +56,39 @@ __device__ __forceinline__ void board_inputs(const r48::Board &b, float (&x)[16]
 __device__ __forceinline__ float relu6(float a) { return fminf(fmaxf(a, 0.0f), 6.0f); }
 
 // ---- the policy of a wave's 64 boards (lane l holds board l) ----
-// Layer 1 (16 -> 64 actor, 16 -> 64 critic) on the f32 MFMA: D[unit][board] = W1 . [1; x] per unit block
+// Layer 1 (16 -> 64 actor, 16 -> 64 critic) on the f32 MFMA: D[unit][board] = W1 . x + b1 per unit block
 // m (0, 1: actor units 32m..32m+31; 2, 3: critic) and board block nb (boards 32nb..32nb+31 of the wave),
-// nine v_mfma_f32_32x32x2_f32 K-steps: step 0 the bias (A = b1 in lane half 0, B = 1), step s >= 1
-// inputs 2(s-1) + h. An f32 MFMA is bit for bit the k-ordered fmaf chain, so every hidden unit is
-// fma(w15, x15, ... fma(w0, x0, b1)) -- one chain in input order. Layer 2 (64 -> 4 actor, 64 -> 1
+// eight v_mfma_f32_32x32x2_f32 K-steps (inputs 2s + h) from C = the bias (LDS). An f32 MFMA is bit for
+// bit the k-ordered fmaf chain, so every hidden unit is fma(w15, x15, ... fma(w0, x0, b1)) -- one chain
+// in input order. Layer 2 (64 -> 4 actor, 64 -> 1
 // critic) on the VALU: a lane holds 16 units of each block for one board (D rows 8(r >> 2) + 4h +
 // (r & 3)), contracts them with its half's layer-2 weights (LDS), and one v_permlane32_swap + add per
 // output sums the two halves into the lane that owns the board.
 
-// A operands: a[m][s] = W1[unit 32(m & 1) + (lane & 31) of net m >> 1][input 2(s - 1) + h], a[m][0] =
-// the bias in lane half 0 -- loaded once per kernel (36 VGPRs)
-__device__ __forceinline__ void load_layer1(const float *__restrict__ w, int lane, float (&a)[4][9])
+// A operands: a[m][s] = W1[unit 32(m & 1) + (lane & 31) of net m >> 1][input 2s + h] -- loaded once per
+// kernel (32 VGPRs)
+__device__ __forceinline__ void load_layer1(const float *__restrict__ w, int lane, float (&a)[4][8])
 {
     const int h = lane >> 5;
 #pragma unroll
     for (int m = 0; m < 4; m++) {
-        const int u = 32 * (m & 1) + (lane & 31), w1 = m < 2 ? kA1W : kC1W, b1 = m < 2 ? kA1B : kC1B;
-        a[m][0] = h ? 0.0f : w[b1 + u];
+        const int u = 32 * (m & 1) + (lane & 31), w1 = m < 2 ? kA1W : kC1W;
 #pragma unroll
-        for (int s = 1; s < 9; s++)
-            a[m][s] = w[w1 + 32 * (u >> 1) + 2 * (2 * (s - 1) + h) + (u & 1)];
+        for (int s = 0; s < 8; s++)
+            a[m][s] = w[w1 + 32 * (u >> 1) + 2 * (2 * s + h) + (u & 1)];
     }
 }
 
 // layer-2 weights by lane half h, actor block mm and D register r (unit u = 32 mm + 8(r >> 2) + 4h + (r & 3)):
-// a2l[(2h + mm) 16 + r] = a2[0..3][u], c2l[(2h + mm) 16 + r] = c2[u]; filled by the whole block
-__device__ __forceinline__ void stage_layer2(const float *__restrict__ w, float4 *a2l, float *c2l)
+// a2l[(2h + mm) 16 + r] = a2[0..3][u], c2l[(2h + mm) 16 + r] = c2[u]; and the layer-1 biases as the MFMA's
+// C operand, b1l[(2m + h) 16 + r] = bias of D register r's unit in block m; filled by the whole block
+__device__ __forceinline__ void stage_layer2(const float *__restrict__ w, float4 *a2l, float *c2l, float *b1l)
 {
     const int t = threadIdx.x;
+    if (t < 128) {
+        const int m = t >> 5, h = (t >> 4) & 1, r = t & 15;
+        b1l[t] = w[(m < 2 ? kA1B : kC1B) + 32 * (m & 1) + 8 * (r >> 2) + 4 * h + (r & 3)];
+    }
     if (t < 64) {
         const int h = t >> 5, mm = (t >> 4) & 1, r = t & 15;
         const int u = 32 * mm + 8 * (r >> 2) + 4 * h + (r & 3), p = u >> 1, e = u & 1;
@@ -102,16 +107,16 @@ __device__ __forceinline__ float2 swap32(float lo, float hi)
 // logits z (post-ReLU, a3c.py:153) and, when VALUE, the critic's value of the lane's board; every lane of
 // the wave must be active (padding lanes run on a valid duplicate board)
 template <bool VALUE>
-__device__ __forceinline__ void mlp_forward(const float *__restrict__ w, const float (&a)[4][9], const float4 *a2l,
-                                            const float *c2l, int h, const float (&x)[16], float (&z)[4], float &v)
+__device__ __forceinline__ void mlp_forward(const float *__restrict__ w, const float (&a)[4][8], const float4 *a2l,
+                                            const float *c2l, const float *b1l, int h, const float (&x)[16],
+                                            float (&z)[4], float &v)
 {
-    // B operands of board block 0 / 1: one swap per K-step turns the lanes' own inputs (2j, 2j + 1)
-    // into [own x_2j | partner's x_2j+1] and [partner's x_2j | own x_2j+1]
-    float b0[9], b1[9];
-    b0[0] = b1[0] = h ? 0.0f : 1.0f;
+    // B operands of board block 0 / 1: one swap per K-step turns the lanes' own inputs (2s, 2s + 1)
+    // into [own x_2s | partner's x_2s+1] and [partner's x_2s | own x_2s+1]
+    float b0[8], b1[8];
 #pragma unroll
-    for (int s = 1; s < 9; s++) {
-        const float2 q = swap32(x[2 * (s - 1)], x[2 * (s - 1) + 1]);
+    for (int s = 0; s < 8; s++) {
+        const float2 q = swap32(x[2 * s], x[2 * s + 1]);
         b0[s] = q.x;
         b1[s] = q.y;
     }
@@ -119,9 +124,15 @@ __device__ __forceinline__ void mlp_forward(const float *__restrict__ w, const f
     constexpr int kM = VALUE ? 4 : 2;
 #pragma unroll
     for (int m = 0; m < kM; m++) {
-        f32x16 d0 = {}, d1 = {};
+        f32x16 d0;   // C = the bias of each D register's unit: the chain starts at b1, as the reference
 #pragma unroll
-        for (int s = 0; s < 9; s++) {
+        for (int q = 0; q < 4; q++) {
+            const float4 bq = reinterpret_cast<const float4 *>(b1l + (2 * m + h) * 16)[q];
+            d0[4 * q] = bq.x, d0[4 * q + 1] = bq.y, d0[4 * q + 2] = bq.z, d0[4 * q + 3] = bq.w;
+        }
+        f32x16 d1 = d0;
+#pragma unroll
+        for (int s = 0; s < 8; s++) {
             d0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[m][s], b0[s], d0, 0, 0, 0);
             d1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[m][s], b1[s], d1, 0, 0, 0);
         }
@@ -187,7 +198,8 @@ __global__ __launch_bounds__(kBlock) void k_mlp_forward(const int8_t *__restrict
 {
     __shared__ float4 a2l[64];
     __shared__ float c2l[64];
-    stage_layer2(w, a2l, c2l);
+    __shared__ __attribute__((aligned(16))) float b1l[128];
+    stage_layer2(w, a2l, c2l, b1l);
     __syncthreads();
     const int lane = threadIdx.x & 63, h = lane >> 5;
     const int64_t i0 = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -195,14 +207,14 @@ __global__ __launch_bounds__(kBlock) void k_mlp_forward(const int8_t *__restrict
         return;   // a whole wave past the end (wave-uniform)
     const bool live = i0 < n;
     const int64_t i = live ? i0 : n - 1;   // padding lanes: a valid duplicate, nothing stored
-    float a[4][9];
+    float a[4][8];
     load_layer1(w, lane, a);
     float x[16], z[4], v;
     board_inputs<MODE>(load_board(boards, i), x);
     if (value)   // wave-uniform
-        mlp_forward<true>(w, a, a2l, c2l, h, x, z, v);
+        mlp_forward<true>(w, a, a2l, c2l, b1l, h, x, z, v);
     else
-        mlp_forward<false>(w, a, a2l, c2l, h, x, z, v);
+        mlp_forward<false>(w, a, a2l, c2l, b1l, h, x, z, v);
     if (!live)
         return;
     if (logits)
@@ -215,6 +227,18 @@ __global__ __launch_bounds__(kBlock) void k_mlp_forward(const int8_t *__restrict
 
 // VALUES: also V(boards[t]) of every step (the reference loss's td sums need V of the training
 // states before the gradient pass; rollout_values in trainer.py)
+// The two waves of a SIMD run identical step loops from the same start: odd hardware wave slots issue at
+// raised priority, so one wave runs ahead and the other fills its gaps instead of both reaching the
+// MFMA-heavy layer 1 together (with the bias as the C operand: rollout 5.96 -> 5.78 ms, reference loss,
+// n = 6, bit-identical; profiles/r05/a3c/mlp_policy_bias_c_desync_ab.txt)
+__device__ __forceinline__ void desync_waves()
+{
+    uint32_t hw;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    if (hw & 1)
+        __builtin_amdgcn_s_setprio(1);
+}
+
 template <int MODE, bool REWARD, bool VALUES>
 __global__ __launch_bounds__(kBlock) void k_mlp_rollout(int8_t *__restrict__ boards, int64_t n, int32_t T,
                                                         const float *__restrict__ w, int8_t *__restrict__ traj,
@@ -226,7 +250,8 @@ __global__ __launch_bounds__(kBlock) void k_mlp_rollout(int8_t *__restrict__ boa
 {
     __shared__ float4 a2l[64];
     __shared__ float c2l[64];
-    stage_layer2(w, a2l, c2l);
+    __shared__ __attribute__((aligned(16))) float b1l[128];
+    stage_layer2(w, a2l, c2l, b1l);
     __syncthreads();
     const int lane = threadIdx.x & 63, h = lane >> 5;
     const int64_t i0 = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -234,8 +259,9 @@ __global__ __launch_bounds__(kBlock) void k_mlp_rollout(int8_t *__restrict__ boa
         return;   // a whole wave past the end (wave-uniform)
     const bool live = i0 < n;
     const int64_t i = live ? i0 : n - 1;   // padding lanes step a valid duplicate and store nothing
-    float a[4][9];
+    float a[4][8];
     load_layer1(w, lane, a);
+    desync_waves();
     const uint64_t gid = (uint64_t)(gid0 + i);
     r48::Board b = load_board(boards, i);
     int32_t len = T;
@@ -245,7 +271,7 @@ __global__ __launch_bounds__(kBlock) void k_mlp_rollout(int8_t *__restrict__ boa
             store_board(traj, at, b);
         float x[16], z[4], v;
         board_inputs<MODE>(b, x);
-        mlp_forward<VALUES>(w, a, a2l, c2l, h, x, z, v);
+        mlp_forward<VALUES>(w, a, a2l, c2l, b1l, h, x, z, v);
         const uint32_t act = sample_action(z, gid, ctr0 + (uint32_t)t, pk0, pk1);
         uint32_t dx, dy;
         r48::step_draw(gid, step0 + (uint32_t)t, ek0, ek1, dx, dy);
