@@ -53,7 +53,9 @@ __device__ __forceinline__ void board_inputs(const r48::Board &b, float (&x)[16]
         x[c] = cell_input<MODE>((w[c >> 2] >> (8 * (c & 3))) & 0xFFu);
 }
 
-__device__ __forceinline__ float relu6(float a) { return fminf(fmaxf(a, 0.0f), 6.0f); }
+// ReLU6 as one v_med3_f32: fminf(fmaxf(a, 0), 6) on an MFMA result also costs a v_max_f32 a, a, a (the
+// IEEE-mode quieting of a possible signalling NaN) per value -- 128 extra VALU per rollout step
+__device__ __forceinline__ float relu6(float a) { return __builtin_amdgcn_fmed3f(a, 0.0f, 6.0f); }
 
 // ---- the policy of a wave's 64 boards (lane l holds board l) ----
 // Layer 1 (16 -> 64 actor, 16 -> 64 critic) on the f32 MFMA: D[unit][board] = W1 . x + b1 per unit block
