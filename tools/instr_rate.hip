@@ -74,6 +74,44 @@ __device__ __forceinline__ void o_cmp64_cnd64(uint32_t &x, uint32_t k, uint32_t)
     asm volatile("v_cmp_gt_u32_e64 %1, %0, %2\n\tv_cndmask_b32_e64 %0, %0, %2, %1" : "+v"(x), "=&s"(m) : "v"(k));
 }
 OP2(o_sub_lit, "v_sub_u32 %0, 0x80808080, %0")
+OP2(o_xad, "v_xad_u32 %0, %0, %1, %2")
+OP2(o_add_lshl, "v_add_lshl_u32 %0, %0, %1, 3")
+OP2(o_med3, "v_med3_u32 %0, %0, %1, %2")
+OP2(o_subrev, "v_subrev_u32 %0, %0, %1")
+__device__ __forceinline__ void o_sub_sgpr(uint32_t &x, uint32_t k, uint32_t k2)
+{
+    asm volatile("v_sub_u32 %0, %1, %0" : "+v"(x) : "s"(__builtin_amdgcn_readfirstlane(k2)));
+}
+__device__ __forceinline__ void o_bitop3_vvs_s(uint32_t &x, uint32_t k, uint32_t k2)
+{
+    asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0xc8" : "+v"(x) : "v"(k), "s"(__builtin_amdgcn_readfirstlane(k2)));
+}
+__device__ __forceinline__ void o_add_e64_s(uint32_t &x, uint32_t k, uint32_t k2)
+{
+    asm volatile("v_add_u32_e64 %0, %1, %0" : "+v"(x) : "s"(__builtin_amdgcn_readfirstlane(k2)));
+}
+__device__ __forceinline__ void o_mad64_s(uint32_t &x, uint32_t k, uint32_t k2)
+{
+    uint64_t r;
+    asm volatile("v_mad_u64_u32 %0, vcc, %1, %2, 0" : "=v"(r) : "v"(x), "s"(__builtin_amdgcn_readfirstlane(k2)) : "vcc");
+    x = (uint32_t)(r >> 32);
+}
+__device__ __forceinline__ void o_xor_inl(uint32_t &x, uint32_t k, uint32_t k2)
+{
+    asm volatile("v_xor_b32 %0, 64, %0" : "+v"(x));
+}
+__device__ __forceinline__ void o_mix_sv(uint32_t &x, uint32_t k, uint32_t k2)
+{
+    asm volatile("v_sub_u32 %0, %1, %0\n\tv_add_u32 %0, %0, %2" : "+v"(x) : "s"(__builtin_amdgcn_readfirstlane(k2)), "v"(k));
+}
+__device__ __forceinline__ void o_mix_vv(uint32_t &x, uint32_t k, uint32_t k2)
+{
+    asm volatile("v_sub_u32 %0, %1, %0\n\tv_add_u32 %0, %0, %2" : "+v"(x) : "v"(k2), "v"(k));
+}
+__device__ __forceinline__ void o_and_sgpr(uint32_t &x, uint32_t k, uint32_t k2)
+{
+    asm volatile("v_and_b32 %0, %1, %0" : "+v"(x) : "s"(__builtin_amdgcn_readfirstlane(k2)));
+}
 OP2(o_and_lit, "v_and_b32 %0, 0x80808080, %0")
 OP2(o_bitop3_vvs, "v_bitop3_b32 %0, %0, %1, %2 bitop3:0xc8")
 __device__ __forceinline__ void o_nop_add(uint32_t &x, uint32_t k, uint32_t)
@@ -98,7 +136,7 @@ __device__ __forceinline__ void o_mad64(uint32_t &x, uint32_t k, uint32_t)
     X(o_mulu24) X(o_bcnt) X(o_cnd) X(o_cmp_cnd) X(o_lshl) X(o_lshr) X(o_lshlv) X(o_ashr) X(o_lshl_or)         \
     X(o_lshl_add) X(o_and_or) X(o_or3) X(o_add3) X(o_alignbit) X(o_bfe) X(o_min) X(o_max3) X(o_sad) X(o_msad)  \
     X(o_pkadd) X(o_pkmax) X(o_dot4) X(o_mov) X(o_cmp_vcc) X(o_addco) X(o_sdwa_add) X(o_mad64) X(o_cnd64) X(o_cmp64_cnd64) \
-    X(o_sub_lit) X(o_and_lit) X(o_bitop3_vvs) X(o_nop_add)
+    X(o_sub_lit) X(o_and_lit) X(o_bitop3_vvs) X(o_nop_add) X(o_xad) X(o_add_lshl) X(o_med3) X(o_subrev) X(o_sub_sgpr) X(o_and_sgpr) X(o_bitop3_vvs_s) X(o_add_e64_s) X(o_mad64_s) X(o_xor_inl) X(o_mix_sv) X(o_mix_vv)
 #define DEF(N) KERNEL(N, N)
 LIST(DEF)
 
