@@ -124,20 +124,28 @@ __device__ __forceinline__ void mlp_forward(const float *__restrict__ w, const f
     }
     float zp[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}}, vp[2] = {0.f, 0.f};
     constexpr int kM = VALUE ? 4 : 2;
-#pragma unroll
-    for (int m = 0; m < kM; m++) {
-        f32x16 d0;   // C = the bias of each D register's unit: the chain starts at b1, as the reference
+    // Software pipeline over the 32-unit blocks: block m + 1's MFMA chains are issued before block m's
+    // ReLU6 + layer-2 VALU (two D register pairs)...
+    f32x16 D0[2], D1[2];
+    auto issue = [&](int m, f32x16 &d0, f32x16 &d1) {
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             const float4 bq = reinterpret_cast<const float4 *>(b1l + (2 * m + h) * 16)[q];
             d0[4 * q] = bq.x, d0[4 * q + 1] = bq.y, d0[4 * q + 2] = bq.z, d0[4 * q + 3] = bq.w;
         }
-        f32x16 d1 = d0;
+        d1 = d0;
 #pragma unroll
         for (int s = 0; s < 8; s++) {
             d0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[m][s], b0[s], d0, 0, 0, 0);
             d1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[m][s], b1[s], d1, 0, 0, 0);
         }
+    };
+    issue(0, D0[0], D1[0]);
+#pragma unroll
+    for (int m = 0; m < kM; m++) {
+        if (m + 1 < kM)
+            issue(m + 1, D0[(m + 1) & 1], D1[(m + 1) & 1]);
+        const f32x16 &d0 = D0[m & 1], &d1 = D1[m & 1];
         const int base = (2 * h + (m & 1)) * 16;
 #pragma unroll
         for (int r = 0; r < 16; r++) {
@@ -151,6 +159,19 @@ __device__ __forceinline__ void mlp_forward(const float *__restrict__ w, const f
             } else {
                 const float wc = c2l[base + r];
                 vp[0] = fmaf(wc, h0, vp[0]), vp[1] = fmaf(wc, h1, vp[1]);
+            }
+        }
+        // ...and the scheduler is told to interleave them: one MFMA of block m + 1, then that many VALU of
+        // block m (its 160 / 64 instructions over the next block's 16 MFMAs). Left alone it issues all
+        // MFMAs first and the ReLU6 / layer-2 VALU after them.
+        if (m + 1 < kM) {
+#pragma unroll
+            for (int i = 0; i < 16; i++) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
+                if (m < 2)
+                    __builtin_amdgcn_sched_group_barrier(0x002, 10, 0);   // VALU
+                else
+                    __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
             }
         }
     }
