@@ -45,8 +45,8 @@
 // The weight-fragment fences (r48_cnn_common.h wfence) also let global memory instructions cross
 // here (mask 0x416 instead of 0x406): the next tile's row loads are then placed by the scheduler
 // instead of staying pinned between two MFMAs, which one wave per SIMD cannot hide. Same
-// instructions otherwise, bit-identical gradients; 21.79 -> 21.16 ms per 1e8 rows pooled over two
-// boxes, faster in 10 of 10 paired runs (profiles/r05/a3c/train/fence_mask_vmem_ab.txt).
+// instructions otherwise, bit-identical gradients; 21.82 -> 21.19 ms per 1e8 rows pooled over three
+// boxes, faster in 14 of 14 paired runs (profiles/r05/a3c/train/fence_mask_vmem_ab.txt).
 #ifndef R48_WFENCE
 #define R48_WFENCE 0x416
 #endif
