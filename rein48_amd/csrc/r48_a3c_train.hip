@@ -42,13 +42,15 @@
 #include <string>
 
 #include "../../include/rein48.h"
-// The weight-fragment fences (r48_cnn_common.h wfence) also let global memory instructions cross
-// here (mask 0x416 instead of 0x406): the next tile's row loads are then placed by the scheduler
-// instead of staying pinned between two MFMAs, which one wave per SIMD cannot hide. Same
-// instructions otherwise, bit-identical gradients; 21.82 -> 21.19 ms per 1e8 rows pooled over three
-// boxes, faster in 14 of 14 paired runs (profiles/r05/a3c/train/fence_mask_vmem_ab.txt).
+// The weight-fragment fences (r48_cnn_common.h wfence) also let global memory instructions and LDS
+// writes cross here (mask 0x616 instead of 0x406): the next tile's row loads and the image stores
+// are then placed by the scheduler instead of staying pinned between two MFMAs, which one wave per
+// SIMD cannot hide; the LDS fragment reads and the MFMAs keep their order. Same instructions
+// otherwise, bit-identical gradients: VMEM (0x416) 21.82 -> 21.19 ms per 1e8 rows pooled over three
+// boxes (14 of 14 paired runs faster), + LDS writes (0x616) 21.95 -> 21.18 vs 0x416 over two more
+// (10 of 10) (profiles/r05/a3c/train/fence_mask_vmem_ab.txt).
 #ifndef R48_WFENCE
-#define R48_WFENCE 0x416
+#define R48_WFENCE 0x616
 #endif
 #include "r48_cnn_common.h"
 #include "r48_host.h"
