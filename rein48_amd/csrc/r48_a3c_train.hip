@@ -48,7 +48,9 @@
 // SIMD cannot hide; the LDS fragment reads and the MFMAs keep their order. Same instructions
 // otherwise, bit-identical gradients: VMEM (0x416) 21.82 -> 21.19 ms per 1e8 rows pooled over three
 // boxes (14 of 14 paired runs faster), + LDS writes (0x616) 21.95 -> 21.18 vs 0x416 over two more
-// (10 of 10) (profiles/r05/a3c/train/fence_mask_vmem_ab.txt).
+// (10 of 10) (profiles/r05/a3c/train/fence_mask_vmem_ab.txt). The kernel's own phase fences (the
+// epilogue / transpose points of conv1 and the dh2 phase) use the same mask instead of a full
+// barrier: 22.22 -> 21.53 ms per 1e8 rows over two more boxes (10 of 10).
 #ifndef R48_WFENCE
 #define R48_WFENCE 0x616
 #endif
@@ -265,7 +267,7 @@ __device__ __forceinline__ void fwd_conv1(const uint4 *w, const float *b, int la
             wfence();
             nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, x, b1, 0, 0, 0);
         }
-        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_sched_barrier(R48_WFENCE);
         h1[R][0] = acc_to_frag_relu(acc, 0);
         h1[R][1] = acc_to_frag_relu(acc, 1);
         acc = nxt;
@@ -573,7 +575,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
                             acc16_a(db2, dh2t[b >> 1][b & 1][s], (b & 1) ? sel1 : sel0);
                     }
                 }
-                __builtin_amdgcn_sched_barrier(0);
+                __builtin_amdgcn_sched_barrier(R48_WFENCE);
                 if (m < 8) {
                     const int p = m >> 1, g = m & 1;
                     dh2[p][g][0] = mask_pk(acc_to_frag(acc, 0), h2[p][g][0]);
@@ -582,7 +584,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
                     store_frag(my, la, 64 * p + 32 * g + 16, dh2[p][g][1]);
                     dh2t[p][g][0] = trr(my, la, m, 0);
                     dh2t[p][g][1] = trr(my, la, m, 1);
-                    __builtin_amdgcn_sched_barrier(0);
+                    __builtin_amdgcn_sched_barrier(R48_WFENCE);
                 }
                 acc = nxt;
             }
