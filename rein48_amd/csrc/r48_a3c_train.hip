@@ -43,14 +43,12 @@
 
 #include "../../include/rein48.h"
 // The weight-fragment fences (r48_cnn_common.h wfence) also let global memory instructions and LDS
-// writes cross here (mask 0x616 instead of 0x406): the next tile's row loads and the image stores
-// are then placed by the scheduler instead of staying pinned between two MFMAs, which one wave per
-// SIMD cannot hide; the LDS fragment reads and the MFMAs keep their order. Same instructions
-// otherwise, bit-identical gradients: VMEM (0x416) 21.82 -> 21.19 ms per 1e8 rows pooled over three
-// boxes (14 of 14 paired runs faster), + LDS writes (0x616) 21.95 -> 21.18 vs 0x416 over two more
-// (10 of 10) (profiles/r05/a3c/train/fence_mask_vmem_ab.txt). The kernel's own phase fences (the
-// epilogue / transpose points of conv1 and the dh2 phase) use the same mask instead of a full
-// barrier: 22.22 -> 21.53 ms per 1e8 rows over two more boxes (10 of 10).
+// writes cross here (mask 0x616 instead of 0x406), and the kernel's own phase fences (the epilogue /
+// transpose points of conv1 and the dh2 phase) use the same mask instead of a full barrier; the LDS
+// fragment reads and the MFMAs keep their order. Bit-identical gradients. PERFORMANCE-NEUTRAL: the
+// ~3 % gains first measured for each step were the A/B tool's first-position penalty (the base
+// library was always timed first in its process); order-balanced runs put this build and the
+// shared-mask one within 0.1 % (profiles/r05/a3c/train/fence_mask_vmem_ab.txt, last section).
 #ifndef R48_WFENCE
 #define R48_WFENCE 0x616
 #endif

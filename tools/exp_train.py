@@ -23,6 +23,19 @@ boards = torch.randint(0, 12, (rows, 16), generator=g, dtype=torch.int8).to(dev)
 actions = torch.randint(0, 4, (rows,), generator=g, dtype=torch.int8).to(dev)
 targets = torch.randn(rows, generator=g).to(dev)
 wn = torch.full((rows,), 1.0 / rows, device=dev)
+# R48_EXP_SEG=1: the trainer's path instead -- per-board segment weights (r48_cnn_train_grad_seg,
+# the k_cnn_train<MODE, SEG=true> instance): rows = T x n step-major, board b's segment length L in
+# 1..T (synthetic), seg[b] = {w0, c0, L (int bits), 0}
+SEG = os.environ.get("R48_EXP_SEG") == "1"
+seg = None
+if SEG:
+    T = rows // n
+    L = torch.randint(1, T + 1, (n,), generator=g, dtype=torch.int32)
+    segf = torch.zeros((n, 4), dtype=torch.float32)
+    segf[:, 0] = 1.0 / rows
+    segf[:, 2] = L.view(torch.float32)
+    seg = segf.to(dev)
+    wn = None
 for path in libs:
     _lib.LIB_PATH, _lib._lib = path, None
     torch.manual_seed(0)
@@ -30,7 +43,7 @@ for path in libs:
     packed = pack_cnn_train(net)
     ws = torch.empty(_lib.load().r48_cnn_train_workspace_floats(), dtype=torch.float32, device=dev)
     run = lambda: cnn_train_grad(net, boards, actions, targets, wn, None, None, beta=0.01, exponents=True,
-                                 n_boards=n, packed=packed, workspace=ws)
+                                 n_boards=n, packed=packed, workspace=ws, seg=seg)
     out = run()
     torch.cuda.synchronize()
     grads = torch.cat([t.detach().float().reshape(-1) for t in out[0]])
@@ -46,5 +59,5 @@ for path in libs:
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / reps
-    print("%-40s %8.2f ms per %d rows  (%.2f ms per 1e8)  grad digest %08x" % (os.path.basename(path), ms, rows,
+    print(("seg " if SEG else "") + "%-40s %8.2f ms per %d rows  (%.2f ms per 1e8)  grad digest %08x" % (os.path.basename(path), ms, rows,
                                                                                ms * 1e8 / rows, digest), flush=True)
