@@ -6,6 +6,7 @@ synthetic states for the product library, or for variant libraries given on the 
 """
 import os
 import sys
+import time
 
 import torch
 
@@ -48,6 +49,13 @@ for path in libs:
     torch.cuda.synchronize()
     grads = torch.cat([t.detach().float().reshape(-1) for t in out[0]])
     digest = int((grads.view(torch.int32).long() * 2654435761).sum()) & 0xFFFFFFFF   # bit-level fingerprint
+    # the first library timed in a process ran ~3 % slow (order-balanced runs in
+    # profiles/r05/a3c/train/fence_mask_vmem_ab.txt, session 8): warm the GPU for 2 s first
+    if path == libs[0]:
+        t_w = time.time()
+        while time.time() - t_w < 2.0:
+            run()
+            torch.cuda.synchronize()
     for _ in range(2):
         run()
     torch.cuda.synchronize()
