@@ -101,18 +101,33 @@ def pack_cnn_train(net, fwd=None):
 GRAD_FLOATS = 9703   # r48_cnn_train_grad's record: dW2 [64][128] | db2 [64] | dW1 [32][5] | dWh [5][257] | losses [2]
 
 
-def _check_weights(wn, cm, counts, seg):
-    """wn [+ cm + counts] per row, or seg [+ counts] per board (r48_a3c_segments)."""
+def _check_weights(wn, cm, counts, seg, rows, n_boards):
+    """wn [+ cm + counts] per row, or seg [+ counts] per board (r48_a3c_segments). The kernels read
+    seg[row % n_boards] and counts[board] as float4, so both are checked against n_boards here (a
+    mismatch would be an out-of-bounds read, not an error). Returns n_boards."""
+    if n_boards is None:
+        if seg is not None or counts is not None:
+            raise ValueError("per-board weights (seg / counts) need n_boards")
+        n_boards = rows
+    n_boards = int(n_boards)
+    if n_boards < 1 or rows % n_boards:
+        raise ValueError("rows (%d) must be a multiple of n_boards (%d)" % (rows, n_boards))
+    for name, t in (("seg", seg), ("counts", counts)):
+        if t is not None and (not t.is_cuda or t.dtype != torch.float32 or not t.is_contiguous()
+                              or tuple(t.shape) != (n_boards, 4)):
+            raise ValueError("%s must be a contiguous float32 GPU tensor [n_boards=%d, 4]" % (name, n_boards))
     if seg is not None:
         if wn is not None or cm is not None:
             raise ValueError("per-board weights (seg) replace wn / cm")
-        if not seg.is_cuda or seg.dtype != torch.float32 or not seg.is_contiguous() or seg.shape[-1] != 4:
-            raise ValueError("seg must be a contiguous float32 GPU tensor [n_boards, 4]")
-        return
-    if wn is None or not wn.is_cuda or wn.dtype != torch.float32 or not wn.is_contiguous():
-        raise ValueError("wn must be a contiguous float32 GPU tensor")
+        return n_boards
+    for name, t in (("wn", wn), ("cm", cm)):
+        if t is not None and (not t.is_cuda or t.dtype != torch.float32 or not t.is_contiguous() or t.numel() != rows):
+            raise ValueError("%s must be a contiguous float32 GPU tensor of %d rows" % (name, rows))
+    if wn is None:
+        raise ValueError("wn (or seg) is required")
     if (cm is None) != (counts is None):
         raise ValueError("reference mode needs both cm and counts")
+    return n_boards
 
 
 def cnn_train_grad(net, boards, actions, targets, wn=None, cm=None, counts=None, beta=0.001, exponents=False,
@@ -130,19 +145,23 @@ def cnn_train_grad(net, boards, actions, targets, wn=None, cm=None, counts=None,
                         ("targets", targets, torch.float32)):
         if not t.is_cuda or t.dtype != dt or not t.is_contiguous():
             raise ValueError("%s must be a contiguous %s GPU tensor" % (name, dt))
-    _check_weights(wn, cm, counts, seg)
+    n_boards = _check_weights(wn, cm, counts, seg, rows, n_boards)
     wfrag, bias = packed if packed is not None else pack_cnn_train(net)
     if workspace is None:
         workspace = torch.empty(L.r48_cnn_train_workspace_floats(), dtype=torch.float32, device=dev)
+    elif (not workspace.is_cuda or workspace.dtype != torch.float32 or not workspace.is_contiguous()
+          or workspace.numel() < L.r48_cnn_train_workspace_floats()):
+        raise ValueError("workspace must be a contiguous float32 GPU tensor of >= %d floats"
+                         % L.r48_cnn_train_workspace_floats())
     out = torch.empty(GRAD_FLOATS, dtype=torch.float32, device=dev)
     mode = _lib.FEAT_EXPONENTS if exponents else _lib.FEAT_VALUES
     stream = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
     if seg is not None:
-        check(L.r48_cnn_train_grad_seg(ptr(boards), rows, int(n_boards or rows), ptr(actions), ptr(targets), ptr(seg),
+        check(L.r48_cnn_train_grad_seg(ptr(boards), rows, n_boards, ptr(actions), ptr(targets), ptr(seg),
                                        ptr(counts), float(beta), mode, ptr(wfrag), ptr(bias), ptr(workspace), ptr(out),
                                        stream))
     else:
-        check(L.r48_cnn_train_grad(ptr(boards), rows, int(n_boards or rows), ptr(actions), ptr(targets), ptr(wn),
+        check(L.r48_cnn_train_grad(ptr(boards), rows, n_boards, ptr(actions), ptr(targets), ptr(wn),
                                    ptr(cm), ptr(counts), float(beta), mode, ptr(wfrag), ptr(bias), ptr(workspace),
                                    ptr(out), stream))
     dw2 = out[:64 * 128].view(64, 128)
@@ -229,19 +248,23 @@ def mlp_train_grad(net, boards, actions, targets, wn=None, cm=None, counts=None,
     for t, name in ((boards, "boards"), (actions, "actions"), (targets, "targets")):
         if not t.is_cuda or not t.is_contiguous():
             raise ValueError("%s must be a contiguous GPU tensor" % name)
-    _check_weights(wn, cm, counts, seg)
+    n_boards = _check_weights(wn, cm, counts, seg, rows, n_boards)
     if w is None:
         w = pack_mlp(net)
     L = _lib.load()
+    need = int(L.r48_mlp_train_workspace_floats(rows))   # grows with rows: the hot pass's flagged-tile lists
     if workspace is None:
-        workspace = torch.empty(int(L.r48_mlp_train_workspace_floats(rows)), dtype=torch.float32, device=dev)
+        workspace = torch.empty(need, dtype=torch.float32, device=dev)
+    elif (not workspace.is_cuda or workspace.dtype != torch.float32 or not workspace.is_contiguous()
+          or workspace.numel() < need):
+        raise ValueError("workspace must be a contiguous float32 GPU tensor of >= %d floats for %d rows" % (need, rows))
     out = torch.empty(2504, dtype=torch.float32, device=dev)
     mode = _lib.FEAT_EXPONENTS if exponents else _lib.FEAT_VALUES
     stream = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
     if seg is not None:
-        check(L.r48_mlp_train_grad_seg(ptr(boards), rows, int(n_boards or rows), ptr(actions), ptr(targets), ptr(seg),
+        check(L.r48_mlp_train_grad_seg(ptr(boards), rows, n_boards, ptr(actions), ptr(targets), ptr(seg),
                                        ptr(counts), float(beta), mode, ptr(w), ptr(workspace), ptr(out), stream))
     else:
-        check(L.r48_mlp_train_grad(ptr(boards), rows, int(n_boards or rows), ptr(actions), ptr(targets), ptr(wn),
+        check(L.r48_mlp_train_grad(ptr(boards), rows, n_boards, ptr(actions), ptr(targets), ptr(wn),
                                    ptr(cm), ptr(counts), float(beta), mode, ptr(w), ptr(workspace), ptr(out), stream))
     return out[:MLP_GRAD_FLOATS], out[MLP_GRAD_FLOATS], out[MLP_GRAD_FLOATS + 1]

@@ -15,14 +15,30 @@ import torch
 import torch.distributed as dist
 
 
+def _staged(collective, t, group, **kw):
+    """Run `collective` on t. gloo has no device path on every build, so a GPU tensor under
+    gloo (the two-ranks-on-one-GPU tests) goes through a host copy; RCCL takes it in place."""
+    if t.is_cuda and dist.get_backend(group) == "gloo":
+        h = t.cpu()
+        collective(h, group=group, **kw)
+        t.copy_(h)
+    else:
+        collective(t, group=group, **kw)
+
+
 class FlatParams:
+    EXTRA = 8
+
     def __init__(self, module):
         params = [p for p in module.parameters() if p.requires_grad]
         self.params = params
         dev, dt = params[0].device, params[0].dtype
         total = sum(p.numel() for p in params)
         self.data = torch.zeros(total, dtype=dt, device=dev)
-        self.grad = torch.zeros(total, dtype=dt, device=dev)
+        # the gradient is the head of the all-reduce message; its tail carries up to EXTRA reported
+        # scalars (losses, ...) so they are averaged by the same collective
+        self._msg = torch.zeros(total + self.EXTRA, dtype=dt, device=dev)
+        self.grad = self._msg[:total]
         off = 0
         for p in params:
             k = p.numel()
@@ -34,18 +50,31 @@ class FlatParams:
     def zero_grad(self):
         self.grad.zero_()
 
-    def allreduce_grad(self, group=None):
-        """Average the gradient over the process group (one collective)."""
+    def allreduce_grad(self, group=None, extras=None):
+        """Average the gradient over the process group (one collective). `extras` (a 1-d tensor of
+        at most EXTRA scalars, e.g. the losses) is averaged by the same all-reduce; returns it
+        (averaged; unchanged on one rank), or None."""
+        total, k = self.grad.numel(), 0
+        if extras is not None:
+            extras = extras.reshape(-1)
+            k = extras.numel()
+            if k > self.EXTRA:
+                raise ValueError("at most %d extra scalars ride the gradient all-reduce" % self.EXTRA)
         if dist.is_available() and dist.is_initialized():
             world = dist.get_world_size(group)
             if world > 1:
-                dist.all_reduce(self.grad, op=dist.ReduceOp.SUM, group=group)
-                self.grad.div_(world)
+                msg = self._msg[:total + k]
+                if k:
+                    msg[total:].copy_(extras)
+                _staged(dist.all_reduce, msg, group, op=dist.ReduceOp.SUM)
+                msg.div_(world)
+                return msg[total:].clone() if k else None
+        return extras
 
     def broadcast_(self, src=0, group=None):
         """Start every replica from rank src's parameters."""
         if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
-            dist.broadcast(self.data, src=src, group=group)
+            _staged(dist.broadcast, self.data, group, src=src)
 
 
 class FlatBuffers:
@@ -75,12 +104,12 @@ class FlatBuffers:
         if self.data.numel() and dist.is_available() and dist.is_initialized():
             world = dist.get_world_size(group)
             if world > 1:
-                dist.all_reduce(self.data, op=dist.ReduceOp.SUM, group=group)
+                _staged(dist.all_reduce, self.data, group, op=dist.ReduceOp.SUM)
                 self.data.div_(world)
 
     def broadcast_(self, src=0, group=None):
         if self.data.numel() and dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
-            dist.broadcast(self.data, src=src, group=group)
+            _staged(dist.broadcast, self.data, group, src=src)
 
 
 class RMSPropTF1:

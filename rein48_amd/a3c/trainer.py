@@ -303,32 +303,34 @@ class A3CTrainer:
             # pass 2 as ONE fused kernel over all T x n states (no activation hits HBM): MFMA for the
             # CNN (r48_a3c_train.hip), fp32 MFMA + VALU for the reference MLP (r48_mlp_train.hip)
             actor, critic = self._fused_gradient(states, targets, stats)
-            self.flat.allreduce_grad(self.group)
+            # the reported scalars ride the gradient's all-reduce (one collective): every rank
+            # reports the whole job's means, which equal a one-rank trainer's over the union of shards
+            rep = self.flat.allreduce_grad(self.group, torch.stack([
+                actor.float(), critic.float(), self.lengths.float().mean(), self.finished.float().mean()]))
             self.opt.step()
             self.updates += 1
             self._wepoch += 1
-            # the reported scalars in ONE device-to-host transfer (one synchronisation)
-            a, c, ml, fin = torch.stack([actor.float(), critic.float(), self.lengths.float().mean(),
-                                         self.finished.float().mean()]).tolist()
+            a, c, ml, fin = rep.tolist()   # ONE device-to-host transfer (one synchronisation)
             return {"actor_loss": a, "critic_loss": c, "mean_length": ml, "finished": fin}
         # pass 2: chunked forward/backward, gradients accumulate in the flat buffer
         self.flat.zero_grad()
-        actor_total, critic_total = 0.0, 0.0
+        actor_total = critic_total = torch.zeros((), dtype=torch.float32, device=self.device)
         for t0 in range(0, T, cfg.update_chunk):
             t1 = min(T, t0 + cfg.update_chunk)
             logits, v = self._net(self._features(states[t0:t1]))
             actor, critic = chunk_loss(logits.view(t1 - t0, n, 4), v.view(t1 - t0, n), self.actions[t0:t1],
                                        targets[t0:t1], self.mask[t0:t1], stats, mode=cfg.mode, beta=cfg.beta)
             (actor + critic).backward()
-            actor_total += float(actor.detach())
-            critic_total += float(critic.detach())
-        self.flat.allreduce_grad(self.group)   # RCCL across GPUs (a3c.py:79-80's push, synchronous)
+            actor_total = actor_total + actor.detach().float()
+            critic_total = critic_total + critic.detach().float()
+        # RCCL across GPUs (a3c.py:79-80's push, synchronous); the reported scalars ride along
+        rep = self.flat.allreduce_grad(self.group, torch.stack([
+            actor_total, critic_total, self.lengths.float().mean(), self.finished.float().mean()]))
         self.opt.step()                        # fused TF1 RMSProp (a3c.py:264-265)
         self.updates += 1
         self._wepoch += 1
-        return {"actor_loss": actor_total, "critic_loss": critic_total,
-                "mean_length": float(self.lengths.float().mean()),
-                "finished": float(self.finished.float().mean())}
+        a, c, ml, fin = rep.tolist()
+        return {"actor_loss": a, "critic_loss": c, "mean_length": ml, "finished": fin}
 
     def _fused_gradient(self, states, targets, stats):
         """Per-row weights of losses.chunk_loss for r48_cnn_train_grad: wn = mask / (B n) and, in
@@ -348,13 +350,14 @@ class A3CTrainer:
             seg, counts = None, stats["counts"].float().contiguous() if ref else None
         if self._mlp_fused():
             from .fused import mlp_train_grad
-            if getattr(self, "_mlp_ws", None) is None:
-                self._mlp_ws = torch.empty(int(_lib.load().r48_mlp_train_workspace_floats(states.numel() // 16)), dtype=torch.float32,
-                                           device=self.device)
+            rows = states.numel() // 16
+            if getattr(self, "_mlp_ws", None) is None or self._mlp_ws[0] != rows:   # its size grows with rows
+                self._mlp_ws = (rows, torch.empty(int(_lib.load().r48_mlp_train_workspace_floats(rows)),
+                                                  dtype=torch.float32, device=self.device))
             g, actor, critic = mlp_train_grad(
                 self.net, states.reshape(-1, 16), self.actions.reshape(-1), targets.reshape(-1).contiguous(),
                 None if wn is None else wn.view(-1), None if cm is None else cm.view(-1), counts, beta=cfg.beta,
-                exponents=cfg.features == "exponents", n_boards=n, w=self._mlp_weights(), workspace=self._mlp_ws,
+                exponents=cfg.features == "exponents", n_boards=n, w=self._mlp_weights(), workspace=self._mlp_ws[1],
                 seg=seg)
             self.flat.grad.copy_(g)
             return actor, critic

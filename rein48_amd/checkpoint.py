@@ -16,13 +16,15 @@ One file per rank: each rank owns its boards and its replay shard (SURVEY.md 8(e
 per-rank path (e.g. "ckpt.rank%d.pt" % rank). Files are written with torch.save and read back with
 torch.load(weights_only=True): plain tensors, numbers and strings, nothing executable.
 
-load() refuses (ValueError) a file whose resume could not be bit-identical: another kind or format,
+load() also reads format-1 files (round 4: no draw contract or shard recorded; contract 3 is
+assumed, with a warning). It refuses (ValueError) a file whose resume could not be bit-identical: another kind or format,
 another draw contract (R48_DRAW_CONTRACT: the same counters would give other draws), another rank's
 shard (its first global board id, which keys every Philox draw), or a configuration that differs in a
 field that fixes buffer shapes, the draws (seed), the network's inputs (features) or numerics (bf16),
 or the loss (mode). Hyper-parameters such as lr, gamma or epsilon may differ (a deliberate change).
 """
 import dataclasses
+import warnings
 
 import torch
 
@@ -121,9 +123,17 @@ def load(trainer, path):
     """Restore a checkpoint written by save() into a trainer built with a matching configuration."""
     kind = _kind(trainer)
     st = torch.load(path, map_location="cpu", weights_only=True)
-    if st.get("format") != FORMAT or st.get("kind") != kind:
+    if st.get("format") not in (1, FORMAT) or st.get("kind") != kind:
         raise ValueError("checkpoint: %s is a %s checkpoint of format %s, not a %s one of format %d"
                          % (path, st.get("kind"), st.get("format"), kind, FORMAT))
+    if st["format"] == 1:
+        # format 1 (round 4) predates the recorded draw contract and shard: contract 3 (Philox4x32-7
+        # step draws, commit 66448e8) is assumed -- a file written by a library from before that
+        # commit resumes under other env draws -- and the shard cannot be checked
+        warnings.warn("checkpoint: %s is format 1: draw contract 3 assumed (files from before it resume "
+                      "under other draws), its rank shard is not recorded (pass this rank's own file)" % path,
+                      stacklevel=2)
+        st = dict(st, draw_contract=3, gid0=_gid0(trainer, kind))
     if st["draw_contract"] != DRAW_CONTRACT:
         raise ValueError("checkpoint: %s was written under draw contract %d, this library draws under %d"
                          % (path, st["draw_contract"], DRAW_CONTRACT))

@@ -228,7 +228,8 @@ int launched(const char *what)
 // Per-segment constants of the A3C loss (losses.segment_stats, a3c.py:99-123) for segments of
 // length len[i] (mask = t < len[i]): B[i] = max(len[i], 1); td_sum[i] = sum over t < len[i] of
 // targets[t][i] - values[t][i]; counts[i][k] = #{t < len[i] : actions[t][i] == k}. One lane per
-// segment; the T rows are coalesced across lanes, 8 rows of loads in flight.
+// segment (summed from t = len[i] - 1 down); the T rows are coalesced across lanes, 8 rows of loads
+// in flight.
 template <bool TD>
 __global__ __launch_bounds__(kBlock) void k_segment_stats(const float *__restrict__ values,
                                                           const float *__restrict__ targets,
@@ -242,14 +243,16 @@ __global__ __launch_bounds__(kBlock) void k_segment_stats(const float *__restric
         return;
     const int32_t L = min(max(len[i], 0), T);
     float td = 0.0f, c[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    // summed from t = L - 1 down to 0: k_segments' order, so the fused update's c0 and this td_sum
+    // are bit-identical
     constexpr int kAhead = 8;
-    int32_t t = 0;
-    for (; t + kAhead <= L; t += kAhead) {
+    int32_t t = L - 1;
+    for (; t + 1 >= kAhead; t -= kAhead) {
         float d[kAhead];
         int a[kAhead];
 #pragma unroll
         for (int k = 0; k < kAhead; k++) {
-            const int64_t o = (int64_t)(t + k) * n + i;
+            const int64_t o = (int64_t)(t - k) * n + i;
             d[k] = TD ? targets[o] - values[o] : 0.0f;
             a[k] = actions[o] & 3;
         }
@@ -261,7 +264,7 @@ __global__ __launch_bounds__(kBlock) void k_segment_stats(const float *__restric
                 c[q] += a[k] == q ? 1.0f : 0.0f;
         }
     }
-    for (; t < L; t++) {
+    for (; t >= 0; t--) {
         const int64_t o = (int64_t)t * n + i;
         if (TD)
             td += targets[o] - values[o];
@@ -301,8 +304,8 @@ __global__ __launch_bounds__(kBlock) void k_row_weights(const int32_t *__restric
 // targets), and per board seg = {w0, c0, L, 0} -- the per-row weights of k_row_weights at every row
 // t < L (w0 = (1 / B) (1 / n), c0 = (td_sum / ((4 B) B)) (1 / n), B = max(L, 1), L as int bits),
 // which the train kernels expand themselves -- plus, with TD (the reference loss), td_sum over
-// t < L of targets - values (summed from t = L - 1 down: the scan's order, not k_segment_stats')
-// and the action counts. One lane per board, the T rows coalesced across lanes, 8 rows of loads in
+// t < L of targets - values (summed from t = L - 1 down: the scan's order, which k_segment_stats
+// follows) and the action counts. One lane per board, the T rows coalesced across lanes, 8 rows of loads in
 // flight.
 template <bool DROP_LAST, bool TD>
 __global__ __launch_bounds__(kBlock) void k_segments(const float *__restrict__ rewards, const float *__restrict__ values,

@@ -765,7 +765,8 @@ int cnn_train_launch(const int8_t *boards, int64_t rows, int64_t n_boards, const
     // one instantiation per input encoding (no per-cell branch); each needs the LDS opt-in once
     auto kern = seg ? (mode == R48_FEAT_VALUES ? k_cnn_train<R48_FEAT_VALUES, true> : k_cnn_train<R48_FEAT_EXPONENTS, true>)
                     : (mode == R48_FEAT_VALUES ? k_cnn_train<R48_FEAT_VALUES, false> : k_cnn_train<R48_FEAT_EXPONENTS, false>);
-    r48::ensure_dynamic_lds(reinterpret_cast<const void *>(kern), (int)lds, r48::stream_device((hipStream_t)stream));
+    if (!r48::ensure_dynamic_lds(reinterpret_cast<const void *>(kern), (int)lds, r48::stream_device((hipStream_t)stream)))
+        return R48_EHIP;
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), lds, (hipStream_t)stream, boards, rows, n_boards, actions,
                        targets, wn, cm, (const float4 *)seg, counts, beta, (const uint4 *)wfrag, bias, workspace);
     // the group sums go after the records in the workspace (r48_cnn_train_workspace_floats)

@@ -851,18 +851,25 @@ int device_cus(int device)
     return cus;
 }
 
-void ensure_dynamic_lds(const void *kernel, int bytes, int device)
+bool ensure_dynamic_lds(const void *kernel, int bytes, int device)
 {
     static std::mutex mu;
     static std::set<std::pair<const void *, int>> done;
     std::lock_guard<std::mutex> lock(mu);
-    if (!done.insert({kernel, device}).second)
-        return;
+    if (done.count({kernel, device}))
+        return true;
     int prev = -1;
     const bool switched = hipGetDevice(&prev) == hipSuccess && prev != device && hipSetDevice(device) == hipSuccess;
-    (void)hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    const hipError_t e = hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
     if (switched)
         (void)hipSetDevice(prev);
+    if (e != hipSuccess) {   // not recorded: the next launch tries the opt-in again
+        set_last_error("hipFuncSetAttribute(MaxDynamicSharedMemorySize = " + std::to_string(bytes) +
+                       ", device " + std::to_string(device) + "): " + hipGetErrorString(e));
+        return false;
+    }
+    done.insert({kernel, device});
+    return true;
 }
 }  // namespace r48
 

@@ -13,5 +13,6 @@ int stream_device(hipStream_t stream);
 int device_cus(int device);
 // hipFuncAttributeMaxDynamicSharedMemorySize = bytes for `kernel` on `device`, set once per
 // (kernel, device) pair; thread-safe (a mutex around a small set), the caller's current device kept.
-void ensure_dynamic_lds(const void *kernel, int bytes, int device);
+// false (and r48_last_error set) when the opt-in fails; only a success is remembered.
+bool ensure_dynamic_lds(const void *kernel, int bytes, int device);
 }  // namespace r48

@@ -373,7 +373,8 @@ int r48_resnet_q_forward(const int8_t *boards, int64_t n, const void *wblob, flo
     const int64_t tiles = (n + kBoardsPerTile - 1) / kBoardsPerTile;
     const int grid = (int)(tiles < cus ? tiles : cus);
     const size_t lds = (size_t)(2 * kBufFrags * 64) * 16;
-    r48::ensure_dynamic_lds(reinterpret_cast<const void *>(k_resnet_q), (int)lds, dev);
+    if (!r48::ensure_dynamic_lds(reinterpret_cast<const void *>(k_resnet_q), (int)lds, dev))
+        return R48_EHIP;
     hipLaunchKernelGGL(k_resnet_q, dim3(grid), dim3(kThreads), lds, (hipStream_t)stream, boards, n,
                        reinterpret_cast<const uint4 *>(wblob), q, actions, eps, (uint32_t)seed,
                        (uint32_t)(seed >> 32), gid0, ctr);

@@ -491,8 +491,8 @@ def test_segments_equal_returns_stats_and_row_weights(reference, n):
     """r48_a3c_segments (the fused update's one per-board pass) vs the three kernels it replaces on
     ragged segment lengths 0..T (and one past T): targets bit-identical to r48_discounted_returns
     (both drop_last modes, n = 4096 takes its float4 kernel), counts equal to r48_a3c_segment_stats',
-    w0 / c0 / L equal to r48_a3c_row_weights' wn / cm at every row t < L -- w0 bit for bit, c0 to the
-    fp32 rounding of the td sum's order (the segment pass sums from t = L - 1 down)."""
+    w0 / c0 / L equal to r48_a3c_row_weights' wn / cm at every row t < L, bit for bit (both td sums
+    run from t = L - 1 down, so the fused and unfused reference updates share c0 exactly)."""
     from rein48_amd.a3c import kernels as K
     T = 100
     g = torch.Generator(device="cpu").manual_seed(12)
@@ -516,8 +516,7 @@ def test_segments_equal_returns_stats_and_row_weights(reference, n):
     if reference:
         assert torch.equal(counts, st["counts"])
         got_cm = torch.where(valid, seg[None, :, 1].expand(T, n), torch.zeros_like(cm))
-        mag = ((want - values).abs() * valid).sum(0) / (4.0 * st["B"] * st["B"]) / n
-        assert bool(((got_cm - cm).abs() <= 1e-5 * mag[None, :] + 1e-30).all())
+        assert torch.equal(got_cm, cm)      # both sum the td terms from t = L - 1 down
     else:
         assert counts is None and bool((seg[:, 1] == 0).all())
 
@@ -858,3 +857,114 @@ def test_rollout_megakernel_odd_board_offset():
         out.append((tr.boards.clone(), tr.actions.clone(), tr.done.clone(), tr.rewards.clone(), tr.lengths.clone()))
     for a, b in zip(*out):
         assert torch.equal(a, b)
+
+
+# ---------------------------------------------------------------- config 4: data-parallel A3C
+_DP_CASES = {   # (net, bf16, mode, features, boards per rank)
+    "cnn_textbook": ("cnn", True, "textbook", "exponents", 1003),
+    "cnn_reference": ("cnn", True, "reference", "values", 1003),
+    "mlp_reference": ("mlp", False, "reference", "values", 1001),
+}
+
+
+def _dp_cfg(case, n_boards):
+    from rein48_amd.a3c import A3CConfig
+    net, bf16, mode, feats, _ = _DP_CASES[case]
+    return A3CConfig(n_boards=n_boards, max_steps=100, mode=mode, net=net, bf16=bf16, features=feats, seed=31)
+
+
+def _dp_record(tr, out):
+    """One update's observable state as numpy (torch tensors would travel as fds that vanish with
+    the worker): trajectory rows, lengths, reported scalars, averaged gradient, parameters, ms."""
+    c = lambda t: t.detach().cpu().numpy().copy()  # noqa: E731
+    return {"boards": c(tr.boards), "actions": c(tr.actions), "done": c(tr.done), "rewards": c(tr.rewards),
+            "lengths": c(tr.lengths), "out": out, "grad": c(tr.flat.grad), "data": c(tr.flat.data),
+            "ms": c(tr.opt.ms)}
+
+
+def _dp_worker(rank, world, port, case, q, sync):
+    import os
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from rein48_amd.a3c import A3CTrainer
+        torch.manual_seed(1000 + rank)       # the trainer reseeds; rank 0's broadcast makes them equal anyway
+        tr = A3CTrainer(_dp_cfg(case, _DP_CASES[case][4]), device=DEV)
+        recs = []
+        for _ in range(2):
+            tr.rollout()
+            recs.append(_dp_record(tr, tr.update()))
+        q.put((rank, recs))
+        sync.wait(timeout=300)               # keep the process group up until the parent has read both
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("case", list(_DP_CASES))
+def test_two_rank_a3c_trainer_equals_one_rank_over_the_union(case):
+    """Config 4's data-parallel semantics on the fused HIP path (a3c.py:73-86 push/pull made
+    synchronous, :271-292 the workers): two gloo ranks sharing cuda:0, each an A3CTrainer over
+    its own shard of n boards (global ids r*n .. r*n+n-1, odd n so rank 1's shard starts on an odd
+    board), two updates each, against ONE rank over the 2n-board union with the same seed.
+
+    - every rank's rollout is bit-identical to the union trainer's rows of its shard (the env and
+      the action draws are keyed by the global board id, not by the rank);
+    - both ranks' gradients, parameters and RMSProp slots are bit-identical to each other (one
+      all-reduce, the same optimizer step);
+    - the averaged gradient equals the union trainer's to fp32 summation order (per tensor
+      1e-3 of its largest entry; the CNN's bf16 products are the same per row, only the order of
+      the fp32 row sums differs -- a wrong shard normalisation would be off by 2x), and so does
+      the RMSProp step of every parameter;
+    - the reported losses, mean length and finished fraction are equal on both ranks and equal
+      the union trainer's (they ride the gradient's all-reduce).
+    Before update 2 the union trainer takes the ranks' parameters and optimizer slots, so update 2
+    is again "the same update" (otherwise a last-ulp weight difference may flip one sampled
+    action out of 10^5 and the trajectories part)."""
+    import socket
+    import torch.multiprocessing as mp
+    from rein48_amd.a3c import A3CTrainer
+    n = _DP_CASES[case][4]
+    ctx = mp.get_context("spawn")
+    q, sync = ctx.Queue(), ctx.Event()
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    procs = [ctx.Process(target=_dp_worker, args=(r, 2, port, case, q, sync)) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        ranks = dict(q.get(timeout=300) for _ in range(2))
+    finally:
+        sync.set()
+        for p in procs:
+            p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    one = A3CTrainer(_dp_cfg(case, 2 * n), device=DEV)
+    for u in range(2):
+        r0, r1 = ranks[0][u], ranks[1][u]
+        if u:   # update 2 starts from the state the ranks reached
+            with torch.no_grad():
+                one.flat.data.copy_(torch.from_numpy(ranks[0][0]["data"]))
+                one.opt.ms.copy_(torch.from_numpy(ranks[0][0]["ms"]))
+        prev = one.flat.data.cpu().numpy().copy()
+        one.rollout()
+        ref = _dp_record(one, one.update())
+        for k in ("grad", "data", "ms"):
+            np.testing.assert_array_equal(r0[k], r1[k], err_msg="%s differs between the ranks" % k)
+        assert r0["out"] == r1["out"]
+        for r, rec in ((0, r0), (1, r1)):
+            sl = slice(r * n, (r + 1) * n)
+            for k in ("boards", "actions", "done", "rewards", "lengths"):
+                np.testing.assert_array_equal(rec[k], ref[k][..., sl, :] if k == "boards" else ref[k][..., sl],
+                                              err_msg="update %d rank %d %s" % (u + 1, r, k))
+        off = 0
+        for p in one.net.parameters():   # per tensor, relative to its largest entry
+            sl = slice(off, off + p.numel())
+            off += p.numel()
+            for what, a, b in (("grad", r0["grad"][sl], ref["grad"][sl]),
+                               ("step", r0["data"][sl] - prev[sl], ref["data"][sl] - prev[sl])):
+                err, scale = float(np.abs(a - b).max()), float(np.abs(b).max())
+                assert err <= 1e-3 * scale + 1e-9, (case, u + 1, what, tuple(p.shape), err, scale)
+        for key in ("actor_loss", "critic_loss", "mean_length", "finished"):
+            np.testing.assert_allclose(r0["out"][key], ref["out"][key], rtol=1e-4, atol=1e-6, err_msg=key)

@@ -75,3 +75,32 @@ def test_checkpoint_rejects_another_seed_rank_or_contract(tmp_path):
     with pytest.raises(ValueError, match="draw contract"):
         checkpoint.load(_learner(), tmp_path / "old.pt")
     checkpoint.load(DQNLearner(DQNConfig(channels=8, blocks=2, bf16=False, seed=3, lr=5e-4), device="cpu"), path)
+
+
+def test_checkpoint_reads_format_1_with_a_warning(tmp_path):
+    """a format-1 file (no draw_contract / gid0 keys) still resumes -- contract 3 assumed,
+    with a warning -- and resumes bit-identically; the config checks still apply."""
+    from rein48_amd import checkpoint
+    from rein48_amd.dqn import DQNConfig, DQNLearner
+    data = _batches(4)
+    a = _learner()
+    for x, act, y in data[:2]:
+        a.learn(x, act, y)
+    checkpoint.save(a, tmp_path / "new.pt")
+    st = torch.load(tmp_path / "new.pt", weights_only=True)
+    st["format"] = 1
+    del st["draw_contract"], st["gid0"]
+    torch.save(st, tmp_path / "v1.pt")
+    b = _learner()
+    with pytest.warns(UserWarning, match="format 1"):
+        checkpoint.load(b, tmp_path / "v1.pt")
+    for x, act, y in data[2:]:
+        a.learn(x, act, y)
+        b.learn(x, act, y)
+    assert torch.equal(a.flat.data, b.flat.data) and b.updates == a.updates == 4
+    with pytest.raises(ValueError, match="seed"), pytest.warns(UserWarning):
+        checkpoint.load(DQNLearner(DQNConfig(channels=8, blocks=2, bf16=False, seed=4), device="cpu"), tmp_path / "v1.pt")
+    st["format"] = 0
+    torch.save(st, tmp_path / "v0.pt")
+    with pytest.raises(ValueError, match="format"):
+        checkpoint.load(_learner(), tmp_path / "v0.pt")
