@@ -19,11 +19,14 @@ barrier skew cannot shorten it; value = all boards x K / that window.
 Extra objects on the JSON line:
   roofline      k_step_n is VALU-issue bound (boards in VGPRs, no memory traffic inside its step
                 loop): achieved = MODELLED VALU issue cycles per board-step (the shipped loop's
-                static instruction mix x measured per-instruction issue costs, committed in
-                profiles/<round>/pmc_k_step_n.json together with the hash of the kernel sources it
-                was made from) x board-steps / the SAME wall time as `value` -> frac; frac_device
-                uses the HIP-event dispatch time of the same region instead; peak = one issue cycle
-                per SIMD per clock (1024 SIMDs x 2.4 GHz). `hbm_def` expresses the same rate in GB/s
+                static instruction mix x measured per-instruction issue costs, plus the measured
+                operand costs -- literal, inline constant -- and the SIMD's SGPR-read limit,
+                tools/isa_hist.py model(); committed in profiles/<round>/pmc_k_step_n.json together
+                with the hash of the kernel sources it was made from) x board-steps / the SAME wall
+                time as `value` -> frac; frac_device uses the HIP-event dispatch time of the same
+                region instead; frac_counter beside them is the counter-only fraction (SQ_INSTS_VALU
+                per board-step at the device rate / one wave64 VALU per 2 cycles per SIMD, no cost
+                model); peak = one issue cycle per SIMD per clock (1024 SIMDs x 2.4 GHz). `hbm_def` expresses the same rate in GB/s
                 at SURVEY.md 8(d)'s 34 B per board-step -- not a roofline fraction: k_step_n makes
                 no per-step HBM round trip; the HBM roofline point is hbm.k_step_2p26 below. If the
                 committed profile's source hash
@@ -291,13 +294,19 @@ def roofline_step_n(n, wall_s, dev_ms, steps):
     out.update({
         "achieved": cyc * rate_wall / 1e9, "frac": cyc * rate_wall / 1e9 / VALU_ISSUE_PEAK_G,
         "frac_device": cyc * rate_dev / 1e9 / VALU_ISSUE_PEAK_G,
+        # beside the modelled fraction: the counter-only one (SQ_INSTS_VALU per board-step at this run's
+        # device rate / one wave64 VALU per 2 cycles per SIMD), no cost model in it
+        "frac_counter": per * rate_dev / 1e9 / VALU_PEAK_G,
         "traffic": prof["hbm_bytes_per_dispatch"] * n / prof["boards"],
         "traffic_unit": "bytes per launch (HBM/fabric; the boards are read and written once per call)",
         "traffic_source": "profiles/%s/pmc_k_step_n.json: rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE passes of a 2^20-board "
                           "K=%d dispatch (committed profile; scaled to this run's boards)"
                           % (PROFILE_ROUND, prof.get("steps_per_dispatch", 20)),
         "issue_cycles_per_board_step": cyc,
-        "issue_cycles_source": "build/r48_env.s hot loop (tools/isa_hist.py) x profiles/r02/instr_rate.txt",
+        "issue_cycles_source": "build/r48_env.s hot loop (tools/isa_hist.py model(): opcode costs of "
+                               "profiles/r02/instr_rate.txt + literal / inline-constant costs and the SGPR-read "
+                               "bound of profiles/r05/env/instr_rate_r05.txt)",
+        "opcode_only_cycles_per_board_step": prof.get("opcode_only_cycles_per_board_step"),
         "valu_wave_instr_per_board_step": per,
         "valu_instr_rate": {"achieved": per * rate_dev / 1e9, "peak": VALU_PEAK_G, "unit": "G VALU wave-instr/s",
                             "frac": per * rate_dev / 1e9 / VALU_PEAK_G,

@@ -50,9 +50,12 @@ def main():
     s = summarize("k_step_n", BOARDS // 2, [os.path.join(d, x) for x in ("sqa", "sqb", "stepn_fetch", "stepn_write")])
     pm = s["per_dispatch_mean"]
     bsteps = BOARDS * K
-    hist, blocks = isa_hist.analyse(os.path.join(ROOT, "build", "r48_env.s"), KSTEPN)
+    asm = os.path.join(ROOT, "build", "r48_env.s")
+    hist, blocks = isa_hist.analyse(asm, KSTEPN)
     valu = sum(hist.values())
-    cyc = sum(isa_hist.cost(k) * v for k, v in hist.items())
+    cyc_opcode = sum(isa_hist.cost(k) * v for k, v in hist.items())
+    mdl = isa_hist.model(isa_hist.loop_lines(asm, KSTEPN)[0])
+    cyc = mdl["modelled_cycles"]      # opcode costs + literal / inline-constant costs, SGPR-read bound
     s.update({
         "kernel": "k_step_n<RANDOM=1,AUTO_RESET=1,REWARD=0,NP=1>",
         "boards": BOARDS, "steps_per_dispatch": K, "board_steps_per_dispatch": bsteps,
@@ -63,10 +66,17 @@ def main():
         "algorithmic_bytes_per_dispatch": 34 * BOARDS,
         "isa_loop": {"asm": "build/r48_env.s (make asm)", "blocks": blocks, "valu_per_wave_pass": valu,
                      "board_steps_per_wave_pass": 128, "modelled_issue_cycles_per_wave_pass": cyc,
+                     "opcode_only_cycles_per_wave_pass": cyc_opcode, "operand_model": mdl,
                      "histogram": dict(hist.most_common())},
         "modelled_cycles_per_board_step": cyc / 128.0,
+        "opcode_only_cycles_per_board_step": cyc_opcode / 128.0,
+        "counter_valu_frac": pm["SQ_INSTS_VALU"] / (s["pmc_dispatch_ns_mean"] * 1e-9) / 1e9 / (SIMDS * CLOCK_GHZ / 2.0),
         "note": "a wave pass = one step of the 128 boards of a wave (64 lanes x a board pair); issue costs per "
-                "instruction from profiles/r02/instr_rate.txt (8 independent chains x 8 waves per SIMD)",
+                "instruction from profiles/r02/instr_rate.txt (8 independent chains x 8 waves per SIMD), plus the "
+                "round-5 operand costs (profiles/r05/env/instr_rate_r05.txt: literal +0.26, inline constant +0.16 "
+                "cycles on full-rate instructions; SGPR-reading VALU limited to one per 4.2 cycles per SIMD, a "
+                "separate bound). counter_valu_frac = SQ_INSTS_VALU / profiled dispatch time / (1024 SIMDs x 2.4 GHz "
+                "/ 2): the counter-only fraction, no cost model",
     })
     json.dump(s, open(os.path.join(OUT, "pmc_k_step_n.json"), "w"), indent=1)
     # ---- k_step at 2^20 and 2^26
@@ -95,12 +105,14 @@ def main():
           "median_dispatch_ns": med, "mean_dispatch_ns": sum(durs) / len(durs),
           "board_steps_per_dispatch": bsteps,
           "modelled_issue_cycles_per_board_step": cyc_bs,
+          "opcode_only_cycles_per_board_step": cyc_opcode / 128.0,
+          "frac_opcode_only": cyc_opcode / 128.0 * bsteps / (med * 1e-9) / 1e9 / (SIMDS * CLOCK_GHZ),
           "achieved_G_issue_cycles_per_s": ach, "peak_G_issue_cycles_per_s": SIMDS * CLOCK_GHZ,
           "frac": ach / (SIMDS * CLOCK_GHZ),
           "valu_wave_instr_per_board_step_pmc": pm["SQ_INSTS_VALU"] / bsteps,
           "instr_rate_frac": pm["SQ_INSTS_VALU"] / (med * 1e-9) / 1e9 / (SIMDS * CLOCK_GHZ / 2.0),
-          "formula": "frac = modelled issue cycles per board-step x 2^20 x 20 / median dispatch time / "
-                     "(1024 SIMDs x 2.4 GHz); instr_rate_frac = SQ_INSTS_VALU per dispatch / median dispatch time / "
+          "formula": "frac = modelled issue cycles per board-step (opcode + operand costs, isa_hist.model) x 2^20 x 20 / "
+                     "median dispatch time / (1024 SIMDs x 2.4 GHz); instr_rate_frac = SQ_INSTS_VALU per dispatch / median dispatch time / "
                      "(1024 SIMDs x 2.4 GHz / 2 cycles per full-rate wave64 instruction)",
           "trace": "profiles/%s/kernel_stats_bench.csv (rocprofv3 --kernel-trace --stats of python3 bench.py --gpus 1 "
                    "--steps 20 --warmup 5)" % rnd}
