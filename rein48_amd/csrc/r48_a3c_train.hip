@@ -52,9 +52,6 @@
 #ifndef R48_WFENCE
 #define R48_WFENCE 0x616
 #endif
-#ifndef R48_MASK_VOLATILE
-#define R48_MASK_VOLATILE 1
-#endif
 #include "r48_cnn_common.h"
 #include "r48_host.h"
 
@@ -183,11 +180,7 @@ __device__ __forceinline__ bf16x8 mask_pk(const bf16x8 &d, const bf16x8 &act)
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         uint32_t m;
-#if R48_MASK_VOLATILE
         asm volatile("v_pk_min_u16 %0, %1, %2" : "=v"(m) : "v"(aw[q]), "s"(0x00010001u));
-#else
-        asm("v_pk_min_u16 %0, %1, %2" : "=v"(m) : "v"(aw[q]), "s"(0x00010001u));
-#endif
         dw[q] = __builtin_bit_cast(uint32_t, (u16x2)(__builtin_bit_cast(u16x2, dw[q]) * __builtin_bit_cast(u16x2, m)));
     }
     bf16x8 f;
