@@ -243,7 +243,8 @@ int r48_rmsprop_tf1(float *var, const float *grad, float *ms, float *mom, int64_
  * boards int8[n][16] -> logits float[n][4] and value float[n] (each nullable), and, when
  * actions != NULL, the choose_action draw of r48_sample_actions (same Philox contract) into
  * actions int8[n]; boards_out (nullable, 16-byte aligned): a copy of the input boards (the
- * rollout's trajectory snapshot, a3c.py:203-209). wfrag: 41 x 64 x 8 bf16 weight fragments and
+ * rollout's trajectory snapshot, a3c.py:203-209). wfrag: 33 x 64 x 8 bf16 weight fragments (conv1,
+ * conv2, and the heads laid out for 16x16x32 MFMAs) and
  * bias: 104 floats, both packed by rein48_amd/a3c/fused.py:pack_cnn (16-byte aligned). mode:
  * R48_FEAT_VALUES/EXPONENTS. */
 int r48_cnn_policy_forward(const int8_t *boards, int64_t n, const void *wfrag, const float *bias,

@@ -1,12 +1,17 @@
 """Host side of the fused CNN policy kernel (r48_cnn_policy_forward, rein48_amd/csrc/r48_policy.hip).
 
-pack_cnn(net) lays out ActorCriticCNN's weights as the kernel's MFMA A-operand fragments
+pack_cnn(net) lays out ActorCriticCNN's weights as the policy kernels' MFMA A-operand fragments
 (v_mfma_f32_32x32x16_bf16: lane l, r = l & 31, h = l >> 5, element j):
   W1 fragment R (9, conv1 output position R):     W1dense[32R + r][8h + j]
   W2 fragment (g, kk, s) (16):                     conv2.w[32g + r][32kk + f]
-  Wh fragment (p, g, s) (16):                      heads.w[r][64p + 32g + f]   (rows r >= 5 zero)
 with f = 16s + 8(j>>2) + 4h + (j&3), the row order in which a 32x32 accumulator feeds the next
-MFMA as its B operand. Biases: b1[32], b2[64], bh[5] padded to 104 floats.
+MFMA as its B operand; then the heads on v_mfma_f32_16x16x32_bf16 (lane l: m = l & 15, q = l >> 4):
+  H16 fragment (p, g) (8):                         heads.w[m][64p + 32g + e]   (rows m >= 5 zero)
+with e = 16(q & 1) + 4(q >> 1) + 8(j>>2) + (j&3), the feature order of a block's two 32x32-layout
+fragments after their v_permlane16_swap (r48_cnn_common.h cnn_conv2_heads16). 33 fragments.
+pack_cnn_train(net) is the fused update's blob: the 32x32 heads Wh fragment (p, g, s) (16):
+heads.w[r][64p + 32g + f] (rows r >= 5 zero) after W1 / W2 (41 forward fragments), then Wh^T / W2^T.
+Biases: b1[32], b2[64], bh[5] padded to 104 floats.
 """
 import ctypes as C
 
@@ -27,7 +32,11 @@ def _index_maps():
                    for g in range(2) for kk in range(4) for s in range(2)])                     # into conv2.w[64,128]
     wh = np.stack([np.where((r < 5)[:, None], r[:, None] * 256 + 64 * p + 32 * g + f_perm(s), -1)
                    for p in range(4) for g in range(2) for s in range(2)])                      # into heads.w[5,256]
-    return w1, w2, wh
+    m, q = lane & 15, lane >> 4
+    e = 16 * (q[:, None] & 1) + 4 * (q[:, None] >> 1) + 8 * (j[None, :] >> 2) + (j[None, :] & 3)    # [64, 8]
+    wh16 = np.stack([np.where((m < 5)[:, None], m[:, None] * 256 + 64 * p + 32 * g + e, -1)
+                     for p in range(4) for g in range(2)])                                      # into heads.w[5,256]
+    return w1, w2, wh, wh16
 
 
 def _index_maps_backward():
@@ -61,41 +70,51 @@ def _on_device(name, maps, dev):
     return _DEV_MAPS[key]
 
 
-@torch.no_grad()
-def pack_cnn(net):
-    """-> (wfrag bf16 [41, 64, 8], bias f32 [104]) on the net's device."""
+def _pack_parts(net):
+    """(W1 fragments, W2 fragments, bias) shared by both blobs, and the padded heads.w gather source."""
     global _MAPS
     if _MAPS is None:
         _MAPS = _index_maps()
     dev = net.conv1.weight.device
-    w1_idx, w2_idx, wh_idx = _on_device("fwd", _MAPS, dev)
+    w1_idx, w2_idx, _, _ = _on_device("fwd", _MAPS, dev)
     w1_dense, _, _, _ = net.dense_weights()
     f1 = w1_dense.reshape(-1)[w1_idx]
     f2 = net.conv2.weight.reshape(-1)[w2_idx]
     hw = torch.cat([net.heads.weight.reshape(-1), torch.zeros(1, device=dev)])
-    fh = hw[torch.where(wh_idx < 0, hw.numel() - 1, wh_idx)]
-    wfrag = torch.cat([f1, f2, fh]).to(torch.bfloat16).contiguous()
     bias = torch.zeros(104, dtype=torch.float32, device=dev)
     bias[:32] = net.conv1.bias
     bias[32:96] = net.conv2.bias
     bias[96:101] = net.heads.bias
-    return wfrag, bias
+    return f1, f2, hw, bias
+
+
+def _gather_heads(hw, idx):
+    return hw[torch.where(idx < 0, hw.numel() - 1, idx)]
+
+
+@torch.no_grad()
+def pack_cnn(net):
+    """-> (wfrag bf16 [33, 64, 8], bias f32 [104]) on the net's device: the policy kernels' blob."""
+    f1, f2, hw, bias = _pack_parts(net)
+    wh16_idx = _on_device("fwd", _MAPS, net.conv1.weight.device)[3]
+    return torch.cat([f1, f2, _gather_heads(hw, wh16_idx)]).to(torch.bfloat16).contiguous(), bias
 
 
 @torch.no_grad()
 def pack_cnn_train(net, fwd=None):
-    """-> (wfrag bf16 [65, 64, 8], bias f32 [104]): pack_cnn's 41 forward fragments followed by
-    the 8 Wh^T and 16 W2^T fragments of the fused update. fwd: pack_cnn(net) if already made."""
+    """-> (wfrag bf16 [65, 64, 8], bias f32 [104]): the fused update's 41 forward fragments (W1, W2,
+    the 32x32 heads) followed by its 8 Wh^T and 16 W2^T fragments. fwd: accepted for compatibility
+    (the policy blob's heads are laid out for 16x16 MFMAs, so the update packs its own)."""
     global _MAPS_BWD
     if _MAPS_BWD is None:
         _MAPS_BWD = _index_maps_backward()
-    wfrag, bias = pack_cnn(net) if fwd is None else fwd
+    f1, f2, hw, bias = _pack_parts(net)
     dev = net.conv1.weight.device
+    wh_idx = _on_device("fwd", _MAPS, dev)[2]
     wht_idx, w2t_idx = _on_device("bwd", _MAPS_BWD, dev)
-    hw = torch.cat([net.heads.weight.reshape(-1), torch.zeros(1, device=dev)])
-    fwht = hw[torch.where(wht_idx < 0, hw.numel() - 1, wht_idx)]
     fw2t = net.conv2.weight.reshape(-1)[w2t_idx]
-    return torch.cat([wfrag, torch.cat([fwht, fw2t]).to(torch.bfloat16)]).contiguous(), bias
+    return torch.cat([f1, f2, _gather_heads(hw, wh_idx), _gather_heads(hw, wht_idx),
+                      fw2t]).to(torch.bfloat16).contiguous(), bias
 
 
 GRAD_FLOATS = 9703   # r48_cnn_train_grad's record: dW2 [64][128] | db2 [64] | dW1 [32][5] | dWh [5][257] | losses [2]

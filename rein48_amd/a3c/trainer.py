@@ -103,7 +103,7 @@ class A3CTrainer:
                 v = pack_cnn(self.net)
             elif kind == "cnn_train":
                 from .fused import pack_cnn_train
-                v = pack_cnn_train(self.net, fwd=self._packed("cnn"))
+                v = pack_cnn_train(self.net)
             else:
                 from .fused import pack_mlp
                 v = pack_mlp(self.net, out=c[1] if c is not None else None)

@@ -316,4 +316,136 @@ __device__ __forceinline__ void cnn_conv2_heads_grouped(const uint4 *w, const fl
     out = o;
 }
 
+// ---- policy form with the heads on v_mfma_f32_16x16x32_bf16 (r48_policy.hip). The heads have 5
+// outputs: as 32x32x16 MFMAs they fill 5 of 32 rows (16 MFMAs, 512 cycles per tile); as 16x16x32 ones
+// 5 of 16 (16 MFMAs of 16 cycles, 256). One head fragment H16(p, g) (16 outputs x the 32 features of
+// conv2 block (p, g), lane l: output l & 15, features 8 (l >> 4) + j in the order below) feeds two
+// MFMAs, one per 16-board group. A 16x16x32 B operand wants board l & 15 in every lane quarter, so
+// the two 32x32-layout fragments s = 0, 1 of a block are exchanged in one v_permlane16_swap per
+// dword: after it, fragment 0 holds boards 0-15 and fragment 1 boards 16-31, lane quarter q carrying
+// features 16 (q & 1) + 4 (q >> 1) + 8 (j >> 2) + (j & 3) (rein48_amd/a3c/fused.py packs H16 so).
+// Policy blob: conv1 (9) | conv2 (16) | H16 (p, g) at 25 + 2p + g (8) = 33 fragments.
+constexpr int kFragWh16 = 8, kFragsPolicy = kFragW1 + kFragW2 + kFragWh16;
+// read order: conv1 R (9), W2(0, u) (8), then per output position p: W2(1, 2p), H16(p, 0),
+// W2(1, 2p + 1) (12), then H16(p, 1) (4)
+constexpr int kPolicyReads = 9 + 8 + 12 + 4;
+__host__ __device__ constexpr int policy_frag(int i)
+{
+    if (i < 9)
+        return i;
+    i -= 9;
+    if (i < 8)
+        return kFragW1 + i;                                             // W2(0, u = i)
+    i -= 8;
+    if (i < 12) {
+        const int p = i / 3, r = i % 3;
+        return r == 1 ? kFragW1 + kFragW2 + 2 * p : kFragW1 + 8 + 2 * p + (r >> 1);   // H16(p, 0) | W2(1, u)
+    }
+    i -= 12;
+    if (i < 4)
+        return kFragW1 + kFragW2 + 2 * i + 1;                           // H16(p = i, 1)
+    return 0;
+}
+
+using f32x4 = __attribute__((ext_vector_type(4))) float;
+
+// fragments x, y (s = 0, 1 of one 32x32 block) -> the 16x16x32 B operands of board groups 0 and 1
+__device__ __forceinline__ void swap16(bf16x8 &x, bf16x8 &y)
+{
+    uint32_t a[4], b[4];
+    __builtin_memcpy(a, &x, 16);
+    __builtin_memcpy(b, &y, 16);
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const auto r = __builtin_amdgcn_permlane16_swap(a[q], b[q], false, false);
+        a[q] = r[0];
+        b[q] = r[1];
+    }
+    __builtin_memcpy(&x, a, 16);
+    __builtin_memcpy(&y, b, 16);
+}
+
+// out (lane half 0 registers 0..3: logits of board lane & 31, lane half 1 register 0: its value,
+// without the head bias -- the layout of cnn_conv2_heads_grouped) from the 9 conv1 fragments h1; the
+// stream holds policy_frag(9), (10) on entry. conv2 as cnn_conv2_heads_grouped (same products in
+// the same order, so h2 is identical), the heads on 16x16x32: half 0's 8 head MFMAs interleave with
+// half 1's conv2 MFMAs, half 1's follow its epilogue.
+__device__ __forceinline__ void cnn_conv2_heads16(const uint4 *w, const float *b, int lane, int h,
+                                                  const bf16x8 (&h1)[9][2], WStream &ws, f32x16 &out)
+{
+    auto next = [&](int i) { return ws.step(w, policy_frag(i + 2 < kPolicyReads ? i + 2 : 0), lane); };
+    f32x16 acc[4];
+    int i = 9;
+    {
+        const f32x16 b2 = load_bias(b + 32, h);
+#pragma unroll
+        for (int u = 0; u < 8; u++, i++) {
+            const bf16x8 wa = next(i);
+            wfence();
+#pragma unroll
+            for (int p = 0; p < 4; p++)
+                acc[p] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, h1[kP2[p][u >> 1]][u & 1], u ? acc[p] : b2, 0, 0,
+                                                                 0);
+            wfence();
+        }
+    }
+    bf16x8 h2[4][2];
+#pragma unroll
+    for (int p = 0; p < 4; p++) {
+        h2[p][0] = acc_to_frag_relu(acc[p], 0);
+        h2[p][1] = acc_to_frag_relu(acc[p], 1);
+    }
+    f32x4 o0 = {0.f, 0.f, 0.f, 0.f}, o1 = o0;     // board groups 0 (boards 0-15), 1 (16-31)
+    {
+        const f32x16 b2 = load_bias(b + 64, h);
+        bf16x8 wh;
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const bf16x8 wa = next(i++);
+            wfence();
+#pragma unroll
+            for (int p = 0; p < 4; p++)
+                acc[p] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, h1[kP2[p][u >> 1]][u & 1], u ? acc[p] : b2, 0, 0,
+                                                                 0);
+            wfence();
+            const int p = u >> 1;
+            if ((u & 1) == 0) {
+                swap16(h2[p][0], h2[p][1]);
+                wh = next(i++);
+                wfence();
+                o0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, h2[p][0], o0, 0, 0, 0);
+            } else {
+                o1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, h2[p][1], o1, 0, 0, 0);
+            }
+            wfence();
+        }
+    }
+#pragma unroll
+    for (int p = 0; p < 4; p++) {
+        bf16x8 x = acc_to_frag_relu(acc[p], 0), y = acc_to_frag_relu(acc[p], 1);
+        swap16(x, y);
+        const bf16x8 wh = next(i++);
+        wfence();
+        o0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, x, o0, 0, 0, 0);
+        o1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, y, o1, 0, 0, 0);
+        wfence();
+    }
+    // D of group g: lane l, register r = output 4 (l >> 4) + r of board 16 g + (l & 15): logits in
+    // lanes 0-15, the value in register 0 of lanes 16-31. One permlane16 swap per register puts
+    // group 1's logits into lanes 16-31 of o0 and group 0's values into lanes 0-15 of o1; one
+    // permlane32 swap then moves the values to lane half 1 of o0's register 0.
+    uint32_t a[4], c[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const auto t = __builtin_amdgcn_permlane16_swap(__float_as_uint(o0[r]), __float_as_uint(o1[r]), false, false);
+        a[r] = t[0];
+        c[r] = t[1];
+    }
+    a[0] = __builtin_amdgcn_permlane32_swap(a[0], c[0], false, false)[0];
+    out = f32x16{};
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+        out[r] = __uint_as_float(a[r]);
+}
+
 }  // namespace r48cnn

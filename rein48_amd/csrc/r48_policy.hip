@@ -14,8 +14,10 @@
 // operand in registers (v_cvt_pk_bf16_f32, no LDS, no lane movement). The k order inside such a
 // fragment is permuted (element j of lane half h = row 16s + 8(j>>2) + 4h + (j&3)); the host
 // packs the weight (A) fragments in exactly that order, once per parameter update
-// (rein48_amd/a3c/fused.py). Per 32 boards: 9 + 64 + 16 = 89 MFMAs (~70 kFLOP per board).
-// Weights (41 fragments x 1 KiB) are staged in LDS once per workgroup; waves loop over tiles.
+// (rein48_amd/a3c/fused.py). Per 32 boards: 9 + 64 32x32x16 MFMAs and, for the 5 head outputs,
+// 16 v_mfma_f32_16x16x32_bf16 (half the cycles of 32x32 ones with 27 of 32 rows padding;
+// r48_cnn_common.h cnn_conv2_heads16), ~70 kFLOP per board.
+// Weights (33 fragments x 1 KiB) are staged in LDS once per workgroup; waves loop over tiles.
 // Biases enter as the MFMA accumulator, ReLU is an int16 max on the packed bf16 pairs.
 #include <hip/hip_runtime.h>
 
@@ -51,27 +53,17 @@ constexpr uint32_t kSampleTag = 0xA3Cu;
 #define R48_STAGE_PLAIN 0   // 1: the weight image staged by a plain load / store loop (A/B builds)
 #endif
 
-// conv1 + conv2 + heads of one 32-board tile: the fragment-grouped conv2 (r48_cnn_common.h,
-// 41 LDS fragment reads per tile); R48_POLICY_GROUPED=0 builds the training kernel's chain order
-// (89 reads) for A/B runs. Shared by k_cnn_forward and k_cnn_rollout, so both sum identically.
-#ifndef R48_POLICY_GROUPED
-#define R48_POLICY_GROUPED 1
-#endif
+// conv1 + conv2 + heads of one 32-board tile: the fragment-grouped conv2 (r48_cnn_common.h) and the
+// heads on 16x16x32 MFMAs (cnn_conv2_heads16): 33 LDS fragment reads and 9 + 64 32x32 + 16 16x16
+// MFMAs per tile. Shared by k_cnn_forward and k_cnn_rollout, so both sum identically.
 __device__ __forceinline__ void policy_logits(const uint4 *w_lds, const float *b_lds, int lane, int h, const bf16x8 &x,
                                               f32x16 &out)
 {
     bf16x8 h1[9][2];
     WStream ws;
-#if R48_POLICY_GROUPED
-    ws.start(w_lds, fwd_grouped_frag(0), fwd_grouped_frag(1), lane);
-    cnn_conv1(w_lds, b_lds, lane, h, x, ws, h1, fwd_grouped_frag(9), fwd_grouped_frag(10));
-    cnn_conv2_heads_grouped(w_lds, b_lds, lane, h, h1, ws, out);
-#else
-    bf16x8 h2[4][2][2];
-    ws.start(w_lds, fwd_frag(0), fwd_frag(1), lane);
-    cnn_conv1(w_lds, b_lds, lane, h, x, ws, h1);
-    cnn_conv2_heads(w_lds, b_lds, lane, h, h1, ws, h2, out);
-#endif
+    ws.start(w_lds, policy_frag(0), policy_frag(1), lane);
+    cnn_conv1(w_lds, b_lds, lane, h, x, ws, h1, policy_frag(9), policy_frag(10));
+    cnn_conv2_heads16(w_lds, b_lds, lane, h, h1, ws, out);
 }
 
 // The two waves of a SIMD run identical tile loops and start together, so their MFMA-free phases
@@ -105,13 +97,13 @@ __global__ __launch_bounds__(kThreads, kOcc) void k_cnn_forward(const int8_t *__
                                                              int8_t *__restrict__ boards_out, int64_t gid0,
                                                              uint32_t k0, uint32_t k1, uint32_t ctr)
 {
-    __shared__ uint4 w_lds[kFrags * 64];
+    __shared__ uint4 w_lds[kFragsPolicy * 64];
     __shared__ __attribute__((aligned(16))) float b_lds[32 + 64 + 8];   // float4 reads (load_bias)
 #if R48_STAGE_PLAIN
-    for (int i = threadIdx.x; i < kFrags * 64; i += kThreads)
+    for (int i = threadIdx.x; i < kFragsPolicy * 64; i += kThreads)
         w_lds[i] = wfrag[i];
 #else
-    stage_lds<kFrags * 64, kThreads>(w_lds, wfrag);
+    stage_lds<kFragsPolicy * 64, kThreads>(w_lds, wfrag);
 #endif
     for (int i = threadIdx.x; i < 32 + 64 + 8; i += kThreads)
         b_lds[i] = bias[i];
@@ -205,17 +197,23 @@ __device__ __forceinline__ f32x16 policy_out(const uint4 *w_lds, const float *b_
     return out;
 }
 
-// softmax + Philox inverse CDF of one board's logits z, exactly as k_cnn_forward's epilogue
-__device__ __forceinline__ uint32_t sample_action(const float (&z)[4], uint64_t gid, uint32_t ctr, uint32_t pk0,
-                                                  uint32_t pk1)
+// the action draw's uniform (Philox4x32-10 keyed by board and sample counter, the k_sample contract):
+// it depends on neither the board nor the logits, so the rollout computes it before the step's
+// policy MFMAs, where it fills their issue gaps
+__device__ __forceinline__ float sample_uniform(uint64_t gid, uint32_t ctr, uint32_t pk0, uint32_t pk1)
+{
+    uint32_t w[4] = {(uint32_t)gid, (uint32_t)(gid >> 32), ctr, kSampleTag};
+    r48::philox4x32_10(w, pk0, pk1);
+    return (float)(w[0] >> 8) * (1.0f / 16777216.0f);
+}
+
+// softmax + inverse CDF of one board's logits z at uniform u, exactly as k_cnn_forward's epilogue
+__device__ __forceinline__ uint32_t sample_action(const float (&z)[4], float u)
 {
     const float m = fmaxf(fmaxf(z[0], z[1]), fmaxf(z[2], z[3]));
     const float e0 = __expf(z[0] - m), e1 = __expf(z[1] - m), e2 = __expf(z[2] - m), e3 = __expf(z[3] - m);
     const float inv = 1.0f / (e0 + e1 + e2 + e3);
     const float p0 = e0 * inv, c1 = p0 + e1 * inv, c2 = c1 + e2 * inv;
-    uint32_t w[4] = {(uint32_t)gid, (uint32_t)(gid >> 32), ctr, kSampleTag};
-    r48::philox4x32_10(w, pk0, pk1);
-    const float u = (float)(w[0] >> 8) * (1.0f / 16777216.0f);
     return (p0 > u) ? 0u : (c1 > u) ? 1u : (c2 > u) ? 2u : 3u;
 }
 
@@ -249,13 +247,13 @@ __global__ __launch_bounds__(kThreads, kOccRoll) void k_cnn_rollout(int8_t *__re
                                                              uint32_t pk1, uint32_t ctr0, uint32_t ek0, uint32_t ek1,
                                                              uint32_t step0)
 {
-    __shared__ uint4 w_lds[kFrags * 64];
+    __shared__ uint4 w_lds[kFragsPolicy * 64];
     __shared__ __attribute__((aligned(16))) float b_lds[32 + 64 + 8];
 #if R48_STAGE_PLAIN
-    for (int i = threadIdx.x; i < kFrags * 64; i += kThreads)
+    for (int i = threadIdx.x; i < kFragsPolicy * 64; i += kThreads)
         w_lds[i] = wfrag[i];
 #else
-    stage_lds<kFrags * 64, kThreads>(w_lds, wfrag);
+    stage_lds<kFragsPolicy * 64, kThreads>(w_lds, wfrag);
 #endif
     for (int i = threadIdx.x; i < 32 + 64 + 8; i += kThreads)
         b_lds[i] = bias[i];
@@ -290,6 +288,7 @@ __global__ __launch_bounds__(kThreads, kOccRoll) void k_cnn_rollout(int8_t *__re
                 *reinterpret_cast<uint2 *>(traj + 16 * (row0 + bA) + 8 * h) = rawA;
             if (liveB)
                 *reinterpret_cast<uint2 *>(traj + 16 * (row0 + bB) + 8 * h) = rawB;
+            const float u = sample_uniform(gE, ctr0 + (uint32_t)t, pk0, pk1);
             const f32x16 oA = policy_out<MODE>(w_lds, b_lds, lane, h, rawA);
             const f32x16 oB = policy_out<MODE>(w_lds, b_lds, lane, h, rawB);
             // V(pre-step board): the value head sits in register 0 of lane half 1 (as in
@@ -308,7 +307,7 @@ __global__ __launch_bounds__(kThreads, kOccRoll) void k_cnn_rollout(int8_t *__re
                 const float zb = __shfl_xor(oB[k], 32);
                 z[k] = (h == 0 ? oA[k] : zb) + b_lds[96 + k];
             }
-            const uint32_t act = sample_action(z, gE, ctr0 + (uint32_t)t, pk0, pk1);
+            const uint32_t act = sample_action(z, u);
             // assemble the env board: half 0 gets A's rows 2-3 from its partner, half 1 B's rows 0-1
             const uint2 send = h == 0 ? rawB : rawA;
             const uint2 recv = make_uint2((uint32_t)__shfl_xor((int)send.x, 32), (uint32_t)__shfl_xor((int)send.y, 32));

@@ -18,7 +18,10 @@ COST = {"v_perm_b32": HALF, "v_bfi_b32": HALF, "v_lshlrev_b32": 4.27, "v_bcnt_u3
         "v_lshl_add_u32": 4.38, "v_bfe_u32": 4.36, "v_min_u32_e32": 4.38, "v_max3_u32": 4.34, "v_alignbit_b32": 4.34,
         "v_bitop3_b32": 2.46, "v_xor3_b32": 2.46, "v_mul_lo_u32": 4.35, "v_cndmask_b32_e32": 4.28,
         "v_cndmask_b32_e64": 4.28, "v_lshrrev_b32": 2.24, "v_ashrrev_i32": 2.21,
-        "v_xad_u32": 4.31, "v_add_lshl_u32": 4.32, "v_med3_u32": 4.39}   # last three: profiles/r05/env/instr_rate_r05.txt
+        "v_xad_u32": 4.31, "v_add_lshl_u32": 4.32, "v_med3_u32": 4.39,   # these three: profiles/r05/env/instr_rate_r05.txt
+        # packed 16-bit VALU (the CNN kernels' ReLU / ReLU' masks): half rate (pkmax 4.38, pkadd 4.35 of
+        # profiles/r05/env/instr_rate_r05.txt; min / mul_lo assumed the same)
+        "v_pk_max_i16": 4.38, "v_pk_add_u16": 4.35, "v_pk_min_u16": 4.38, "v_pk_mul_lo_u16": 4.38}
 
 
 def cost(op):
