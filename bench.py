@@ -68,7 +68,7 @@ HBM_MEASURED_GBS = 6290.0  # float4 copy measured on MI355X (same guide)
 SIMDS, CLOCK_GHZ = 1024, 2.4            # 256 CUs x 4 SIMDs; max clock (same guide)
 VALU_PEAK_G = SIMDS * CLOCK_GHZ / 2.0   # G wave-instructions/s: one full-rate wave64 VALU instr per 2 cycles
 VALU_ISSUE_PEAK_G = SIMDS * CLOCK_GHZ   # G VALU issue-cycles/s
-PROFILE_ROUND = "r05"
+PROFILE_ROUND = "r06"
 PROFILE_DIR = os.path.join(ROOT, "profiles", PROFILE_ROUND)
 ENV_SOURCES = ("rein48_amd/csrc/r48_env.hip", "rein48_amd/csrc/r48_board.h")
 

@@ -37,6 +37,25 @@ def summarize(kernel, grid, dirs):
            "per_dispatch_mean": {c: sum(v) / len(v) for c, v in sorted(counters.items())}}
     if dur:
         out["pmc_dispatch_ns_mean"] = sum(dur.values()) / len(dur)
+    # clock and MFMA occupancy from the dispatches that carry GRBM_GUI_ACTIVE (summed over the 8 XCDs):
+    # clock = GRBM / 8 / duration; MFMA busy = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM / 8)
+    clk = [cs["GRBM_GUI_ACTIVE"] / 8.0 / dur[k] for k, cs in per.items() if "GRBM_GUI_ACTIVE" in cs and dur.get(k)]
+    busy = [cs["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024.0 * cs["GRBM_GUI_ACTIVE"] / 8.0) for cs in per.values()
+            if "GRBM_GUI_ACTIVE" in cs and "SQ_VALU_MFMA_BUSY_CYCLES" in cs]
+    m = out["per_dispatch_mean"]
+    der = {}
+    if clk:
+        der["clock_ghz"] = sum(clk) / len(clk)
+    if busy:
+        der["mfma_busy_of_simd_cycles"] = sum(busy) / len(busy)
+    if m.get("SQ_INSTS_VALU_MFMA_BF16") and m.get("SQ_INSTS_VALU"):
+        der["non_mfma_valu_per_mfma"] = (m["SQ_INSTS_VALU"] - m["SQ_INSTS_VALU_MFMA_BF16"]) / m["SQ_INSTS_VALU_MFMA_BF16"]
+    if m.get("SQ_VALU_MFMA_COEXEC_CYCLES") and m.get("SQ_VALU_MFMA_BUSY_CYCLES"):
+        der["coexec_of_mfma_busy"] = m["SQ_VALU_MFMA_COEXEC_CYCLES"] / m["SQ_VALU_MFMA_BUSY_CYCLES"]
+    if m.get("SQ_LDS_BANK_CONFLICT") and m.get("SQ_LDS_IDX_ACTIVE"):
+        der["lds_conflict_of_lds_cycles"] = m["SQ_LDS_BANK_CONFLICT"] / m["SQ_LDS_IDX_ACTIVE"]
+    if der:
+        out["derived"] = der
     return out
 
 
