@@ -21,7 +21,10 @@ COST = {"v_perm_b32": HALF, "v_bfi_b32": HALF, "v_lshlrev_b32": 4.27, "v_bcnt_u3
         "v_xad_u32": 4.31, "v_add_lshl_u32": 4.32, "v_med3_u32": 4.39,   # these three: profiles/r05/env/instr_rate_r05.txt
         # packed 16-bit VALU (the CNN kernels' ReLU / ReLU' masks): half rate (pkmax 4.38, pkadd 4.35 of
         # profiles/r05/env/instr_rate_r05.txt; min / mul_lo assumed the same)
-        "v_pk_max_i16": 4.38, "v_pk_add_u16": 4.35, "v_pk_min_u16": 4.38, "v_pk_mul_lo_u16": 4.38}
+        "v_pk_max_i16": 4.38, "v_pk_add_u16": 4.35, "v_pk_min_u16": 4.38, "v_pk_mul_lo_u16": 4.38,
+        # profiles/r06/isa/instr_rate16.txt (8 waves per SIMD)
+        "v_cvt_pk_bf16_f32": 4.19, "v_pk_max_f16": 4.26, "v_pk_mul_f16": 4.21, "v_pk_add_f16": 4.20,
+        "v_pk_fma_f16": 4.16, "v_max_i16": 2.42, "v_permlane16_swap_b32": 8.15, "v_permlane32_swap_b32": 8.21}
 
 
 def cost(op):
