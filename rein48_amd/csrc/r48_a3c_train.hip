@@ -752,15 +752,19 @@ int fail(int code, const std::string &msg)
     return code;
 }
 
-// one fixed persistent grid (the MI355X's 256 CUs), not a query of the current device, so the
-// per-wave record workspace (r48_cnn_train_workspace_floats) and the launch always agree
-constexpr int grid_size() { return 256; }
+// the persistent grid: one workgroup per CU of the stream's device, at most kMaxGrid (the MI355X's
+// 256 CUs) -- the per-wave record workspace (r48_cnn_train_workspace_floats) is sized for kMaxGrid,
+// so it covers any device (a compute partition with fewer CUs launches fewer workgroups, each
+// walking more tiles; the reduction sums exactly the records the launch wrote)
+constexpr int kMaxGrid = 256;
+constexpr int grid_size() { return kMaxGrid; }
 
 int cnn_train_launch(const int8_t *boards, int64_t rows, int64_t n_boards, const int8_t *actions, const float *targets,
                      const float *wn, const float *cm, const float *seg, const float *counts, float beta, int32_t mode,
                      const void *wfrag, const float *bias, float *workspace, float *grad, void *stream)
 {
-    const int grid = grid_size();
+    const int cus = r48::device_cus(r48::stream_device((hipStream_t)stream));
+    const int grid = cus < kMaxGrid ? cus : kMaxGrid;
     const size_t lds = kLds;
     // one instantiation per input encoding (no per-cell branch); each needs the LDS opt-in once
     auto kern = seg ? (mode == R48_FEAT_VALUES ? k_cnn_train<R48_FEAT_VALUES, true> : k_cnn_train<R48_FEAT_EXPONENTS, true>)
@@ -770,7 +774,7 @@ int cnn_train_launch(const int8_t *boards, int64_t rows, int64_t n_boards, const
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), lds, (hipStream_t)stream, boards, rows, n_boards, actions,
                        targets, wn, cm, (const float4 *)seg, counts, beta, (const uint4 *)wfrag, bias, workspace);
     // the group sums go after the records in the workspace (r48_cnn_train_workspace_floats)
-    float *group_sums = workspace + (int64_t)grid * kWaves * kPartial;
+    float *group_sums = workspace + (int64_t)kMaxGrid * kWaves * kPartial;
     hipLaunchKernelGGL(k_reduce_groups, dim3((kPartial + 255) / 256, kGroups), dim3(256), 0, (hipStream_t)stream,
                        workspace, (int64_t)grid * kWaves, group_sums);
     hipLaunchKernelGGL(k_reduce, dim3((kPartial + 255) / 256), dim3(256), 0, (hipStream_t)stream, group_sums, grad);
