@@ -248,20 +248,45 @@ __device__ __forceinline__ bf16x8 splat_frag(uint32_t w)
     return f;
 }
 
+// weight-fragment read-ahead depth of the forward and of the position loop's W2^T stream (A/B builds)
+#ifndef R48_WDEPTH
+#define R48_WDEPTH 2
+#endif
+constexpr int kWDepth = R48_WDEPTH;
+struct WStreamD {
+    bf16x8 q[kWDepth];
+    __device__ __forceinline__ void start(const uint4 *w, int lane)
+    {
+#pragma unroll
+        for (int d = 0; d < kWDepth; d++)
+            q[d] = frag_at(w, fwd_frag(d), lane);
+    }
+    __device__ __forceinline__ bf16x8 step(const uint4 *w, int ahead, int lane)
+    {
+        const bf16x8 cur = q[0];
+#pragma unroll
+        for (int d = 0; d + 1 < kWDepth; d++)
+            q[d] = q[d + 1];
+        q[kWDepth - 1] = frag_at(w, ahead, lane);
+        return cur;
+    }
+};
+__host__ __device__ constexpr int fwd_ahead(int i) { return i + kWDepth < kFwdMfmas ? fwd_frag(i + kWDepth) : 0; }
+
 // conv1 as cnn_conv1 (same products, same bits), with the MFMA of position R + 1 issued before the
 // epilogue of R (two accumulators in flight) so the pipe runs under the bf16 pack + ReLU
 __device__ __forceinline__ void fwd_conv1(const uint4 *w, const float *b, int lane, int h, const bf16x8 &x,
-                                          WStream &ws, bf16x8 (&h1)[9][2], int after0, int after1)
+                                          WStreamD &ws, bf16x8 (&h1)[9][2])
 {
     const f32x16 b1 = load_bias(b, h);
-    bf16x8 wa = ws.step(w, 2, lane);
+    bf16x8 wa = ws.step(w, fwd_ahead(0), lane);
     wfence();
     f32x16 acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, x, b1, 0, 0, 0);
 #pragma unroll
     for (int R = 0; R < 9; R++) {
         f32x16 nxt = acc;
         if (R + 1 < 9) {
-            wa = ws.step(w, R + 3 < 9 ? R + 3 : (R + 3 == 9 ? after0 : after1), lane);
+            wa = ws.step(w, fwd_ahead(R + 1), lane);
             wfence();
             nxt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, x, b1, 0, 0, 0);
         }
@@ -278,7 +303,7 @@ __device__ __forceinline__ void fwd_conv1(const uint4 *w, const float *b, int la
 // runs under the next chain's MFMAs. 89 fragment reads per tile (the grouped order reads 41 but
 // needs four accumulators and all of h1 at once: no room for the epilogues to overlap).
 __device__ __forceinline__ void fwd_conv2_heads_chain(const uint4 *w, const float *b, int lane, int h,
-                                                      const bf16x8 (&h1)[9][2], WStream &ws, bf16x8 (&h2)[4][2][2],
+                                                      const bf16x8 (&h1)[9][2], WStreamD &ws, bf16x8 (&h2)[4][2][2],
                                                       f32x16 &out, uint16_t *img, const LaneAddr &la)
 {
     const f32x16 b2[2] = {load_bias(b + 32, h), load_bias(b + 64, h)};
@@ -292,7 +317,7 @@ __device__ __forceinline__ void fwd_conv2_heads_chain(const uint4 *w, const floa
             f32x16 a = b2[c & 1];
 #pragma unroll
             for (int u = 0; u < 8; u++, i++) {
-                const bf16x8 wa = ws.step(w, fwd_frag(i + 2 < kFwdMfmas ? i + 2 : 0), lane);
+                const bf16x8 wa = ws.step(w, fwd_ahead(i), lane);
                 wfence();
                 a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, h1[kP2[p][u >> 1]][u & 1], a, 0, 0, 0);
                 wfence();
@@ -305,7 +330,7 @@ __device__ __forceinline__ void fwd_conv2_heads_chain(const uint4 *w, const floa
             for (int s = 0; s < 2; s++, i++) {
                 h2[p][g][s] = acc_to_frag_relu(acc[cp & 1], s);
                 store_frag(img, la, 64 * p + 32 * g + 16 * s, h2[p][g][s]);
-                const bf16x8 wa = ws.step(w, fwd_frag(i + 2 < kFwdMfmas ? i + 2 : 0), lane);
+                const bf16x8 wa = ws.step(w, fwd_ahead(i), lane);
                 wfence();
                 out = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, h2[p][g][s], out, 0, 0, 0);
                 wfence();
@@ -449,9 +474,9 @@ __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
         f32x16 out;
         {
             bf16x8 h1[9][2];
-            WStream ws;
-            ws.start(w, fwd_frag(0), fwd_frag(1), lane);
-            fwd_conv1(w, bl, lane, h, x, ws, h1, fwd_frag(9), fwd_frag(10));
+            WStreamD ws;
+            ws.start(w, lane);
+            fwd_conv1(w, bl, lane, h, x, ws, h1);
             fwd_conv2_heads_chain(w, bl, lane, h, h1, ws, h2, out, my, la);
         }
         // ---------------- loss gradient per row (lane half 0: logits rows 0..3; value in lane + 32)
@@ -599,7 +624,10 @@ __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
                 b1s[r] = b1c;
             // W2^T fragments (B operands of dh1^T) stream two MFMAs ahead over the 64 (pair, g, s)
             auto w2t = [](int m) { return kOffW2T + (kDh1K[m >> 2] * 2 + ((m >> 1) & 1)) * 2 + (m & 1); };
-            bf16x8 q0 = frag_at(w, w2t(0), lane), q1 = frag_at(w, w2t(1), lane);
+            bf16x8 qw[kWDepth];
+#pragma unroll
+            for (int d = 0; d < kWDepth; d++)
+                qw[d] = frag_at(w, w2t(d), lane);
             // h1^T_R: A = x (rows x cells), B = W1_R^T (the W1 fragment's registers), C = b1 per lane
             f32x16 a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x, frag_at(w, 0, lane), b1s, 0, 0, 0);
             f32x16 dprev = zero;
@@ -618,10 +646,12 @@ __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
                 for (int m = 4 * kRFirst[R]; m < 4 * kRFirst[R + 1]; m++) {
                     const int n = m >> 2, p = kDh1P[n], g = (m >> 1) & 1, s = m & 1;
                     const int first = 4 * kRFirst[R];
-                    const bf16x8 wb = q0;
-                    q0 = q1;
-                    if (m + 2 < 64)
-                        q1 = frag_at(w, w2t(m + 2), lane);
+                    const bf16x8 wb = qw[0];
+#pragma unroll
+                    for (int d = 0; d + 1 < kWDepth; d++)
+                        qw[d] = qw[d + 1];
+                    if (m + kWDepth < 64)
+                        qw[kWDepth - 1] = frag_at(w, w2t(m + kWDepth), lane);
                     wfence();
                     d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(dh2[p][g][s], wb, d, 0, 0, 0);
                     if (m == first && R + 1 < 9)
