@@ -248,9 +248,12 @@ __device__ __forceinline__ bf16x8 splat_frag(uint32_t w)
     return f;
 }
 
-// weight-fragment read-ahead depth of the forward and of the position loop's W2^T stream (A/B builds)
+// weight-fragment read-ahead depth of the forward and of the position loop's W2^T stream: 3 fragments
+// (3 MFMAs, ~96 cycles) ahead of their MFMA, +4 VGPRs over 2; kernel 19.38-19.43 vs 19.59-19.69 ms per
+// 1e8 rows for the round-5 kernel (depth 2), 19.54-19.66 at depth 4, four alternated process-per-library
+// rounds, identical gradient digests (profiles/r06/a3c/train/read_ahead_depth_ab.txt)
 #ifndef R48_WDEPTH
-#define R48_WDEPTH 2
+#define R48_WDEPTH 3
 #endif
 constexpr int kWDepth = R48_WDEPTH;
 struct WStreamD {
@@ -622,7 +625,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_cnn_train(
 #pragma unroll
             for (int r = 0; r < 16; r++)
                 b1s[r] = b1c;
-            // W2^T fragments (B operands of dh1^T) stream two MFMAs ahead over the 64 (pair, g, s)
+            // W2^T fragments (B operands of dh1^T) stream kWDepth MFMAs ahead over the 64 (pair, g, s)
             auto w2t = [](int m) { return kOffW2T + (kDh1K[m >> 2] * 2 + ((m >> 1) & 1)) * 2 + (m & 1); };
             bf16x8 qw[kWDepth];
 #pragma unroll
