@@ -156,166 +156,6 @@ __host__ __device__ constexpr int fwd_frag(int i)
                  : kFragW1 + kFragW2 + b * 2 + (u - 8);                     // heads of chain b
 }
 
-// A-fragment stream two MFMAs deep: q0 feeds the next MFMA, q1 the one after; step() returns q0
-// and issues the read of fragment `ahead` (the MFMA after q1's)
-struct WStream {
-    bf16x8 q0, q1;
-    __device__ __forceinline__ void start(const uint4 *w, int f0, int f1, int lane)
-    {
-        q0 = frag_at(w, f0, lane);
-        q1 = frag_at(w, f1, lane);
-    }
-    __device__ __forceinline__ bf16x8 step(const uint4 *w, int ahead, int lane)
-    {
-        const bf16x8 cur = q0;
-        q0 = q1;
-        q1 = frag_at(w, ahead, lane);
-        return cur;
-    }
-};
-
-// ReLU(conv1 x + b1) for the 9 positions; the stream holds fragments 0 and 1 on entry and
-// `after0`, `after1` (default: fwd_frag(9), fwd_frag(10)) on exit
-__device__ __forceinline__ void cnn_conv1(const uint4 *w, const float *b, int lane, int h, const bf16x8 &x,
-                                          WStream &ws, bf16x8 (&h1)[9][2], int after0 = fwd_frag(9),
-                                          int after1 = fwd_frag(10))
-{
-    const f32x16 b1 = load_bias(b, h);
-#pragma unroll
-    for (int R = 0; R < 9; R++) {
-        const bf16x8 wa = ws.step(w, R + 2 < 9 ? R + 2 : (R + 2 == 9 ? after0 : after1), lane);
-        wfence();
-        const f32x16 a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, x, b1, 0, 0, 0);
-        wfence();
-        h1[R][0] = acc_to_frag_relu(a, 0);
-        h1[R][1] = acc_to_frag_relu(a, 1);
-    }
-}
-
-// conv2 + heads: h2[p][g][s] = ReLU(conv2 h1 + b2) fragments and out (rows 0..3 logits, row 4
-// value, without the head bias); the stream holds fwd_frag(9), fwd_frag(10) on entry. Issue order
-// as fwd_frag: chain c (c = 2p + g), then the heads of chain c - 1.
-__device__ __forceinline__ void cnn_conv2_heads(const uint4 *w, const float *b, int lane, int h,
-                                                const bf16x8 (&h1)[9][2], WStream &ws, bf16x8 (&h2)[4][2][2],
-                                                f32x16 &out)
-{
-    const f32x16 b2[2] = {load_bias(b + 32, h), load_bias(b + 64, h)};
-    out = f32x16{};
-    f32x16 acc[2];
-    int i = 9;
-#pragma unroll
-    for (int c = 0; c <= 8; c++) {
-        if (c < 8) {
-            const int p = c >> 1;
-            f32x16 a = b2[c & 1];
-#pragma unroll
-            for (int u = 0; u < 8; u++, i++) {
-                const bf16x8 wa = ws.step(w, fwd_frag(i + 2 < kFwdMfmas ? i + 2 : 0), lane);
-                wfence();
-                a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, h1[kP2[p][u >> 1]][u & 1], a, 0, 0, 0);
-                wfence();
-            }
-            acc[c & 1] = a;
-        }
-        if (c >= 1) {
-            const int cp = c - 1, p = cp >> 1, g = cp & 1;
-#pragma unroll
-            for (int s = 0; s < 2; s++, i++) {
-                h2[p][g][s] = acc_to_frag_relu(acc[cp & 1], s);
-                const bf16x8 wa = ws.step(w, fwd_frag(i + 2 < kFwdMfmas ? i + 2 : 0), lane);
-                wfence();
-                out = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, h2[p][g][s], out, 0, 0, 0);
-                wfence();
-            }
-        }
-    }
-}
-
-// ---- inference form of conv2 + heads (r48_policy.hip): the same products, grouped by weight
-// fragment. conv2's 16 fragments W2(g, u) (g = output half, u = 2kk + s) are each read ONCE per tile
-// and feed the 4 positions' chains of half g (4 independent accumulators), instead of one read per
-// chain: 41 fragment reads per 32-board tile instead of 89, and no MFMA waits on the previous one.
-// Half 0's head MFMAs interleave with half 1's conv2 MFMAs (one per fragment); half 1's heads
-// follow its epilogue. Read order of fwd_grouped_frag: conv1 (9), W2(0, u) (8), [W2(1, u), head
-// (p = u >> 1, g = 0, s = u & 1)] (16), head (p, 1, s) (8).
-constexpr int kFwdGroupedReads = 9 + 8 + 16 + 8;
-__host__ __device__ constexpr int fwd_grouped_frag(int i)
-{
-    if (i < 9)
-        return i;
-    i -= 9;
-    if (i < 8)
-        return kFragW1 + i;                                            // W2(0, u = i)
-    i -= 8;
-    if (i < 16)
-        return (i & 1) ? kFragW1 + kFragW2 + 2 * (2 * (i >> 2)) + ((i >> 1) & 1)   // head (i >> 2, 0, (i >> 1) & 1)
-                       : kFragW1 + 8 + (i >> 1);                                   // W2(1, u = i >> 1)
-    i -= 16;
-    if (i < 8)
-        return kFragW1 + kFragW2 + 2 * (2 * (i >> 1) + 1) + (i & 1);  // head (i >> 1, 1, i & 1)
-    return 0;
-}
-
-// out (rows 0..3 logits, row 4 value, without the head bias) from the 9 conv1 fragments h1; the
-// stream holds fwd_grouped_frag(9), (10) on entry. Every accumulator sums its products in the same
-// order in every caller (k_cnn_forward, k_cnn_rollout), so their results are bit-identical.
-__device__ __forceinline__ void cnn_conv2_heads_grouped(const uint4 *w, const float *b, int lane, int h,
-                                                        const bf16x8 (&h1)[9][2], WStream &ws, f32x16 &out)
-{
-    auto next = [&](int i) { return ws.step(w, fwd_grouped_frag(i + 2 < kFwdGroupedReads ? i + 2 : 0), lane); };
-    f32x16 acc[4];
-    int i = 9;
-    {
-        const f32x16 b2 = load_bias(b + 32, h);
-#pragma unroll
-        for (int u = 0; u < 8; u++, i++) {
-            const bf16x8 wa = next(i);
-            wfence();
-#pragma unroll
-            for (int p = 0; p < 4; p++)
-                acc[p] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, h1[kP2[p][u >> 1]][u & 1], u ? acc[p] : b2, 0, 0,
-                                                                 0);
-            wfence();
-        }
-    }
-    bf16x8 h2[4][2];
-#pragma unroll
-    for (int p = 0; p < 4; p++) {
-        h2[p][0] = acc_to_frag_relu(acc[p], 0);
-        h2[p][1] = acc_to_frag_relu(acc[p], 1);
-    }
-    f32x16 o = f32x16{};
-    {
-        const f32x16 b2 = load_bias(b + 64, h);
-#pragma unroll
-        for (int u = 0; u < 8; u++) {
-            const bf16x8 wa = next(i++);
-            wfence();
-#pragma unroll
-            for (int p = 0; p < 4; p++)
-                acc[p] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, h1[kP2[p][u >> 1]][u & 1], u ? acc[p] : b2, 0, 0,
-                                                                 0);
-            wfence();
-            const bf16x8 wh = next(i++);
-            wfence();
-            o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, h2[u >> 1][u & 1], o, 0, 0, 0);
-            wfence();
-        }
-    }
-#pragma unroll
-    for (int p = 0; p < 4; p++) {
-#pragma unroll
-        for (int s = 0; s < 2; s++) {
-            const bf16x8 hh = acc_to_frag_relu(acc[p], s);
-            const bf16x8 wh = next(i++);
-            wfence();
-            o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, hh, o, 0, 0, 0);
-            wfence();
-        }
-    }
-    out = o;
-}
-
 // ---- policy form with the heads on v_mfma_f32_16x16x32_bf16 (r48_policy.hip). The heads have 5
 // outputs: as 32x32x16 MFMAs they fill 5 of 32 rows (16 MFMAs, 512 cycles per tile); as 16x16x32 ones
 // 5 of 16 (16 MFMAs of 16 cycles, 256). One head fragment H16(p, g) (16 outputs x the 32 features of
@@ -366,14 +206,56 @@ __device__ __forceinline__ void swap16(bf16x8 &x, bf16x8 &y)
 }
 
 // out (lane half 0 registers 0..3: logits of board lane & 31, lane half 1 register 0: its value,
-// without the head bias -- the layout of cnn_conv2_heads_grouped) from the 9 conv1 fragments h1; the
-// stream holds policy_frag(9), (10) on entry. conv2 as cnn_conv2_heads_grouped (same products in
-// the same order, so h2 is identical), the heads on 16x16x32: half 0's 8 head MFMAs interleave with
-// half 1's conv2 MFMAs, half 1's follow its epilogue.
-__device__ __forceinline__ void cnn_conv2_heads16(const uint4 *w, const float *b, int lane, int h,
-                                                  const bf16x8 (&h1)[9][2], WStream &ws, f32x16 &out)
+// without the head bias) from the 9 conv1 fragments h1; the stream continues at read 9. conv2 grouped
+// by weight fragment: each of its 16 fragments W2(g, u) is read ONCE per tile and feeds the 4 output
+// positions' accumulators of half g (no MFMA waits on the previous one); the heads on 16x16x32: half
+// 0's 8 head MFMAs interleave with half 1's conv2 MFMAs, half 1's follow its epilogue.
+// A-fragment stream D fragments deep over policy_frag (the policy kernels' read-ahead)
+#ifndef R48_POLICY_WDEPTH
+#define R48_POLICY_WDEPTH 2
+#endif
+template <int D>
+struct PolicyStream {
+    bf16x8 q[D];
+    __device__ __forceinline__ void start(const uint4 *w, int lane)
+    {
+#pragma unroll
+        for (int d = 0; d < D; d++)
+            q[d] = frag_at(w, policy_frag(d), lane);
+    }
+    // the fragment of read i; issues the read of i + D
+    __device__ __forceinline__ bf16x8 next(const uint4 *w, int i, int lane)
+    {
+        const bf16x8 cur = q[0];
+#pragma unroll
+        for (int d = 0; d + 1 < D; d++)
+            q[d] = q[d + 1];
+        q[D - 1] = frag_at(w, policy_frag(i + D < kPolicyReads ? i + D : 0), lane);
+        return cur;
+    }
+};
+using PolicyWStream = PolicyStream<R48_POLICY_WDEPTH>;
+
+// ReLU(conv1 x + b1) for the 9 positions from the policy stream (reads 0..8)
+__device__ __forceinline__ void policy_conv1(const uint4 *w, const float *b, int lane, int h, const bf16x8 &x,
+                                             PolicyWStream &ws, bf16x8 (&h1)[9][2])
 {
-    auto next = [&](int i) { return ws.step(w, policy_frag(i + 2 < kPolicyReads ? i + 2 : 0), lane); };
+    const f32x16 b1 = load_bias(b, h);
+#pragma unroll
+    for (int R = 0; R < 9; R++) {
+        const bf16x8 wa = ws.next(w, R, lane);
+        wfence();
+        const f32x16 a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, x, b1, 0, 0, 0);
+        wfence();
+        h1[R][0] = acc_to_frag_relu(a, 0);
+        h1[R][1] = acc_to_frag_relu(a, 1);
+    }
+}
+
+__device__ __forceinline__ void cnn_conv2_heads16(const uint4 *w, const float *b, int lane, int h,
+                                                  const bf16x8 (&h1)[9][2], PolicyWStream &ws, f32x16 &out)
+{
+    auto next = [&](int i) { return ws.next(w, i, lane); };
     f32x16 acc[4];
     int i = 9;
     {

@@ -60,9 +60,9 @@ __device__ __forceinline__ void policy_logits(const uint4 *w_lds, const float *b
                                               f32x16 &out)
 {
     bf16x8 h1[9][2];
-    WStream ws;
-    ws.start(w_lds, policy_frag(0), policy_frag(1), lane);
-    cnn_conv1(w_lds, b_lds, lane, h, x, ws, h1, policy_frag(9), policy_frag(10));
+    PolicyWStream ws;
+    ws.start(w_lds, lane);
+    policy_conv1(w_lds, b_lds, lane, h, x, ws, h1);
     cnn_conv2_heads16(w_lds, b_lds, lane, h, h1, ws, out);
 }
 

@@ -1,54 +1,12 @@
 // Compile-time checks of the fused CNN kernels' weight-fragment read schedules
 // (rein48_amd/csrc/r48_cnn_common.h): every read names a valid fragment, the policy order reads each
-// of its 33 fragments exactly once (heads after the conv2 half they consume), the grouped inference
-// order reads each of the 41 fragments exactly once, and a head fragment is read only after the
-// conv2 half it consumes is complete; the chain order (training kernel) reads conv1 and head
-// fragments once and every conv2 fragment once per output position.
+// of its 33 fragments exactly once (heads after the conv2 half they consume, conv1 first); the chain
+// order (training kernel) reads conv1 and head fragments once and every conv2 fragment once per
+// output position.
 // Built by tests/test_board_logic_host.py with `hipcc --offload-host-only -fsyntax-only`.
 #include "../../rein48_amd/csrc/r48_cnn_common.h"
 
 using namespace r48cnn;
-
-constexpr bool grouped_reads_each_fragment_once()
-{
-    int cnt[kFrags] = {};
-    for (int i = 0; i < kFwdGroupedReads; i++) {
-        const int f = fwd_grouped_frag(i);
-        if (f < 0 || f >= kFrags)
-            return false;
-        cnt[f]++;
-    }
-    for (int f = 0; f < kFrags; f++)
-        if (cnt[f] != 1)
-            return false;
-    return true;
-}
-
-constexpr bool grouped_heads_after_their_half()
-{
-    // last read of W2(g, .) must precede the first head read of half g
-    int last_w2[2] = {-1, -1}, first_head[2] = {1 << 20, 1 << 20};
-    for (int i = 0; i < kFwdGroupedReads; i++) {
-        const int f = fwd_grouped_frag(i);
-        if (f >= kFragW1 && f < kFragW1 + kFragW2) {
-            const int g = (f - kFragW1) >> 3;
-            last_w2[g] = i;
-        } else if (f >= kFragW1 + kFragW2) {
-            const int c = (f - kFragW1 - kFragW2) >> 1, g = c & 1;
-            if (i < first_head[g])
-                first_head[g] = i;
-        }
-    }
-    return last_w2[0] < first_head[0] && last_w2[1] < first_head[1];
-}
-
-constexpr bool grouped_conv1_first()
-{
-    for (int i = 0; i < 9; i++)
-        if (fwd_grouped_frag(i) != i)
-            return false;
-    return true;
-}
 
 constexpr bool chain_order_counts()
 {
@@ -105,8 +63,4 @@ constexpr bool policy_heads_after_their_half()
 static_assert(kPolicyReads == kFragsPolicy && kFragsPolicy == 33, "policy schedule length");
 static_assert(policy_reads_each_fragment_once(), "policy schedule reads every fragment once, conv1 first");
 static_assert(policy_heads_after_their_half(), "policy head fragments follow the conv2 half they consume");
-static_assert(kFwdGroupedReads == 41, "grouped schedule length");
-static_assert(grouped_reads_each_fragment_once(), "grouped schedule reads every fragment once");
-static_assert(grouped_heads_after_their_half(), "head fragments follow the conv2 half they consume");
-static_assert(grouped_conv1_first(), "conv1 fragments first, in position order");
 static_assert(chain_order_counts(), "chain schedule: conv2 fragments once per position");
