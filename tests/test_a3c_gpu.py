@@ -901,12 +901,13 @@ def _dp_worker(rank, world, port, case, q, sync):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("case", list(_DP_CASES))
-def test_two_rank_a3c_trainer_equals_one_rank_over_the_union(case):
+@pytest.mark.parametrize("case,world", [(c, 2) for c in _DP_CASES] + [("mlp_reference", 3)])
+def test_two_rank_a3c_trainer_equals_one_rank_over_the_union(case, world):
     """Config 4's data-parallel semantics on the fused HIP path (a3c.py:73-86 push/pull made
-    synchronous, :271-292 the workers): two gloo ranks sharing cuda:0, each an A3CTrainer over
-    its own shard of n boards (global ids r*n .. r*n+n-1, odd n so rank 1's shard starts on an odd
-    board), two updates each, against ONE rank over the 2n-board union with the same seed.
+    synchronous, :271-292 the workers): `world` gloo ranks sharing cuda:0 (2, and 3 for the MLP),
+    each an A3CTrainer over its own shard of n boards (global ids r*n .. r*n+n-1, odd n so rank 1's
+    shard starts on an odd board), two updates each, against ONE rank over the union with the same
+    seed.
 
     - every rank's rollout is bit-identical to the union trainer's rows of its shard (the env and
       the action draws are keyed by the global board id, not by the rank);
@@ -930,19 +931,19 @@ def test_two_rank_a3c_trainer_equals_one_rank_over_the_union(case):
     with socket.socket() as so:
         so.bind(("127.0.0.1", 0))
         port = so.getsockname()[1]
-    procs = [ctx.Process(target=_dp_worker, args=(r, 2, port, case, q, sync)) for r in range(2)]
+    procs = [ctx.Process(target=_dp_worker, args=(r, world, port, case, q, sync)) for r in range(world)]
     for p in procs:
         p.start()
     try:
-        ranks = dict(q.get(timeout=300) for _ in range(2))
+        ranks = dict(q.get(timeout=300) for _ in range(world))
     finally:
         sync.set()
         for p in procs:
             p.join(timeout=60)
     assert all(p.exitcode == 0 for p in procs)
-    one = A3CTrainer(_dp_cfg(case, 2 * n), device=DEV)
+    one = A3CTrainer(_dp_cfg(case, world * n), device=DEV)
     for u in range(2):
-        r0, r1 = ranks[0][u], ranks[1][u]
+        r0 = ranks[0][u]
         if u:   # update 2 starts from the state the ranks reached
             with torch.no_grad():
                 one.flat.data.copy_(torch.from_numpy(ranks[0][0]["data"]))
@@ -950,10 +951,11 @@ def test_two_rank_a3c_trainer_equals_one_rank_over_the_union(case):
         prev = one.flat.data.cpu().numpy().copy()
         one.rollout()
         ref = _dp_record(one, one.update())
-        for k in ("grad", "data", "ms"):
-            np.testing.assert_array_equal(r0[k], r1[k], err_msg="%s differs between the ranks" % k)
-        assert r0["out"] == r1["out"]
-        for r, rec in ((0, r0), (1, r1)):
+        for r in range(1, world):
+            for k in ("grad", "data", "ms"):
+                np.testing.assert_array_equal(r0[k], ranks[r][u][k], err_msg="%s differs between ranks 0, %d" % (k, r))
+            assert r0["out"] == ranks[r][u]["out"]
+        for r, rec in ((r, ranks[r][u]) for r in range(world)):
             sl = slice(r * n, (r + 1) * n)
             for k in ("boards", "actions", "done", "rewards", "lengths"):
                 np.testing.assert_array_equal(rec[k], ref[k][..., sl, :] if k == "boards" else ref[k][..., sl],
@@ -968,3 +970,36 @@ def test_two_rank_a3c_trainer_equals_one_rank_over_the_union(case):
                 assert err <= 1e-3 * scale + 1e-9, (case, u + 1, what, tuple(p.shape), err, scale)
         for key in ("actor_loss", "critic_loss", "mean_length", "finished"):
             np.testing.assert_allclose(r0["out"][key], ref["out"][key], rtol=1e-4, atol=1e-6, err_msg=key)
+
+
+def test_fused_update_argument_checks():
+    """The fused gradients refuse what would read or write out of bounds: a workspace
+    smaller than the row count needs, per-board weights without n_boards or of the wrong shape,
+    counts of the wrong dtype, rows not a multiple of n_boards."""
+    from rein48_amd import _lib
+    from rein48_amd.a3c.fused import cnn_train_grad, mlp_train_grad
+    from rein48_amd.a3c.nets import ActorCriticCNN
+    n, T = 64, 3
+    rows = n * T
+    b = torch.zeros((rows, 16), dtype=torch.int8, device=DEV)
+    a = torch.zeros(rows, dtype=torch.int8, device=DEV)
+    t = torch.zeros(rows, dtype=torch.float32, device=DEV)
+    seg = torch.zeros((n, 4), dtype=torch.float32, device=DEV)
+    mnet, cnet = _mlp_net(), ActorCriticCNN().to(DEV)
+    need = int(_lib.load().r48_mlp_train_workspace_floats(rows))
+    with pytest.raises(ValueError, match="workspace"):
+        mlp_train_grad(mnet, b, a, t, seg=seg, n_boards=n,
+                       workspace=torch.empty(need - 1, dtype=torch.float32, device=DEV))
+    with pytest.raises(ValueError, match="n_boards"):
+        mlp_train_grad(mnet, b, a, t, seg=seg)
+    with pytest.raises(ValueError, match="seg"):
+        mlp_train_grad(mnet, b, a, t, seg=seg[:n - 1].contiguous(), n_boards=n)
+    with pytest.raises(ValueError, match="counts"):
+        cnn_train_grad(cnet, b, a, t, seg=seg, counts=seg.double(), n_boards=n)
+    with pytest.raises(ValueError, match="multiple"):
+        cnn_train_grad(cnet, b, a, t, seg=torch.zeros((n + 1, 4), dtype=torch.float32, device=DEV), n_boards=n + 1)
+    with pytest.raises(ValueError, match="workspace"):
+        cnn_train_grad(cnet, b, a, t, seg=seg, n_boards=n, workspace=torch.empty(16, dtype=torch.float32, device=DEV))
+    g, _, _ = mlp_train_grad(mnet, b, a, t, seg=seg, n_boards=n,
+                             workspace=torch.empty(need, dtype=torch.float32, device=DEV))
+    assert bool(torch.isfinite(g).all())
