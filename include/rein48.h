@@ -428,9 +428,12 @@ int r48_conv3x3_bn_in(const void *x, int64_t boards, const void *wfrag, const fl
  * output dx is the gradient reaching a training-mode BN + ReLU, with that BN's backward reduction
  * fused in the epilogue: bn_part (float[r48_conv_stats_floats()]) gets per-CU records [sum g 64]
  * [sum g (bn_x - mean) 64], g = dx . bn_mask, bn_x the BN's input, mean = bn_save[0..63] -- the
- * input of r48_bn_backward_part. */
-int r48_conv3x3_bn_grad(const void *dy, int64_t boards, const void *wfrag, const void *add, void *dx,
-                        const void *bn_x, const uint8_t *bn_mask, const float *bn_save, float *bn_part, void *stream);
+ * input of r48_bn_backward_part. add_mask (NULL, or with add: [boards][16][8] bytes, bit k of byte
+ * j = channel 8 j + k): the added term is add . [mask bit] -- a basic block's identity-path
+ * gradient formed from the gradient at the block's output ReLU and that ReLU's forward mask. */
+int r48_conv3x3_bn_grad(const void *dy, int64_t boards, const void *wfrag, const void *add, const uint8_t *add_mask,
+                        void *dx, const void *bn_x, const uint8_t *bn_mask, const float *bn_save, float *bn_part,
+                        void *stream);
 int r48_conv3x3(const void *x, int64_t boards, int32_t cin, const void *wfrag, const float *bias, const void *add,
                 void *y, float *stats, void *stream);
 /* dw fp32 [64][cin][3][3] = sum over boards and in-grid cells of dy[b][p][co] x[b][p + off(t)][ci];

@@ -42,7 +42,7 @@ SIGNATURES = {
     "r48_bn_forward_stats": (C.c_int, [_P, _I32, _P, _P, _I64, _I32, _P, _P, _P, _P, C.c_float, C.c_float, _I32, _P,
                                        _P, _P, _P, _P]),
     "r48_bn_backward_part": (C.c_int, [_P, _I32, _P, _P, _P, _I64, _I32, _P, _P, _P, _P, _P, _P, _P, _P]),
-    "r48_conv3x3_bn_grad": (C.c_int, [_P, _I64, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "r48_conv3x3_bn_grad": (C.c_int, [_P, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "r48_bn_backward": (C.c_int, [_P, _P, _P, _P, _I64, _I32, _P, _P, _I32, _P, _P, _P, _P, _P, _P]),
     "r48_board_onehot": (C.c_int, [_P, _I64, _I32, _P, _P]),
     "r48_board_onehot32": (C.c_int, [_P, _I64, _P, _P]),

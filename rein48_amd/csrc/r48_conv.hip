@@ -102,7 +102,10 @@ constexpr int kConvWaves = 8;
 constexpr int kOutPitch = 4 * 64 + 8;      // bf16 per board in the output-row staging (+16 B: banks)
 
 // ADD: y += add[b][p][co] (bf16, the same layout as y) before the bf16 rounding -- the data
-// gradient of a basic block's first conv plus the gradient of the identity path.
+// gradient of a basic block's first conv plus the gradient of the identity path. ADD = 2: the
+// identity path's gradient is add . [add_mask bit] (add = the gradient reaching the block's output
+// ReLU, add_mask its forward mask, one byte per 8 channels): the masked copy the BN backward would
+// otherwise write out and this conv read back is formed here from the mask byte instead.
 // STATS: the per-channel sums S1 = sum y, S2 = sum y^2 of the bf16 outputs (the statistics of the
 // training-mode BN that follows), accumulated from the staged 16-byte pieces (a lane's pieces are
 // always the same 8 channels), one record [S1 64][S2 64] per workgroup (the grid is then exactly
@@ -121,7 +124,7 @@ constexpr int kOutPitch = 4 * 64 + 8;      // bf16 per board in the output-row s
 // backward. Same arithmetic and bf16 rounding as k_bn_apply, so z equals the apply pass's output.
 // A row is transformed just before its first use (output row r - 1), one row-load after it was
 // issued, so the loads stay ahead of the MFMAs.
-template <int NC, bool ADD, int SM, int IN = 0>
+template <int NC, int ADD, int SM, int IN = 0>
 __global__ __launch_bounds__(64 * kConvWaves, 1) void k_conv3x3(const uint16_t *__restrict__ x, int64_t boards,
                                                                const uint4 *__restrict__ wfrag,
                                                                const float *__restrict__ bias,
@@ -133,7 +136,8 @@ __global__ __launch_bounds__(64 * kConvWaves, 1) void k_conv3x3(const uint16_t *
                                                                const float *__restrict__ coef = nullptr,
                                                                const uint16_t *__restrict__ res = nullptr,
                                                                uint16_t *__restrict__ z_out = nullptr,
-                                                               uint8_t *__restrict__ m_out = nullptr)
+                                                               uint8_t *__restrict__ m_out = nullptr,
+                                                               const uint8_t *__restrict__ add_mask = nullptr)
 {
     constexpr bool STATS = SM != 0;
     constexpr int PO = STATS ? 1 : 2;
@@ -242,13 +246,18 @@ __global__ __launch_bounds__(64 * kConvWaves, 1) void k_conv3x3(const uint16_t *
             for (int oh = 0; oh < 4 / PO; oh++) {   // passes of PO row tiles
                 f32x4 acc[4][PO];                    // [output column][row tile PO oh + o]
                 uint2 ad[4][PO];
+                uint32_t am[4][PO];   // ADD = 2: the mask byte of the lane's 4 channels (bits 4 (g & 1) ..)
                 if (ADD) {
-                    const uint16_t *ar = add + (live ? b : 0) * 16 * kCout + 4 * g;
+                    const int64_t bb = live ? b : 0;
+                    const uint16_t *ar = add + bb * 16 * kCout + 4 * g;
 #pragma unroll
                     for (int col = 0; col < 4; col++)
 #pragma unroll
-                        for (int o = 0; o < PO; o++)
+                        for (int o = 0; o < PO; o++) {
                             ad[col][o] = *reinterpret_cast<const uint2 *>(ar + (4 * r + col) * kCout + 16 * (PO * oh + o));
+                            if (ADD == 2)
+                                am[col][o] = add_mask[(bb * 16 + 4 * r + col) * (kCout / 8) + 2 * (PO * oh + o) + (g >> 1)];
+                        }
                 }
 #pragma unroll
                 for (int k = 0; k < 9 * NC; k++) {
@@ -278,6 +287,11 @@ __global__ __launch_bounds__(64 * kConvWaves, 1) void k_conv3x3(const uint16_t *
                     for (int col = 0; col < 4; col++)
 #pragma unroll
                         for (int o = 0; o < PO; o++) {
+                            if (ADD == 2) {   // masked-off channels add +0, as the written-out copy did
+                                const uint32_t mb = am[col][o] >> (4 * (g & 1));
+                                ad[col][o].x &= (mb & 1u ? 0xFFFFu : 0u) | (mb & 2u ? 0xFFFF0000u : 0u);
+                                ad[col][o].y &= (mb & 4u ? 0xFFFFu : 0u) | (mb & 8u ? 0xFFFF0000u : 0u);
+                            }
                             acc[col][o][0] += __uint_as_float(ad[col][o].x << 16);
                             acc[col][o][1] += __uint_as_float(ad[col][o].x & 0xFFFF0000u);
                             acc[col][o][2] += __uint_as_float(ad[col][o].y << 16);
@@ -960,15 +974,15 @@ int r48_conv3x3(const void *x, int64_t boards, int32_t cin, const void *wfrag, c
     const uint8_t *nm = nullptr;
     const float *ns = nullptr;
     if (cin == 64 && add)
-        hipLaunchKernelGGL((k_conv3x3<2, true, 0>), g, blk, 0, s, xs, boards, wf, bias, a, ys, stats, nx, nm, ns);
+        hipLaunchKernelGGL((k_conv3x3<2, 1, 0>), g, blk, 0, s, xs, boards, wf, bias, a, ys, stats, nx, nm, ns);
     else if (cin == 64 && stats)
-        hipLaunchKernelGGL((k_conv3x3<2, false, 1>), g, blk, 0, s, xs, boards, wf, bias, a, ys, stats, nx, nm, ns);
+        hipLaunchKernelGGL((k_conv3x3<2, 0, 1>), g, blk, 0, s, xs, boards, wf, bias, a, ys, stats, nx, nm, ns);
     else if (cin == 64)
-        hipLaunchKernelGGL((k_conv3x3<2, false, 0>), g, blk, 0, s, xs, boards, wf, bias, a, ys, stats, nx, nm, ns);
+        hipLaunchKernelGGL((k_conv3x3<2, 0, 0>), g, blk, 0, s, xs, boards, wf, bias, a, ys, stats, nx, nm, ns);
     else if (stats)
-        hipLaunchKernelGGL((k_conv3x3<1, false, 1>), g, blk, 0, s, xs, boards, wf, bias, a, ys, stats, nx, nm, ns);
+        hipLaunchKernelGGL((k_conv3x3<1, 0, 1>), g, blk, 0, s, xs, boards, wf, bias, a, ys, stats, nx, nm, ns);
     else
-        hipLaunchKernelGGL((k_conv3x3<1, false, 0>), g, blk, 0, s, xs, boards, wf, bias, a, ys, stats, nx, nm, ns);
+        hipLaunchKernelGGL((k_conv3x3<1, 0, 0>), g, blk, 0, s, xs, boards, wf, bias, a, ys, stats, nx, nm, ns);
     return launched("k_conv3x3");
 }
 
@@ -986,17 +1000,20 @@ int r48_conv3x3_bn_in(const void *x, int64_t boards, const void *wfrag, const fl
     const uint16_t *xs = (const uint16_t *)x, *rs = (const uint16_t *)residual;
     const uint4 *wf = (const uint4 *)wfrag;
     if (residual)
-        hipLaunchKernelGGL((k_conv3x3<2, false, 1, 2>), g, blk, 0, s, xs, boards, wf, bias, nullptr, (uint16_t *)y, stats,
+        hipLaunchKernelGGL((k_conv3x3<2, 0, 1, 2>), g, blk, 0, s, xs, boards, wf, bias, nullptr, (uint16_t *)y, stats,
                            nullptr, nullptr, nullptr, coef, rs, (uint16_t *)z_out, mask_out);
     else
-        hipLaunchKernelGGL((k_conv3x3<2, false, 1, 1>), g, blk, 0, s, xs, boards, wf, bias, nullptr, (uint16_t *)y, stats,
+        hipLaunchKernelGGL((k_conv3x3<2, 0, 1, 1>), g, blk, 0, s, xs, boards, wf, bias, nullptr, (uint16_t *)y, stats,
                            nullptr, nullptr, nullptr, coef, rs, (uint16_t *)z_out, mask_out);
     return launched("k_conv3x3 (bn in)");
 }
 
-int r48_conv3x3_bn_grad(const void *dy, int64_t boards, const void *wfrag, const void *add, void *dx,
-                        const void *bn_x, const uint8_t *bn_mask, const float *bn_save, float *bn_part, void *stream)
+int r48_conv3x3_bn_grad(const void *dy, int64_t boards, const void *wfrag, const void *add, const uint8_t *add_mask,
+                        void *dx, const void *bn_x, const uint8_t *bn_mask, const float *bn_save, float *bn_part,
+                        void *stream)
 {
+    if (add_mask && !add)
+        return fail(R48_EINVAL, "r48_conv3x3_bn_grad: add_mask without add");
     if (!dy || !wfrag || !dx || !bn_x || !bn_mask || !bn_save || !bn_part || boards < 1)
         return fail(R48_EINVAL, "r48_conv3x3_bn_grad: NULL argument or boards < 1");
     if ((reinterpret_cast<uintptr_t>(dy) | reinterpret_cast<uintptr_t>(wfrag) | reinterpret_cast<uintptr_t>(dx) |
@@ -1007,11 +1024,14 @@ int r48_conv3x3_bn_grad(const void *dy, int64_t boards, const void *wfrag, const
     hipStream_t s = (hipStream_t)stream;
     const uint16_t *xs = (const uint16_t *)dy, *a = (const uint16_t *)add, *bx = (const uint16_t *)bn_x;
     const uint4 *wf = (const uint4 *)wfrag;
-    if (add)
-        hipLaunchKernelGGL((k_conv3x3<2, true, 2>), g, blk, 0, s, xs, boards, wf, nullptr, a, (uint16_t *)dx, bn_part,
+    if (add_mask)
+        hipLaunchKernelGGL((k_conv3x3<2, 2, 2>), g, blk, 0, s, xs, boards, wf, nullptr, a, (uint16_t *)dx, bn_part,
+                           bx, bn_mask, bn_save, nullptr, nullptr, nullptr, nullptr, add_mask);
+    else if (add)
+        hipLaunchKernelGGL((k_conv3x3<2, 1, 2>), g, blk, 0, s, xs, boards, wf, nullptr, a, (uint16_t *)dx, bn_part,
                            bx, bn_mask, bn_save);
     else
-        hipLaunchKernelGGL((k_conv3x3<2, false, 2>), g, blk, 0, s, xs, boards, wf, nullptr, a, (uint16_t *)dx,
+        hipLaunchKernelGGL((k_conv3x3<2, 0, 2>), g, blk, 0, s, xs, boards, wf, nullptr, a, (uint16_t *)dx,
                            bn_part, bx, bn_mask, bn_save);
     return launched("k_conv3x3 (bn grad)");
 }

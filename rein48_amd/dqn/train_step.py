@@ -17,7 +17,10 @@ autograd's bookkeeping, and with the fusions it cannot express:
     (r48_conv3x3_bn_grad): its output IS that BN's output gradient, so BN's backward is finish +
     apply with no reduction pass (only the last BN, fed by the head, reduces on its own);
   * a basic block's input gradient (first conv's data gradient + the identity path's gradient)
-    is summed in the data-gradient conv's epilogue (r48_conv3x3 `add`), not by a separate add;
+    is summed in the data-gradient conv's epilogue (r48_conv3x3_bn_grad `add`), not by a separate
+    add -- and the identity path's gradient (the block output's gradient through its ReLU) is formed
+    there from that gradient and the ReLU mask (`add_mask`), so the BN backward writes no masked
+    copy of it (134 MB written and read back per block at the 64K minibatch);
   * parameter gradients are written straight into their .grad views of the flat gradient buffer
     (FlatParams): the convs' weight-gradient reduction, BN's dgamma/dbeta, the head's weight and
     bias gradient (one record);
@@ -65,7 +68,7 @@ class ResNetTrainStep:
                 "m": [torch.empty((B * 16, 8), dtype=torch.uint8, device=dev) for _ in range(9)],
                 "save": [torch.empty(128, dtype=torch.float32, device=dev) for _ in range(9)],
                 "coef": [torch.empty(128, dtype=torch.float32, device=dev) for _ in range(9)],
-                "g": [act() for _ in range(6)],                 # gradient scratch
+                "g": [act() for _ in range(5)],                 # gradient scratch
                 "stem_dw": torch.empty((64, 32, 3, 3), dtype=torch.float32, device=dev),
                 "loss": torch.empty(2, dtype=torch.float32, device=dev),        # mean loss, mean Q(s, a)
                 "stats": torch.empty(int(_lib.load().r48_conv_stats_floats()), dtype=torch.float32, device=dev),
@@ -105,10 +108,10 @@ class ResNetTrainStep:
                                                ptr(bn.weight), ptr(save), ptr(_workspace(rows, 64, y.device)), ptr(dy),
                                                ptr(dres), ptr(bn.weight.grad), ptr(bn.bias.grad), _stream(y)))
 
-    def _conv_bn_grad(self, dy, frags, out, k, add=None, part=None):
-        """out = data gradient conv of dy (+ add) -- the gradient reaching BN k's output -- with BN
-        k's backward reduction summed into `part` in the same pass."""
-        check(_lib.load().r48_conv3x3_bn_grad(ptr(dy), dy.shape[0], ptr(frags), ptr(add), ptr(out),
+    def _conv_bn_grad(self, dy, frags, out, k, add=None, add_mask=None, part=None):
+        """out = data gradient conv of dy (+ add . [add_mask]) -- the gradient reaching BN k's output --
+        with BN k's backward reduction summed into `part` in the same pass."""
+        check(_lib.load().r48_conv3x3_bn_grad(ptr(dy), dy.shape[0], ptr(frags), ptr(add), ptr(add_mask), ptr(out),
                                               ptr(self._Y[k]), ptr(self._M[k]), ptr(self._S[k]), ptr(part),
                                               _stream(dy)))
         return out
@@ -172,8 +175,9 @@ class ResNetTrainStep:
             hw.copy_(dw)
             hb.copy_(db)
         # per block, backwards: BN2 (+ identity) -> conv2 data/weight gradients -> BN1 -> conv1
-        # data gradient + identity gradient (one epilogue) and weight gradient. The incoming
-        # gradient alternates between g[0] and g[5]; g[1..4] hold the block's temporaries.
+        # data gradient + identity gradient (one epilogue: cur . [M[i2]]) and weight gradient. The
+        # incoming gradient alternates between g[0] and g[4] (cur stays intact until the block's
+        # last conv has read it); g[1..3] hold the block's temporaries.
         # Every data-gradient conv also reduces the BN backward of the layer below (its output is
         # that BN's output gradient); only BN 8's reduction (the head's gradient) runs on its own.
         self._Y, self._M, self._S = Y, M, S
@@ -182,16 +186,16 @@ class ResNetTrainStep:
         for b in range(3, -1, -1):
             i1, i2 = 1 + 2 * b, 2 + 2 * b
             h_in = Z[i1 - 1]
-            dy2, dres, dz1, dy1 = G[1], G[2], G[3], G[4]
+            dy2, dz1, dy1 = G[1], G[2], G[3]
             if b == 3:
-                self._bn_backward(i2, cur, M[i2], Y[i2], S[i2], dy2, dres=dres)
+                self._bn_backward(i2, cur, M[i2], Y[i2], S[i2], dy2)
             else:
-                self._bn_backward_part(i2, part, cur, M[i2], Y[i2], S[i2], dy2, dres=dres)
+                self._bn_backward_part(i2, part, cur, M[i2], Y[i2], S[i2], dy2)
             self._conv_bn_grad(dy2, dgrad[i2], dz1, i1, part=part)
             conv3x3_wgrad(dy2, Z[i1], out=convs[i2].weight.grad)
             self._bn_backward_part(i1, part, dz1, M[i1], Y[i1], S[i1], dy1)
-            nxt = G[5] if cur is G[0] else G[0]
-            self._conv_bn_grad(dy1, dgrad[i1], nxt, i1 - 1, add=dres, part=part)
+            nxt = G[4] if cur is G[0] else G[0]
+            self._conv_bn_grad(dy1, dgrad[i1], nxt, i1 - 1, add=cur, add_mask=M[i2], part=part)
             conv3x3_wgrad(dy1, h_in, out=convs[i1].weight.grad)
             cur = nxt
         dy0 = G[1]

@@ -470,29 +470,34 @@ def test_conv3x3_stats_match_fp64_sums(ci, B):
         assert float((got - want).abs().max()) <= 1e-5 * float(want.abs().max())
 
 
-@pytest.mark.parametrize("B,with_add", [(4099, False), (4099, True), (1037, True)])
+@pytest.mark.parametrize("B,with_add", [(4099, False), (4099, True), (1037, True), (4099, "mask"), (1037, "mask")])
 def test_conv3x3_bn_grad_reduction_matches_fp64(B, with_add):
     """r48_conv3x3_bn_grad (the data-gradient conv with the BN-backward reduction of the layer
     below in its epilogue): its output equals the plain r48_conv3x3 launch's bit for bit, and its
     per-CU records summed equal the fp64 per-channel sums of g = out . [mask bit] and of
     g (bn_x - mean) (fp32 partials: within 1e-5 of the sum of the terms' magnitudes). Ragged board
-    counts, with and without the residual add."""
+    counts, with and without the residual add; "mask": the add masked by a ReLU mask in the kernel
+    (add_mask) equals the plain launch with the masked add written out (zeros where a bit is 0)."""
     import ctypes
     from rein48_amd import _lib
     from rein48_amd.dqn.conv import conv3x3, pack_conv_dgrad
-    g = torch.Generator(device="cpu").manual_seed(B + with_add)
+    g = torch.Generator(device="cpu").manual_seed(B + (2 if with_add == "mask" else int(with_add)))
     frags = pack_conv_dgrad((torch.randn(64, 64, 3, 3, generator=g) * 0.1).to(DEV))
     dy = torch.randn(B, 16, 64, generator=g).to(DEV).to(torch.bfloat16)
     add = torch.randn(B, 16, 64, generator=g).to(DEV).to(torch.bfloat16) if with_add else None
     bn_x = (torch.randn(B, 16, 64, generator=g) + 3.0).to(DEV).to(torch.bfloat16)
     mask = torch.randint(0, 256, (B * 16, 8), generator=g, dtype=torch.uint8).to(DEV)
     save = torch.cat([torch.randn(64, generator=g) + 3.0, torch.rand(64, generator=g) + 0.5]).to(DEV)
+    add_mask = torch.randint(0, 256, (B * 16, 8), generator=g, dtype=torch.uint8).to(DEV) if with_add == "mask" else None
     L = _lib.load()
     part = torch.full((int(L.r48_conv_stats_floats()),), float("nan"), dtype=torch.float32, device=DEV)
     out = torch.empty_like(dy)
-    _lib.check(L.r48_conv3x3_bn_grad(_lib.ptr(dy), B, _lib.ptr(frags), _lib.ptr(add), _lib.ptr(out),
+    _lib.check(L.r48_conv3x3_bn_grad(_lib.ptr(dy), B, _lib.ptr(frags), _lib.ptr(add), _lib.ptr(add_mask), _lib.ptr(out),
                                      _lib.ptr(bn_x), _lib.ptr(mask), _lib.ptr(save), _lib.ptr(part),
                                      ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
+    if add_mask is not None:
+        abits = ((add_mask.long().unsqueeze(-1) >> torch.arange(8, device=DEV)) & 1).reshape(B, 16, 64).bool()
+        add = torch.where(abits, add, torch.zeros((), dtype=add.dtype, device=DEV))
     assert torch.equal(out, conv3x3(dy, frags, add=add))
     bits = ((mask.long().unsqueeze(-1) >> torch.arange(8, device=DEV)) & 1).reshape(B * 16, 64).bool()
     gd = torch.where(bits, out.reshape(-1, 64).double(), torch.zeros((), dtype=torch.float64, device=DEV))
@@ -602,7 +607,7 @@ def test_conv3x3_bn_grad_at_bench_size_matches_fp64(B, with_add):
     L = _lib.load()
     part = torch.full((int(L.r48_conv_stats_floats()),), float("nan"), dtype=torch.float32, device=DEV)
     out = torch.empty_like(dy)
-    _lib.check(L.r48_conv3x3_bn_grad(_lib.ptr(dy), B, _lib.ptr(frags), _lib.ptr(add), _lib.ptr(out),
+    _lib.check(L.r48_conv3x3_bn_grad(_lib.ptr(dy), B, _lib.ptr(frags), _lib.ptr(add), None, _lib.ptr(out),
                                      _lib.ptr(bn_x), _lib.ptr(mask), _lib.ptr(save), _lib.ptr(part),
                                      ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
     assert torch.equal(out, conv3x3(dy, frags, add=add))

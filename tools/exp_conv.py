@@ -44,9 +44,9 @@ stats = None
 part = None
 
 
-def bn_grad(dy_, add_, bnx, mask):
+def bn_grad(dy_, add_, bnx, mask, add_mask=None):
     out = torch.empty_like(dy_)
-    C.check(_lib.load().r48_conv3x3_bn_grad(C.ptr(dy_), B, C.ptr(f64), C.ptr(add_), C.ptr(out), C.ptr(bnx),
+    C.check(_lib.load().r48_conv3x3_bn_grad(C.ptr(dy_), B, C.ptr(f64), C.ptr(add_), C.ptr(add_mask), C.ptr(out), C.ptr(bnx),
                                             C.ptr(mask), C.ptr(save), C.ptr(part), C._stream(dy_)))
     return out
 
@@ -71,7 +71,7 @@ def timed(fn, reps=20):
 
 # algorithmic HBM bytes: activations in + out (bf16); wgrad reads dy and x
 io = {"fwd64": B * 16 * (64 + 64) * 2, "fwd32": B * 16 * (32 + 64) * 2, "add64": B * 16 * (64 + 64 + 64) * 2,
-      "fwd64s": B * 16 * (64 + 64) * 2, "dg64bn": B * 16 * (3 * 64 * 2 + 8), "add64bn": B * 16 * (4 * 64 * 2 + 8),
+      "fwd64s": B * 16 * (64 + 64) * 2, "dg64bn": B * 16 * (3 * 64 * 2 + 8), "add64bn": B * 16 * (4 * 64 * 2 + 8), "addm64bn": B * 16 * (4 * 64 * 2 + 16),
       "wgrad64": B * 16 * (64 + 64) * 2, "wgrad32": B * 16 * (64 + 32) * 2}
 for path in libs:
     _lib.LIB_PATH, _lib._lib = path, None
@@ -83,6 +83,7 @@ for path in libs:
             "fwd64s": lambda: C.conv3x3(rot(x64s), f64, bias, stats=stats),
             "dg64bn": lambda: bn_grad(rot(dys), None, rot(x64s), rot(masks)),
             "add64bn": lambda: bn_grad(rot(dys), rot(x64s), rot(x64s), rot(masks)),
+            "addm64bn": lambda: bn_grad(rot(dys), rot(x64s), rot(x64s), rot(masks), rot(masks)),
             "wgrad64": lambda: C.conv3x3_wgrad(rot(dys), rot(x64s)), "wgrad32": lambda: C.conv3x3_wgrad(rot(dys), rot(x32s))}
     line = []
     for k, fn in runs.items():
