@@ -434,7 +434,7 @@ def dqn_config5(dev, seed, n_boards, steps=5, world=1, warmup=3):
         tr.replay.store(st, a, reward.float(), tr.env.boards, done)
         tr.steps += 1
         e[2].record(s)
-        out = tr.update()
+        out = tr.update(sync=False)                   # the loss stays on the GPU: no host wait inside
         e[3].record(s)
         torch.cuda.synchronize(dev)
         act.append(e[0].elapsed_time(e[1]))
@@ -454,7 +454,7 @@ def dqn_config5(dev, seed, n_boards, steps=5, world=1, warmup=3):
             "env_steps_per_s": world * n_boards / ((a_ms + e_ms + u_ms) * 1e-3),
             "act_useful_TFLOPs": n_boards * useful / (a_ms * 1e-3) / 1e12,
             "act_frac_of_bf16_dense_peak": n_boards * useful / (a_ms * 1e-3) / 2.5e15,
-            "loss": out["loss"]}
+            "loss": float(out["loss"])}
 
 
 def _free_port():

@@ -379,11 +379,12 @@ int r48_board_onehot(const int8_t *boards, int64_t n, int32_t out_dtype, void *o
  * first argmax. */
 int r48_egreedy_actions(const float *q, int64_t n, float eps, uint64_t seed, int64_t gid0, uint32_t ctr,
                         int8_t *actions, void *stream);
-/* TD target y[i] = reward[i] + gamma * (1 - done[i]) * q_next_target[i][a*], a* = argmax of
- * q_next_online[i] (double DQN) or of q_next_target[i] when q_next_online is NULL. done
- * nullable (= 0). Q arrays float[n][4], 16-byte aligned. */
+/* TD target y[i] = R + gamma * (1 - done[i]) * q_next_target[i][a*], a* = argmax of
+ * q_next_online[i] (double DQN) or of q_next_target[i] when q_next_online is NULL; R = reward[i],
+ * or log2(1 + reward[i]) (fp32, as torch.log2(1.0 + r)) when log2_reward != 0 -- the trainer's
+ * reward transform folded in. done nullable (= 0). Q arrays float[n][4], 16-byte aligned. */
 int r48_td_target(const float *reward, const uint8_t *done, const float *q_next_target,
-                  const float *q_next_online, int64_t n, float gamma, float *y, void *stream);
+                  const float *q_next_online, int64_t n, float gamma, int32_t log2_reward, float *y, void *stream);
 
 /* Huber loss (smooth L1, beta 1) of the update: d = q[i][action[i]] - y[i]; out[0] = mean loss,
  * out[1] = mean q[i][action[i]]; dq[i][a] = clamp(d, -1, 1) / n for a = action[i], else 0 (the

@@ -57,7 +57,7 @@ SIGNATURES = {
     "r48_q_head_workspace_floats": (_I64, []),
     "r48_q_head_backward": (C.c_int, [_P, _P, _I64, _P, _P, _P, _P, _P]),
     "r48_egreedy_actions": (C.c_int, [_P, _I64, C.c_float, _U64, _I64, _U32, _P, _P]),
-    "r48_td_target": (C.c_int, [_P, _P, _P, _P, _I64, C.c_float, _P, _P]),
+    "r48_td_target": (C.c_int, [_P, _P, _P, _P, _I64, C.c_float, _I32, _P, _P]),
     "r48_replay_create": (C.c_int, [C.POINTER(_P), C.c_int, _I64, _U32, _U64]),
     "r48_replay_destroy": (C.c_int, [_P]),
     "r48_replay_capacity": (_I64, [_P]),

@@ -22,7 +22,7 @@
 //   ring of kRing buffers; the x operand of tap t is the same image read with per-lane row addresses
 //   shifted by the tap (rows outside the grid point at a zero row). 8 waves, each owning one
 //   input-channel tile and its share of the output tiles, accumulate in AGPRs. Each workgroup writes
-//   one fp32 record; k_conv_wgrad_reduce1/2 sum the records in a fixed order (deterministic).
+//   one fp32 record; k_conv_wgrad_reduce sums the records in a fixed order (deterministic).
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -391,7 +391,7 @@ constexpr int kKSteps = kStepRows / 32;
 constexpr int kZeroRow = kStepRows;                              // zero band: kZeroRow + 32 ks
 constexpr int kXRows = kStepRows + 32 * (kKSteps - 1) + 1;
 constexpr int kRing = 3;                                          // LDS buffers: 2 steps ahead
-constexpr int kRedGroup = 16;                                     // records per first-pass group
+constexpr int kRedGroup = 16;                                     // records per group of records_sum16
 
 // chunk swizzle of image row `row`: XOR with row & 7 spreads a transposed read's 4 consecutive rows
 // over the bank row; XOR with 4 when row & 8 keeps the rows 8 apart (the lane groups g = 0, 1 of
@@ -610,52 +610,60 @@ __global__ __launch_bounds__(64 * kWgWaves, 1) void k_conv_wgrad(const uint16_t 
                 rec[(t * kCout + 16 * (cot0 + j) + 4 * g + i) * CIN + 16 * ct + i16] = acc[t][j][i];
 }
 
-// Fixed-order sum of the n_rec records [t][co][ci] in two passes (deterministic): pass 1 sums
-// groups of kRedGroup consecutive records (one lane per group and 4 record entries), pass 2 sums
-// the groups in order and writes torch's [co][ci][3][3] layout.
-template <int CIN>
-__global__ __launch_bounds__(256) void k_conv_wgrad_reduce1(const float4 *__restrict__ partials, int n_rec,
-                                                           float4 *__restrict__ groups)
+// Fixed-order sum of n_rec <= kRedGroup^2 records of len4 float4 entries in ONE pass: a block of
+// 256 threads takes 16 entries; thread (entry e, group q) sums records 16 q .. 16 q + 15 of its entry
+// in record order (beyond n_rec: + 0, as a shorter group), then the first group's threads add the
+// other groups' sums in group order through LDS -- the arithmetic of the former two-pass form
+// (groups, then the groups in order), so bit-identical to it, without the second launch and the
+// group round trip through memory.
+__device__ __forceinline__ bool records_sum16(const float4 *__restrict__ recs, int n_rec, int len4, float4 &out)
 {
-    constexpr int kQ = 9 * kCout * CIN / 4;                       // float4 entries per record
+    __shared__ float4 part[kRedGroup][16];
+    const int el = threadIdx.x & 15, q = threadIdx.x >> 4;
+    const int k = blockIdx.x * 16 + el;
     const int n_grp = (n_rec + kRedGroup - 1) / kRedGroup;
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= kQ * n_grp)
-        return;
-    const int grp = i / kQ, k = i % kQ;
-    const int r0 = grp * kRedGroup, r1 = r0 + kRedGroup < n_rec ? r0 + kRedGroup : n_rec;
-    float4 v[kRedGroup];
+    if (k < len4 && q < n_grp) {
+        const int r0 = q * kRedGroup;
+        float4 v[kRedGroup];
 #pragma unroll
-    for (int r = 0; r < kRedGroup; r++)
-        v[r] = r0 + r < r1 ? partials[(int64_t)(r0 + r) * kQ + k] : make_float4(0.f, 0.f, 0.f, 0.f);
-    float4 s = v[0];
+        for (int r = 0; r < kRedGroup; r++)
+            v[r] = r0 + r < n_rec ? recs[(int64_t)(r0 + r) * len4 + k] : make_float4(0.f, 0.f, 0.f, 0.f);
+        float4 t = v[0];
 #pragma unroll
-    for (int r = 1; r < kRedGroup; r++) {
-        s.x += v[r].x;
-        s.y += v[r].y;
-        s.z += v[r].z;
-        s.w += v[r].w;
+        for (int r = 1; r < kRedGroup; r++) {
+            t.x += v[r].x;
+            t.y += v[r].y;
+            t.z += v[r].z;
+            t.w += v[r].w;
+        }
+        part[q][el] = t;
     }
-    groups[(int64_t)grp * kQ + k] = s;
+    __syncthreads();
+    if (q != 0 || k >= len4)
+        return false;
+    float4 t = part[0][el];
+    for (int g = 1; g < n_grp; g++) {
+        const float4 v = part[g][el];
+        t.x += v.x;
+        t.y += v.y;
+        t.z += v.z;
+        t.w += v.w;
+    }
+    out = t;
+    return true;
 }
 
+// the weight gradient's records [t][co][ci] summed, written in torch's [co][ci][3][3] layout
 template <int CIN>
-__global__ __launch_bounds__(256) void k_conv_wgrad_reduce2(const float4 *__restrict__ groups, int n_grp,
-                                                           float *__restrict__ out)
+__global__ __launch_bounds__(256) void k_conv_wgrad_reduce(const float4 *__restrict__ partials, int n_rec,
+                                                          float *__restrict__ out)
 {
-    constexpr int kQ = 9 * kCout * CIN / 4;
-    const int k = blockIdx.x * 256 + threadIdx.x;                // float4 entry: (t * 64 + co) * CIN + 4 k'
-    if (k >= kQ)
+    constexpr int kQ = 9 * kCout * CIN / 4;                       // float4 entries per record
+    float4 s;
+    if (!records_sum16(partials, n_rec, kQ, s))
         return;
-    float4 s = groups[k];
-    for (int r = 1; r < n_grp; r++) {
-        const float4 v = groups[(int64_t)r * kQ + k];
-        s.x += v.x;
-        s.y += v.y;
-        s.z += v.z;
-        s.w += v.w;
-    }
-    const int e = 4 * k, t = e / (kCout * CIN), co = (e / CIN) % kCout, ci = e % CIN;
+    const int e = 4 * (blockIdx.x * 16 + (threadIdx.x & 15)), t = e / (kCout * CIN), co = (e / CIN) % kCout,
+              ci = e % CIN;
     float *o = out + (co * CIN + ci) * 9 + t;
     o[0] = s.x;
     o[9] = s.y;
@@ -746,7 +754,7 @@ __global__ __launch_bounds__(64 * kHeadWaves) void k_q_head_fwd(const uint16_t *
 // dh[b][k] = bf16(sum_a g[a] W[a][k]); the weight gradient sum_b g[a] h[b][k] and the bias gradient
 // sum_b g[a] accumulate per lane in fp32 (lane l owns k = 16 l .. + 15 of all 4 rows), the waves of a
 // workgroup are summed through LDS in a fixed order, and each workgroup writes one record of
-// kHeadK * 4 + 4 floats (summed by k_records_reduce*: deterministic).
+// kHeadK * 4 + 4 floats (summed by k_records_reduce: deterministic).
 constexpr int kHeadRec = 4 * kHeadK + 4;
 
 __global__ __launch_bounds__(64 * kHeadWaves) void k_q_head_bwd(const float *__restrict__ dq,
@@ -834,50 +842,17 @@ __global__ __launch_bounds__(64 * kHeadWaves) void k_q_head_bwd(const float *__r
     }
 }
 
-// fixed-order sums of n_rec records of `len` floats (len % 4 == 0): pass 1 sums groups of
-// kRedGroup consecutive records, pass 2 the groups in order, the result rounded through bf16 when
-// round_bf16 (the bf16 parameter-gradient contract of nets.py's linear)
-__global__ __launch_bounds__(256) void k_records_reduce1(const float4 *__restrict__ recs, int n_rec, int len4,
-                                                        float4 *__restrict__ groups)
+// fixed-order sum of n_rec records of `len` floats (len % 4 == 0, records_sum16's order), the
+// result rounded through bf16 when round_bf16 (the bf16 parameter-gradient contract of nets.py's linear)
+__global__ __launch_bounds__(256) void k_records_reduce(const float4 *__restrict__ recs, int n_rec, int len4,
+                                                       int round_bf16, float4 *__restrict__ out)
 {
-    const int n_grp = (n_rec + kRedGroup - 1) / kRedGroup;
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= len4 * n_grp)
+    float4 s;
+    if (!records_sum16(recs, n_rec, len4, s))
         return;
-    const int grp = i / len4, k = i % len4;
-    const int r0 = grp * kRedGroup, r1 = r0 + kRedGroup < n_rec ? r0 + kRedGroup : n_rec;
-    float4 v[kRedGroup];
-#pragma unroll
-    for (int r = 0; r < kRedGroup; r++)
-        v[r] = r0 + r < r1 ? recs[(int64_t)(r0 + r) * len4 + k] : make_float4(0.f, 0.f, 0.f, 0.f);
-    float4 s = v[0];
-#pragma unroll
-    for (int r = 1; r < kRedGroup; r++) {
-        s.x += v[r].x;
-        s.y += v[r].y;
-        s.z += v[r].z;
-        s.w += v[r].w;
-    }
-    groups[(int64_t)grp * len4 + k] = s;
-}
-
-__global__ __launch_bounds__(256) void k_records_reduce2(const float4 *__restrict__ groups, int n_grp, int len4,
-                                                        int round_bf16, float4 *__restrict__ out)
-{
-    const int k = blockIdx.x * 256 + threadIdx.x;
-    if (k >= len4)
-        return;
-    float4 s = groups[k];
-    for (int r = 1; r < n_grp; r++) {
-        const float4 v = groups[(int64_t)r * len4 + k];
-        s.x += v.x;
-        s.y += v.y;
-        s.z += v.z;
-        s.w += v.w;
-    }
     if (round_bf16)
         s = make_float4(bf16_round(s.x), bf16_round(s.y), bf16_round(s.z), bf16_round(s.w));
-    out[k] = s;
+    out[blockIdx.x * 16 + (threadIdx.x & 15)] = s;
 }
 
 // ------------------------------------------------------------------- weight fragments
@@ -1051,23 +1026,19 @@ int r48_conv3x3_wgrad(const void *dy, const void *x, int64_t boards, int32_t cin
         15u)
         return fail(R48_EINVAL, "r48_conv3x3_wgrad: dy, x and workspace must be 16-byte aligned");
     const int grid = cu_count();
-    const int n_grp = (grid + kRedGroup - 1) / kRedGroup;
-    const int64_t rec = (int64_t)9 * kCout * cin;
-    const int q = (int)(rec / 4);
+    static_assert(kPersistentGroups <= kRedGroup * kRedGroup, "records_sum16 sums at most 256 records");
+    const int q = 9 * kCout * cin / 4;
     hipStream_t s = (hipStream_t)stream;
-    float4 *groups = reinterpret_cast<float4 *>(workspace + grid * rec);
     if (cin == 64) {
         hipLaunchKernelGGL(k_conv_wgrad<64>, dim3(grid), dim3(64 * kWgWaves), 0, s, (const uint16_t *)dy,
                            (const uint16_t *)x, boards, workspace);
-        hipLaunchKernelGGL(k_conv_wgrad_reduce1<64>, dim3((q * n_grp + 255) / 256), dim3(256), 0, s,
-                           (const float4 *)workspace, grid, groups);
-        hipLaunchKernelGGL(k_conv_wgrad_reduce2<64>, dim3((q + 255) / 256), dim3(256), 0, s, groups, n_grp, dw);
+        hipLaunchKernelGGL(k_conv_wgrad_reduce<64>, dim3((q + 15) / 16), dim3(256), 0, s, (const float4 *)workspace,
+                           grid, dw);
     } else {
         hipLaunchKernelGGL(k_conv_wgrad<32>, dim3(grid), dim3(64 * kWgWaves), 0, s, (const uint16_t *)dy,
                            (const uint16_t *)x, boards, workspace);
-        hipLaunchKernelGGL(k_conv_wgrad_reduce1<32>, dim3((q * n_grp + 255) / 256), dim3(256), 0, s,
-                           (const float4 *)workspace, grid, groups);
-        hipLaunchKernelGGL(k_conv_wgrad_reduce2<32>, dim3((q + 255) / 256), dim3(256), 0, s, groups, n_grp, dw);
+        hipLaunchKernelGGL(k_conv_wgrad_reduce<32>, dim3((q + 15) / 16), dim3(256), 0, s, (const float4 *)workspace,
+                           grid, dw);
     }
     return launched("k_conv_wgrad");
 }
@@ -1101,16 +1072,12 @@ int r48_q_head_backward(const float *dq, const void *h, int64_t boards, const vo
          reinterpret_cast<uintptr_t>(dw)) & 15u)
         return fail(R48_EINVAL, "r48_q_head_backward: all pointers must be 16-byte aligned");
     const int grid = cu_count();
-    const int n_grp = (grid + kRedGroup - 1) / kRedGroup;
     const int len4 = kHeadRec / 4;
     hipStream_t s = (hipStream_t)stream;
-    float4 *groups = reinterpret_cast<float4 *>(workspace + (int64_t)grid * kHeadRec);
     hipLaunchKernelGGL(k_q_head_bwd, dim3(grid), dim3(64 * kHeadWaves), 0, s, dq, (const uint16_t *)h, boards,
                        (const uint16_t *)w, (uint16_t *)dh, workspace);
-    hipLaunchKernelGGL(k_records_reduce1, dim3((len4 * n_grp + 255) / 256), dim3(256), 0, s,
-                       (const float4 *)workspace, grid, len4, groups);
-    hipLaunchKernelGGL(k_records_reduce2, dim3((len4 + 255) / 256), dim3(256), 0, s, groups, n_grp, len4, 1,
-                       (float4 *)dw);
+    hipLaunchKernelGGL(k_records_reduce, dim3((len4 + 15) / 16), dim3(256), 0, s, (const float4 *)workspace, grid,
+                       len4, 1, (float4 *)dw);
     return launched("k_q_head_bwd");
 }
 

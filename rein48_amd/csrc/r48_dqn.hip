@@ -93,7 +93,7 @@ __global__ __launch_bounds__(kBlock) void k_egreedy(const float *__restrict__ q,
     actions[i] = (int8_t)(u < eps ? (w[1] >> 30) : argmax4(qv));
 }
 
-template <bool DOUBLE>
+template <bool DOUBLE, bool LOG2>
 __global__ __launch_bounds__(kBlock) void k_td_target(const float *__restrict__ reward,
                                                       const uint8_t *__restrict__ done,
                                                       const float *__restrict__ q_next_target,
@@ -106,7 +106,8 @@ __global__ __launch_bounds__(kBlock) void k_td_target(const float *__restrict__ 
     const float4 qt = reinterpret_cast<const float4 *>(q_next_target)[i];
     const uint32_t a = DOUBLE ? argmax4(reinterpret_cast<const float4 *>(q_next_online)[i]) : argmax4(qt);
     const float boot = (done && done[i]) ? 0.0f : pick(qt, a);
-    y[i] = reward[i] + gamma * boot;
+    const float r = LOG2 ? log2f(1.0f + reward[i]) : reward[i];   // trainer.py _reward, torch.log2(1.0 + r)
+    y[i] = r + gamma * boot;
 }
 
 // ---- Huber loss of Q(s)[a] against the TD target and its gradient (DQNLearner.learn):
@@ -288,19 +289,26 @@ int r48_egreedy_actions(const float *q, int64_t n, float eps, uint64_t seed, int
 }
 
 int r48_td_target(const float *reward, const uint8_t *done, const float *q_next_target,
-                  const float *q_next_online, int64_t n, float gamma, float *y, void *stream)
+                  const float *q_next_online, int64_t n, float gamma, int32_t log2_reward, float *y, void *stream)
 {
     if (!reward || !q_next_target || !y || n < 0 || !aligned16(q_next_target) ||
         (q_next_online && !aligned16(q_next_online)))
         return fail(R48_EINVAL, "reward/q_next_target/y NULL, n < 0 or Q not 16-byte aligned");
     if (n == 0)
         return R48_OK;
-    if (q_next_online)
-        hipLaunchKernelGGL(k_td_target<true>, grid_for(n), dim3(kBlock), 0, (hipStream_t)stream, reward, done,
-                           q_next_target, q_next_online, n, gamma, y);
+    hipStream_t s = (hipStream_t)stream;
+    if (q_next_online && log2_reward)
+        hipLaunchKernelGGL((k_td_target<true, true>), grid_for(n), dim3(kBlock), 0, s, reward, done, q_next_target,
+                           q_next_online, n, gamma, y);
+    else if (q_next_online)
+        hipLaunchKernelGGL((k_td_target<true, false>), grid_for(n), dim3(kBlock), 0, s, reward, done, q_next_target,
+                           q_next_online, n, gamma, y);
+    else if (log2_reward)
+        hipLaunchKernelGGL((k_td_target<false, true>), grid_for(n), dim3(kBlock), 0, s, reward, done, q_next_target,
+                           nullptr, n, gamma, y);
     else
-        hipLaunchKernelGGL(k_td_target<false>, grid_for(n), dim3(kBlock), 0, (hipStream_t)stream, reward, done,
-                           q_next_target, nullptr, n, gamma, y);
+        hipLaunchKernelGGL((k_td_target<false, false>), grid_for(n), dim3(kBlock), 0, s, reward, done, q_next_target,
+                           nullptr, n, gamma, y);
     return launched("k_td_target");
 }
 

@@ -31,8 +31,9 @@ def egreedy_actions(q, eps, seed, ctr, gid0=0, out=None):
     return out
 
 
-def td_target(reward, done, q_next_target, q_next_online=None, gamma=0.99):
-    """y = r + gamma (1 - done) Q'(s', argmax) (double DQN when q_next_online is given)."""
+def td_target(reward, done, q_next_target, q_next_online=None, gamma=0.99, log2_reward=False):
+    """y = r + gamma (1 - done) Q'(s', argmax) (double DQN when q_next_online is given); r =
+    log2(1 + reward) when log2_reward (the trainer's reward transform, in the same launch)."""
     _dev(reward, "reward", torch.float32)
     _dev(q_next_target, "q_next_target", torch.float32)
     if done is not None:
@@ -41,5 +42,5 @@ def td_target(reward, done, q_next_target, q_next_online=None, gamma=0.99):
         _dev(q_next_online, "q_next_online", torch.float32)
     y = torch.empty_like(reward)
     check(_lib.load().r48_td_target(ptr(reward), ptr(done), ptr(q_next_target), ptr(q_next_online), reward.numel(),
-                                    float(gamma), ptr(y), _stream(reward)))
+                                    float(gamma), int(bool(log2_reward)), ptr(y), _stream(reward)))
     return y

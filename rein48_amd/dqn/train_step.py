@@ -160,7 +160,8 @@ class ResNetTrainStep:
                 conv3x3(Z[i1], fwd[i2], convs[i2].bias, out=Y[i2], stats=st)
                 self._bn_forward(i2, Y[i2], Z[i2], M[i2], S[i2], st, residual=h)
         h = Z[8].view(B, 1024)
-        q = q_head_forward(h, net.head.weight, net.head.bias)
+        hw_bf16 = net.head.weight.detach().to(torch.bfloat16)      # one cast for the head's two kernels
+        q = q_head_forward(h, hw_bf16, net.head.bias)
         # ---- Huber loss of Q(x)[action] and its gradient (d loss / d q): one kernel + one finish
         a8 = action if action.dtype == torch.int8 else action.to(torch.int8)
         dq = torch.empty_like(q)
@@ -170,7 +171,7 @@ class ResNetTrainStep:
         # ---- backward
         hw, hb = net.head.weight.grad, net.head.bias.grad
         fused_head = hb.data_ptr() == hw.data_ptr() + 4 * hw.numel()        # one record: weight rows, bias
-        dh, dw, db = q_head_backward(dq, h, net.head.weight, out=hw if fused_head else None)
+        dh, dw, db = q_head_backward(dq, h, hw_bf16, out=hw if fused_head else None)
         if not fused_head:
             hw.copy_(dw)
             hb.copy_(db)

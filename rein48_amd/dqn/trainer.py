@@ -112,16 +112,23 @@ class DQNLearner:
             p.requires_grad_(False)
         self.opt = Adam(self.flat, cfg.lr)
         self._train_step = None                           # train_step.ResNetTrainStep, built on first use
+        self._grad_overwritten = False                    # the last step was the fused one (learn)
         self.updates = 0
         self._version = 0                                 # bumped by every optimizer step / sync
 
-    def learn(self, x, action, y):
+    def learn(self, x, action, y, sync=True):
         """One synchronous step: Huber loss of Q(x)[action] against the TD target y, gradient
         averaged over the group, Adam, BN running statistics averaged over the group; the target
-        net follows every `target_sync` updates."""
+        net follows every `target_sync` updates. Returns {"loss", "q_mean"} as floats, or as 0-d GPU
+        tensors with sync=False (the host then never waits for the GPU inside an update)."""
         self.net.train()
-        self.flat.zero_grad()
-        if self._fused_step_ok(x):
+        fused = self._fused_step_ok(x)
+        if not (fused and self._grad_overwritten):
+            # the fused step WRITES every parameter gradient but the conv biases' (exactly zero, never
+            # written): after one zeroing, later fused steps need none (autograd accumulates: it does)
+            self.flat.zero_grad()
+        self._grad_overwritten = fused
+        if fused:
             if self._train_step is None:
                 from .train_step import ResNetTrainStep
                 self._train_step = ResNetTrainStep(self.net)
@@ -139,7 +146,10 @@ class DQNLearner:
         self.updates += 1
         if self.updates % self.cfg.target_sync == 0:
             self.sync_target()
-        return {"loss": float(loss.detach()), "q_mean": float(q_mean)}
+        if not sync:
+            return {"loss": loss.detach(), "q_mean": q_mean.detach()}
+        lq = torch.stack([loss.detach().float(), q_mean.detach().float()]).tolist()   # one device-to-host copy
+        return {"loss": lq[0], "q_mean": lq[1]}
 
     def _fused_step_ok(self, x):
         """The explicit fused step (train_step.py) takes the bf16 GPU net with the custom convs and
@@ -244,7 +254,9 @@ class DQNTrainer(DQNLearner):
     def _reward(self, r):
         return torch.log2(1.0 + r) if self.cfg.reward_transform == "log2" else r
 
-    def update(self, batch=None):
+    def update(self, batch=None, sync=True):
+        """One update from a sampled minibatch; sync=False leaves the loss and mean Q as 0-d GPU
+        tensors (learn), so that nothing waits for the GPU."""
         c = self.cfg
         dt = torch.bfloat16 if c.bf16 else torch.float32
         b = self.replay.sample(batch or c.batch)
@@ -257,16 +269,18 @@ class DQNTrainer(DQNLearner):
             self.target.eval()
             qt = self.q_eval(self.target, b["next_state"]).contiguous()
             qo = self.q_eval(self.net, b["next_state"]).contiguous() if c.double else None
-            y = td_target(self._reward(b["reward"]).contiguous(), b["done"], qt, qo, c.gamma)
-        out = self.learn(x, b["action"], y)
+            rw = b["reward"].contiguous()
+            y = td_target(rw, b["done"], qt, qo, c.gamma, log2_reward=True) if c.reward_transform == "log2" \
+                else td_target(self._reward(rw), b["done"], qt, qo, c.gamma)
+        out = self.learn(x, b["action"], y, sync=sync)
         out["batch"] = b
         return out
 
-    def train_step(self):
+    def train_step(self, sync=True):
         reward, done = self.env_step()
         out = {"loss": math.nan}
         if len(self.replay) >= self.cfg.learn_start:
             for _ in range(self.cfg.updates_per_step):
-                out = self.update()
+                out = self.update(sync=sync)
         out["epsilon"] = self.epsilon()
         return out

@@ -54,6 +54,25 @@ def test_td_target_matches_oracle(double):
     np.testing.assert_allclose(y, R.td_target(r, d, qt, qo if double else None, 0.97), rtol=1e-6, atol=1e-6)
 
 
+@pytest.mark.parametrize("double", [False, True])
+def test_td_target_log2_reward_equals_torch_transform(double):
+    """log2_reward folds the trainer's reward transform (torch.log2(1.0 + r), trainer.py _reward) into
+    the TD-target launch: bit-equal to the kernel on the transformed rewards, on merge rewards (0 and
+    sums of tiles up to 2^17) and on arbitrary non-negative floats."""
+    from rein48_amd.dqn.kernels import td_target
+    rng = np.random.default_rng(3)
+    n = 40_003
+    r = np.where(rng.random(n) < 0.5, 0.0, 2.0 ** rng.integers(1, 18, n) * rng.integers(1, 4, n)).astype(np.float32)
+    r[: n // 4] = rng.random(n // 4).astype(np.float32) * 1e3
+    d = (rng.random(n) < 0.2).astype(np.uint8)
+    qt, qo = (rng.normal(size=(n, 4)).astype(np.float32) for _ in range(2))
+    T = lambda a: torch.from_numpy(a).to(DEV)
+    rt = T(r)
+    got = td_target(rt, T(d), T(qt), T(qo) if double else None, 0.97, log2_reward=True)
+    want = td_target(torch.log2(1.0 + rt), T(d), T(qt), T(qo) if double else None, 0.97)
+    assert torch.equal(got, want)
+
+
 def _params(net):
     return {"convs": [(c.weight.detach().double().cpu().numpy(), c.bias.detach().double().cpu().numpy())
                       for c in net.conv_layers()],
@@ -104,7 +123,9 @@ def test_dqn_update_loss_matches_oracle():
         for p in tr.target.parameters():
             p.add_(0.01 * torch.randn_like(p))
     p_on, p_tg = _params(tr.net), _params(tr.target)
-    out = tr.update()
+    out = tr.update(sync=False)                                      # the loss as a 0-d GPU tensor
+    assert torch.is_tensor(out["loss"]) and out["loss"].is_cuda
+    out["loss"] = float(out["loss"])
     b = {k: v.cpu().numpy() for k, v in out["batch"].items()}
     q = R.resnet10_q(p_on, b["state"])[np.arange(len(b["action"])), b["action"].astype(np.int64)]
     y = R.td_target(np.log2(1.0 + b["reward"].astype(np.float64)), b["done"], R.resnet10_q(p_tg, b["next_state"]),
@@ -718,6 +739,40 @@ def test_resnet_train_step_matches_autograd(B):
         ea = float((a - r).norm()) / float(r.norm())
         eb = float((b - r).norm()) / float(r.norm())
         assert eb <= 1.5 * ea + 2e-3, (n, ea, eb)
+
+
+def test_fused_train_step_writes_every_gradient_but_the_conv_biases():
+    """DQNLearner.learn zeroes the flat gradient only before the first of consecutive fused steps:
+    the step must WRITE (not accumulate into) every parameter gradient except the conv biases', which
+    stay exactly zero. Flat gradient filled with NaN, conv-bias slots zeroed, one fused step: no NaN
+    left, biases still zero; a second step without zeroing gives the same gradient bit for bit."""
+    from rein48_amd.a3c.optim import FlatParams
+    from rein48_amd.dqn.conv import board_onehot32
+    from rein48_amd.dqn.nets import ResNet10Q
+    from rein48_amd.dqn.train_step import ResNetTrainStep
+    torch.manual_seed(5)
+    B = 4099
+    net = ResNet10Q(dtype=torch.bfloat16).to(DEV).train()
+    flat = FlatParams(net)
+    rng = np.random.default_rng(5)
+    x = board_onehot32(torch.from_numpy(rng.integers(0, 14, size=(B, 16)).astype(np.int8)).to(DEV)).view(B, 512)
+    action = torch.from_numpy(rng.integers(0, 4, size=B).astype(np.int8)).to(DEV)
+    target = torch.from_numpy(rng.normal(size=B).astype(np.float32)).to(DEV)
+    biases = [c.bias for c in net.conv_layers()]
+    flat.grad.fill_(float("nan"))
+    for bb in biases:
+        bb.grad.zero_()
+    step = ResNetTrainStep(net)
+    stats0 = [(m.running_mean.clone(), m.running_var.clone()) for m in net.bns]
+    step(x, action, target)
+    g1 = flat.grad.clone()
+    assert not bool(torch.isnan(g1).any())
+    assert all(float(bb.grad.abs().max()) == 0.0 for bb in biases)
+    for m, (rm, rv) in zip(net.bns, stats0):
+        m.running_mean.copy_(rm)
+        m.running_var.copy_(rv)
+    step(x, action, target)
+    assert torch.equal(flat.grad, g1)
 
 
 def test_conv_pack_resnet_matches_host_packing():
