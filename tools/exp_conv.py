@@ -51,6 +51,19 @@ def bn_grad(dy_, add_, bnx, mask, add_mask=None):
     return out
 
 
+coef = torch.cat([torch.rand(64, generator=g) + 0.5, torch.randn(64, generator=g) * 0.1]).to(dev)
+
+
+def bn_in(x_, res_):
+    """r48_conv3x3_bn_in: the previous BN + ReLU (+ residual) applied in the operand load."""
+    y_ = torch.empty_like(x_)
+    z_ = torch.empty_like(x_)
+    m_ = torch.empty((B * 16, 8), dtype=torch.uint8, device=dev)
+    C.check(_lib.load().r48_conv3x3_bn_in(C.ptr(x_), B, C.ptr(f64), C.ptr(bias), C.ptr(coef), C.ptr(res_), C.ptr(z_),
+                                          C.ptr(m_), C.ptr(y_), C.ptr(stats), C._stream(x_)))
+    return y_
+
+
 def digest(t):
     v = t.detach().contiguous().view(-1)
     v = v.view(torch.int16).long() if v.dtype == torch.bfloat16 else v.view(torch.int32).long()
@@ -72,6 +85,7 @@ def timed(fn, reps=20):
 # algorithmic HBM bytes: activations in + out (bf16); wgrad reads dy and x
 io = {"fwd64": B * 16 * (64 + 64) * 2, "fwd32": B * 16 * (32 + 64) * 2, "add64": B * 16 * (64 + 64 + 64) * 2,
       "fwd64s": B * 16 * (64 + 64) * 2, "dg64bn": B * 16 * (3 * 64 * 2 + 8), "add64bn": B * 16 * (4 * 64 * 2 + 8), "addm64bn": B * 16 * (4 * 64 * 2 + 16),
+      "in1": B * 16 * (3 * 64 * 2 + 8), "in2": B * 16 * (4 * 64 * 2 + 8),
       "wgrad64": B * 16 * (64 + 64) * 2, "wgrad32": B * 16 * (64 + 32) * 2}
 for path in libs:
     _lib.LIB_PATH, _lib._lib = path, None
@@ -81,6 +95,7 @@ for path in libs:
     runs = {"fwd64": lambda: C.conv3x3(rot(x64s), f64, bias), "fwd32": lambda: C.conv3x3(rot(x32s), f32, bias),
             "add64": lambda: C.conv3x3(rot(x64s), f64, bias, add=rot(dys)),
             "fwd64s": lambda: C.conv3x3(rot(x64s), f64, bias, stats=stats),
+            "in1": lambda: bn_in(rot(x64s), None), "in2": lambda: bn_in(rot(x64s), rot(dys)),
             "dg64bn": lambda: bn_grad(rot(dys), None, rot(x64s), rot(masks)),
             "add64bn": lambda: bn_grad(rot(dys), rot(x64s), rot(x64s), rot(masks)),
             "addm64bn": lambda: bn_grad(rot(dys), rot(x64s), rot(x64s), rot(masks), rot(masks)),

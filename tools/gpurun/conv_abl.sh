@@ -9,4 +9,4 @@ P=rein48_amd/lib/librein48.so
 REV=$(printf '%s\n' "$@" | tac | tr '\n' ' ')
 timeout -k 10 300 python -u tools/exp_conv.py 65536 $P "$@" > $O/exp_conv.txt 2>&1 \
 && timeout -k 10 300 python -u tools/exp_conv.py 65536 $REV $P >> $O/exp_conv.txt 2>&1 && grep -v amdgpu.ids $O/exp_conv.txt \
-&& bash tools/gpurun/dqn_prof.sh $O/prof
+&& { [ -n "$NOPROF" ] || bash tools/gpurun/dqn_prof.sh $O/prof; }
