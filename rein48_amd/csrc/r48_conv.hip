@@ -169,9 +169,9 @@ __global__ __launch_bounds__(64 * kConvWaves, 1) void k_conv3x3(const uint16_t *
     float s1[8] = {}, s2[8] = {};          // statistics of channels 8 (lane & 7) .. + 7
     // xr[R][col][c]: input cell 4 R + col of this lane's board, channels 32 c + 8 g .. + 7
     uint4 xr[4][4][NC];
-    auto load_row = [&](int64_t t, int R) {
+    auto load_row = [&](int64_t t, int R, const uint16_t *base) {
         const int64_t b = t * 16 + n;
-        const uint16_t *src = x + ((b < boards ? b : boards - 1) * 16 + 4 * R) * kCin + 8 * g;
+        const uint16_t *src = base + ((b < boards ? b : boards - 1) * 16 + 4 * R) * kCin + 8 * g;
 #pragma unroll
         for (int col = 0; col < 4; col++)
 #pragma unroll
@@ -221,8 +221,8 @@ __global__ __launch_bounds__(64 * kConvWaves, 1) void k_conv3x3(const uint16_t *
         }
     };
     if (tile < n_tiles) {
-        load_row(tile, 0);
-        load_row(tile, 1);
+        load_row(tile, 0, x);
+        load_row(tile, 1, x);
     }
     for (; tile < n_tiles; tile += stride) {
         const int64_t next = tile + stride;
@@ -230,10 +230,17 @@ __global__ __launch_bounds__(64 * kConvWaves, 1) void k_conv3x3(const uint16_t *
         const bool live = b < boards;
 #pragma unroll
         for (int r = 0; r < 4; r++) {
-            // rows r - 2 of this tile were last read by output row r - 1. Unconditional (the last
-            // tile reloads itself): a load under a branch makes hipcc's counted waits at the join
-            // drain everything in flight
-            load_row(r < 2 ? tile : (next < n_tiles ? next : tile), r < 2 ? r + 2 : r - 2);
+            // rows r - 2 of this tile were last read by output row r - 1. Unconditional: a load under
+            // a branch makes hipcc's counted waits at the join drain everything in flight. After the
+            // wave's last tile the two loads of a next tile read the weight fragments instead (first
+            // 33 KiB, resident in L2 since the workgroup's start; the values are never used): a reload
+            // of the tile itself went back to HBM, 1.25x the input bytes at two tiles per wave
+            // (profiles/r06/dqn/conv_tail_reload.txt)
+            if (r < 2)
+                load_row(tile, r + 2, x);
+            else
+                load_row(next < n_tiles ? next : 0, r - 2,
+                         next < n_tiles ? x : reinterpret_cast<const uint16_t *>(wfrag));
             __builtin_amdgcn_sched_barrier(0);   // issue the row loads here, ahead of this row's MFMAs
             if (IN) {   // rows first used by this output row: 0 and 1 at r = 0, then r + 1
                 if (r == 0)

@@ -20,14 +20,21 @@ import sys
 A = 65536 * 16 * 64 * 2 / 1e6            # MB of one [64K boards, 16 cells, 64 ch] bf16 activation
 M = 65536 * 16 * 8 / 1e6                 # MB of its ReLU-mask bytes
 ALGO = {                                 # algorithmic MB per call: reads + writes
-    "k_conv3x3<2, false, 1>": 2 * A,                      # x in, y out (+ tiny stats records)
-    "k_conv3x3<2, true, 2>": 4 * A + M,                   # dy, add, bn_x in (+ mask), dx out
-    "k_conv3x3<2, false, 2>": 3 * A + M,                  # dy, bn_x in (+ mask), dx out
+    "k_conv3x3<2, 0, 1, 0>": 2 * A,                       # x in, y out (+ tiny stats records)
+    "k_conv3x3<1, 0, 1, 0>": 1.5 * A,                     # the stem: 32-plane x in, y out
+    "k_conv3x3<2, 2, 2, 0>": 4 * A + 2 * M,               # dy, add, bn_x in (+ both masks), dx out
+    "k_conv3x3<2, 1, 2, 0>": 4 * A + M,                   # dy, add, bn_x in (+ mask), dx out
+    "k_conv3x3<2, 0, 2, 0>": 3 * A + M,                   # dy, bn_x in (+ mask), dx out
     "k_conv_wgrad<64>": 2 * A,                            # dy, x in (records out: small)
+    "k_conv_wgrad<32>": 1.5 * A,
     "k_bn_apply<64, true, true, true>": 3 * A + M,        # y, residual in; z, mask out
     "k_bn_apply<64, true, false, true>": 2 * A + M,
     "k_bn_bwd_apply<64, true, true, true>": 4 * A + M,    # dz, mask, y in; dy, dres out
     "k_bn_bwd_apply<64, true, false, true>": 3 * A + M,
+    "k_bn_bwd_reduce<64, true, true>": 2 * A + M,         # dz, mask, y in
+    "k_q_head_fwd": A,
+    "k_q_head_bwd": 2 * A,                                # h in, dh out (records out: small)
+    "k_onehot32": 0.5 * A,
 }
 
 

@@ -3,11 +3,15 @@
 // the conv), a wave per 16-board tile, the tile's 4 input rows in a 4-row register ring refilled one
 // row ahead, a dependent VALU chain per output row standing in for its MFMAs, 1-KiB stores per
 // instruction (the conv's LDS-staged stores), and optionally a second input stream read in the
-// store layout after each row (the SM = 2 epilogue's BN input). Load layouts:
+// store layout after each row (the SM = 2 epilogue's BN input; EPI = 1), or in the residual add's
+// layout (EPI = 2: 8 B per lane per output column and 16-channel pass, the conv's `ad` loads, 16
+// boards x 32 B per instruction). Load layouts:
 //   H  the conv's: lane (board n = l & 15, g = l >> 4) loads 16 B at board n, cell, channels
 //      32 c + 8 g -- every instruction touches 16 half lines (64 B) 2 KiB apart
 //   F  the same bytes re-laid so that one instruction reads 1 KiB contiguous (a tiled layout)
-// Bytes and instruction counts are the same for H and F.
+// Bytes and instruction counts are the same for H and F. With an argument (any) only the chain-0
+// pass runs: the calibration of FETCH_SIZE / WRITE_SIZE for these patterns under rocprofv3 --pmc
+// (every dispatch moves a known 134,217,728 bytes per stream).
 //   hipcc -O3 --offload-arch=gfx950 -o build/probe_conv_io tools/probe_conv_io.hip && build/probe_conv_io
 #include <hip/hip_runtime.h>
 
@@ -26,7 +30,7 @@
 
 constexpr int kWaves = 8;
 
-template <bool FULL, bool EPI>
+template <bool FULL, int EPI>
 __global__ __launch_bounds__(64 * kWaves, 1) void conv_io(const uint4 *__restrict__ x, const uint4 *__restrict__ e,
                                                           uint4 *__restrict__ y, int64_t n_tiles, int chain)
 {
@@ -79,10 +83,18 @@ __global__ __launch_bounds__(64 * kWaves, 1) void conv_io(const uint4 *__restric
                 const int m = 64 * k + lane, bl = m >> 5, q = m & 31;
                 const int64_t o = ((tile * 16 + bl) * 16 + 4 * r) * 8 + q;
                 uint4 w = make_uint4(h, __float_as_uint(acc), (uint32_t)k, (uint32_t)r);
-                if (EPI) {
+                if (EPI == 1) {
                     const uint4 b = e[o];                    // the SM = 2 epilogue's BN-input piece
                     w.x ^= b.x;
                     w.y ^= b.z;
+                }
+                if (EPI == 2) {                              // the residual add's pieces: 8 B per (col, pass)
+                    const uint2 *e2 = reinterpret_cast<const uint2 *>(e);
+                    const int col = k & 3, oh = k >> 2;      // 8 of the row's 16 (col, pass) pieces here ...
+                    const int64_t b = tile * 16 + n;
+                    const int64_t i2 = ((b * 16 + 4 * r + col) * 64 + 16 * oh + 4 * g) / 4;
+                    const uint2 p0 = e2[i2], p1 = e2[i2 + 8];  // ... and the other 8 (passes 2, 3)
+                    w.x ^= p0.x ^ p1.y;
                 }
                 y[o] = w;
             }
@@ -90,7 +102,7 @@ __global__ __launch_bounds__(64 * kWaves, 1) void conv_io(const uint4 *__restric
     }
 }
 
-int main()
+int main(int argc, char **)
 {
     const int64_t boards = 1 << 16, n_tiles = boards / 16;
     const size_t bytes = (size_t)boards * 16 * 128;                      // [boards][16 cells][64 bf16]
@@ -106,19 +118,23 @@ int main()
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
     const int chains[] = {0, 100, 200, 300};
-    for (int chain : chains) {
-        for (int variant = 0; variant < 4; variant++) {
-            const bool full = variant & 1, epi = variant >> 1;
+    const int n_chains = argc > 1 ? 1 : 4;
+    for (int ci = 0; ci < n_chains; ci++) {
+        const int chain = chains[ci];
+        for (int variant = 0; variant < 6; variant++) {
+            const bool full = variant & 1;
+            const int epi = variant >> 1;
             auto launch = [&](int i) {
                 const uint4 *xs = x[i % 3], *es = e[i % 3];
-                if (full && epi)
-                    hipLaunchKernelGGL((conv_io<true, true>), dim3(256), dim3(64 * kWaves), 0, 0, xs, es, y, n_tiles, chain);
-                else if (full)
-                    hipLaunchKernelGGL((conv_io<true, false>), dim3(256), dim3(64 * kWaves), 0, 0, xs, es, y, n_tiles, chain);
-                else if (epi)
-                    hipLaunchKernelGGL((conv_io<false, true>), dim3(256), dim3(64 * kWaves), 0, 0, xs, es, y, n_tiles, chain);
-                else
-                    hipLaunchKernelGGL((conv_io<false, false>), dim3(256), dim3(64 * kWaves), 0, 0, xs, es, y, n_tiles, chain);
+                const dim3 gr(256), bl(64 * kWaves);
+                switch (variant) {
+                case 0: hipLaunchKernelGGL((conv_io<false, 0>), gr, bl, 0, 0, xs, es, y, n_tiles, chain); break;
+                case 1: hipLaunchKernelGGL((conv_io<true, 0>), gr, bl, 0, 0, xs, es, y, n_tiles, chain); break;
+                case 2: hipLaunchKernelGGL((conv_io<false, 1>), gr, bl, 0, 0, xs, es, y, n_tiles, chain); break;
+                case 3: hipLaunchKernelGGL((conv_io<true, 1>), gr, bl, 0, 0, xs, es, y, n_tiles, chain); break;
+                case 4: hipLaunchKernelGGL((conv_io<false, 2>), gr, bl, 0, 0, xs, es, y, n_tiles, chain); break;
+                default: hipLaunchKernelGGL((conv_io<true, 2>), gr, bl, 0, 0, xs, es, y, n_tiles, chain);
+                }
             };
             for (int i = 0; i < 5; i++)
                 launch(i);
@@ -132,9 +148,10 @@ int main()
             float ms = 0;
             CK(hipEventElapsedTime(&ms, a, b));
             const double us = 1e3 * ms / reps;
-            const double moved = (double)bytes * (2 + epi);
+            const double moved = (double)bytes * (2 + (epi ? 1 : 0));
             printf("chain %3d  loads %s  %s  %7.1f us  %5.2f TB/s\n", chain, full ? "F (1 KiB/instr)" : "H (conv half lines)",
-                   epi ? "+ epilogue stream" : "                 ", us, moved / us / 1e6);
+                   epi == 1 ? "+ epilogue stream (1 KiB)" : epi == 2 ? "+ add stream (8 B/lane) " : "                         ",
+                   us, moved / us / 1e6);
         }
     }
     return 0;
