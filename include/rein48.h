@@ -405,6 +405,29 @@ int r48_adam(float *param, const float *grad, float *m, float *v, int64_t n, flo
  * Channels-last bf16 activations [boards][16 cells][C], 64 output channels, 32 or 64 input
  * channels; only the 100 in-grid (cell, tap) pairs are computed. Replace the structured dense
  * GEMMs of nets.py:ResNet10Q._conv (hipBLASLt) in the update. */
+/* The finish of the training-mode BN that a conv's output feeds (forward: r48_conv3x3_stats_finish,
+ * r48_conv3x3_bn_in) or whose backward reduction a data-gradient conv sums (r48_conv3x3_bn_grad),
+ * done in the conv itself by the workgroup that writes the last statistics record, so that no
+ * finish launch sits between the conv and the BN's apply pass. Forward: save = float[2C] {mean,
+ * invstd} of the conv's output over `rows`, coef = float[2C] {a = gamma invstd, b = beta - mean a},
+ * running_mean / running_var (nullable together) updated with momentum and the unbiased variance;
+ * beta, gamma as the BN's. Backward: save is read (the forward's), coef = float[3C] {a, cc, d} of
+ * dx = a g + cc x + d, dgamma / dbeta (nullable) = invstd sum g (x - mean), sum g. The statistics
+ * buffer's last float is the arrival counter: it must be 0 before the first such call (the finishing
+ * workgroup resets it). C = 64 (the update's convs). */
+typedef struct r48_bn_finish_args {
+    const float *gamma;
+    const float *beta;
+    float *running_mean;
+    float *running_var;
+    float *save;
+    float *coef;
+    float *dgamma;
+    float *dbeta;
+    int64_t rows;
+    float momentum;
+    float eps;
+} r48_bn_finish_args;
 /* One-hot input planes for the training stem: out bf16 [n][16][32] (plane e = exponent 0..17,
  * planes 18..31 zero), 16-byte aligned. */
 int r48_board_onehot32(const int8_t *boards, int64_t n, void *out, void *stream);
@@ -414,8 +437,13 @@ int r48_board_onehot32(const int8_t *boards, int64_t n, void *out, void *stream)
  * [64] or NULL; add bf16 [boards][16][64] or NULL (cin 64 only: a basic block's input gradient
  * summed in the epilogue). stats (NULL, or float[r48_conv_stats_floats()]; not with add): the
  * per-channel sum and sum of squares of the bf16 outputs, one record [S1 64][S2 64] per CU, for
- * r48_bn_forward_stats. All pointers 16-byte aligned. */
+ * r48_bn_forward_stats. All pointers 16-byte aligned. The statistics buffer's last float is the
+ * arrival counter of the finishing forms (r48_bn_finish_args). */
 int64_t r48_conv_stats_floats(void);
+/* r48_conv3x3 with stats (no add) and the finish of the BN that its output feeds (fin, required):
+ * the BN's apply pass follows as r48_bn_apply. */
+int r48_conv3x3_stats_finish(const void *x, int64_t boards, int32_t cin, const void *wfrag, const float *bias, void *y,
+                             float *stats, const r48_bn_finish_args *fin, void *stream);
 /* The update's forward conv with the PREVIOUS layer's training-mode BN + ReLU folded into its operand
  * load (rein48_amd/dqn/train_step.py): x bf16 [boards][16][64] is that BN's input (the previous conv's
  * output); coef float[128] = (a[64], b[64]) from r48_bn_finish; residual (nullable) the block's identity
@@ -424,17 +452,20 @@ int64_t r48_conv_stats_floats(void);
  * channels, bit k = z > 0) into mask_out; y and stats as r48_conv3x3 with stats (required). Replaces
  * nets.py's BatchNorm + ReLU (+ identity) followed by the next conv (README.md:15-17). */
 int r48_conv3x3_bn_in(const void *x, int64_t boards, const void *wfrag, const float *bias, const float *coef,
-                      const void *residual, void *z_out, uint8_t *mask_out, void *y, float *stats, void *stream);
+                      const void *residual, void *z_out, uint8_t *mask_out, void *y, float *stats,
+                      const r48_bn_finish_args *fin, void *stream);
 /* A data-gradient conv (64 -> 64 channels, wfrag from pack_conv_dgrad; + add as r48_conv3x3) whose
  * output dx is the gradient reaching a training-mode BN + ReLU, with that BN's backward reduction
  * fused in the epilogue: bn_part (float[r48_conv_stats_floats()]) gets per-CU records [sum g 64]
  * [sum g (bn_x - mean) 64], g = dx . bn_mask, bn_x the BN's input, mean = bn_save[0..63] -- the
  * input of r48_bn_backward_part. add_mask (NULL, or with add: [boards][16][8] bytes, bit k of byte
  * j = channel 8 j + k): the added term is add . [mask bit] -- a basic block's identity-path
- * gradient formed from the gradient at the block's output ReLU and that ReLU's forward mask. */
+ * gradient formed from the gradient at the block's output ReLU and that ReLU's forward mask. fin
+ * (nullable; bn_save == fin->save): that BN's backward finish in the conv, the apply pass following
+ * as r48_bn_backward_apply. r48_conv3x3_bn_in's fin (nullable) finishes the BN of ITS output. */
 int r48_conv3x3_bn_grad(const void *dy, int64_t boards, const void *wfrag, const void *add, const uint8_t *add_mask,
                         void *dx, const void *bn_x, const uint8_t *bn_mask, const float *bn_save, float *bn_part,
-                        void *stream);
+                        const r48_bn_finish_args *fin, void *stream);
 int r48_conv3x3(const void *x, int64_t boards, int32_t cin, const void *wfrag, const float *bias, const void *add,
                 void *y, float *stats, void *stream);
 /* dw fp32 [64][cin][3][3] = sum over boards and in-grid cells of dy[b][p][co] x[b][p + off(t)][ci];
@@ -524,6 +555,13 @@ int r48_bn_backward_part(const float *part, int32_t nblk, const void *dy, const 
 int r48_bn_backward(const void *dy, const void *y, const uint8_t *mask, const void *x, int64_t rows, int32_t C,
                     const float *gamma, const float *save, int32_t relu, float *workspace, void *dx, void *dresidual,
                     float *dgamma, float *dbeta, void *stream);
+/* The apply passes alone, from coefficients a finishing conv wrote (r48_bn_finish_args coef):
+ * forward y = relu?(a x + b (+ residual)) (+ mask as r48_bn_forward), coef float[2C]; backward
+ * dx = a g + cc x + d with g = dy . mask, coef float[3C]. */
+int r48_bn_apply(const void *x, const void *residual, int64_t rows, int32_t C, const float *coef, int32_t relu, void *y,
+                 uint8_t *mask, void *stream);
+int r48_bn_backward_apply(const void *dy, const uint8_t *mask, const void *x, int64_t rows, int32_t C, const float *coef,
+                          void *dx, void *stream);
 
 /* Thread-local message of the last failed call on this thread ("" if none). */
 const char *r48_last_error(void);

@@ -26,6 +26,15 @@ DRAW_CONTRACT = 3          # R48_DRAW_CONTRACT (include/rein48.h); test_abi chec
 
 # name -> (restype, argtypes); mirrors include/rein48.h one to one
 _P, _I32, _I64, _U32, _U64 = C.c_void_p, C.c_int32, C.c_int64, C.c_uint32, C.c_uint64
+
+
+class BnFinishArgs(C.Structure):
+    """r48_bn_finish_args (include/rein48.h): the BN finish a conv does in its last workgroup."""
+    _fields_ = [("gamma", _P), ("beta", _P), ("running_mean", _P), ("running_var", _P), ("save", _P), ("coef", _P),
+                ("dgamma", _P), ("dbeta", _P), ("rows", _I64), ("momentum", C.c_float), ("eps", C.c_float)]
+
+
+_FIN = C.POINTER(BnFinishArgs)
 SIGNATURES = {
     "r48_cnn_train_grad": (C.c_int, [_P, _I64, _I64, _P, _P, _P, _P, _P, C.c_float, _I32, _P, _P, _P, _P, _P]),
     "r48_cnn_train_grad_seg": (C.c_int, [_P, _I64, _I64, _P, _P, _P, _P, C.c_float, _I32, _P, _P, _P, _P, _P]),
@@ -42,7 +51,10 @@ SIGNATURES = {
     "r48_bn_forward_stats": (C.c_int, [_P, _I32, _P, _P, _I64, _I32, _P, _P, _P, _P, C.c_float, C.c_float, _I32, _P,
                                        _P, _P, _P, _P]),
     "r48_bn_backward_part": (C.c_int, [_P, _I32, _P, _P, _P, _I64, _I32, _P, _P, _P, _P, _P, _P, _P, _P]),
-    "r48_conv3x3_bn_grad": (C.c_int, [_P, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "r48_conv3x3_bn_grad": (C.c_int, [_P, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _FIN, _P]),
+    "r48_conv3x3_stats_finish": (C.c_int, [_P, _I64, _I32, _P, _P, _P, _P, _FIN, _P]),
+    "r48_bn_apply": (C.c_int, [_P, _P, _I64, _I32, _P, _I32, _P, _P, _P]),
+    "r48_bn_backward_apply": (C.c_int, [_P, _P, _P, _I64, _I32, _P, _P, _P]),
     "r48_bn_backward": (C.c_int, [_P, _P, _P, _P, _I64, _I32, _P, _P, _I32, _P, _P, _P, _P, _P, _P]),
     "r48_board_onehot": (C.c_int, [_P, _I64, _I32, _P, _P]),
     "r48_board_onehot32": (C.c_int, [_P, _I64, _P, _P]),
@@ -114,7 +126,7 @@ SIGNATURES = {
     "r48_mlp_train_workspace_floats": (_I64, [_I64]),
     "r48_mlp_train_grad": (C.c_int, [_P, _I64, _I64, _P, _P, _P, _P, _P, C.c_float, _I32, _P, _P, _P, _P]),
     "r48_mlp_train_grad_seg": (C.c_int, [_P, _I64, _I64, _P, _P, _P, _P, C.c_float, _I32, _P, _P, _P, _P]),
-    "r48_conv3x3_bn_in": (C.c_int, [_P, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "r48_conv3x3_bn_in": (C.c_int, [_P, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _FIN, _P]),
     "r48_bn_finish": (C.c_int, [_P, _I32, _I64, _I32, _P, _P, _P, _P, C.c_float, C.c_float, _P, _P, _P]),
     "r48_last_error": (C.c_char_p, []),
     "r48_version": (C.c_char_p, []),

@@ -24,6 +24,7 @@
 #include <string>
 
 #include "../../include/rein48.h"
+#include "r48_bn_finish.h"
 
 namespace r48 {
 void set_last_error(const std::string &msg);
@@ -211,22 +212,8 @@ __global__ __launch_bounds__(kBlock) void k_bn_finish(const uint16_t *__restrict
     if (threadIdx.x != 0)
         return;
     const double x0 = x ? (double)__uint_as_float((uint32_t)x[c] << 16) : 0.0;   // shift (NULL: unshifted sums)
-    const double n = (double)rows;
-    const double dm = s1 / n;
-    double var = s2 / n - dm * dm;                 // biased (normalisation), as BN training mode
-    var = var > 0.0 ? var : 0.0;
-    const double mean = x0 + dm;
-    const double invstd = 1.0 / sqrt(var + (double)eps);
-    save[c] = (float)mean;
-    save[C + c] = (float)invstd;
-    const double a = (double)gamma[c] * invstd;
-    coef[c] = (float)a;
-    coef[C + c] = (float)((double)beta[c] - mean * a);
-    if (running_mean) {
-        const double unb = rows > 1 ? var * n / (n - 1.0) : var;
-        running_mean[c] = (float)((1.0 - momentum) * (double)running_mean[c] + momentum * mean);
-        running_var[c] = (float)((1.0 - momentum) * (double)running_var[c] + momentum * unb);
-    }
+    const r48_bn_finish_args f{gamma, beta, running_mean, running_var, save, coef, nullptr, nullptr, rows, momentum, eps};
+    r48bn::fwd_channel(f, C, c, s1, s2, x0);
 }
 
 // mask (optional, MASK): one byte per thread and row, bit k = (y[row][8 cg + k] > 0) -- the ReLU
@@ -375,17 +362,9 @@ __global__ __launch_bounds__(kBlock) void k_bn_bwd_finish(const float *__restric
     channel_totals(part, nblk, C, c, sg, sgx);
     if (threadIdx.x != 0)
         return;
-    const double mean = save[c], invstd = save[C + c], n = (double)rows;
-    const double dg = sgx * invstd;
-    if (dgamma)
-        dgamma[c] = (float)dg;
-    if (dbeta)
-        dbeta[c] = (float)sg;
-    const double a = (double)gamma[c] * invstd;
-    const double cc = -a * invstd * dg / n;
-    coef[c] = (float)a;
-    coef[C + c] = (float)cc;
-    coef[2 * C + c] = (float)(-a * sg / n - cc * mean);
+    const r48_bn_finish_args f{gamma, nullptr, nullptr, nullptr, const_cast<float *>(save), coef, dgamma, dbeta, rows,
+                               0.f, 0.f};
+    r48bn::bwd_channel(f, C, c, sg, sgx);
 }
 
 template <int C, bool RELU, bool DRES, bool MASK>
@@ -482,6 +461,22 @@ int forward_c(const uint16_t *x, const uint16_t *res, int64_t rows, const float 
 }
 
 // finish + apply from per-block sums a producer computed (r48_conv3x3 `stats`: unshifted)
+template <int C>
+int apply_c(const uint16_t *x, const uint16_t *res, int64_t rows, const float *coef, int relu, uint16_t *y, uint8_t *mask,
+            hipStream_t s)
+{
+    const dim3 g(apply_blocks(rows, C));
+    if (relu && res)
+        launch_apply<C, true, true>(g, s, x, res, rows, coef, y, mask);
+    else if (relu)
+        launch_apply<C, true, false>(g, s, x, res, rows, coef, y, mask);
+    else if (res)
+        launch_apply<C, false, true>(g, s, x, res, rows, coef, y, mask);
+    else
+        launch_apply<C, false, false>(g, s, x, res, rows, coef, y, mask);
+    return launched("k_bn_apply");
+}
+
 template <int C>
 int forward_stats_c(const float *part, int nblk, const uint16_t *x, const uint16_t *res, int64_t rows,
                     const float *gamma, const float *beta, float *rm, float *rv, float momentum, float eps, int relu,
@@ -655,6 +650,54 @@ int r48_bn_backward_part(const float *part, int32_t nblk, const void *dy, const 
         return backward_part_c<128>(part, nblk, d, mask, xs, rows, gamma, save, coef, (uint16_t *)dx,
                                     (uint16_t *)dresidual, dgamma, dbeta, s);
     }
+}
+
+int r48_bn_apply(const void *x, const void *residual, int64_t rows, int32_t C, const float *coef, int32_t relu, void *y,
+                 uint8_t *mask, void *stream)
+{
+    int rc = check_args(x, rows, C);
+    if (rc)
+        return rc;
+    if (!coef || !y || !aligned16(y) || (residual && !aligned16(residual)))
+        return fail(R48_EINVAL, "r48_bn_apply: null or misaligned argument");
+    const uint16_t *xs = (const uint16_t *)x, *rs = (const uint16_t *)residual;
+    uint16_t *ys = (uint16_t *)y;
+    hipStream_t s = (hipStream_t)stream;
+    switch (C) {
+    case 32:
+        return apply_c<32>(xs, rs, rows, coef, relu, ys, mask, s);
+    case 64:
+        return apply_c<64>(xs, rs, rows, coef, relu, ys, mask, s);
+    default:
+        return apply_c<128>(xs, rs, rows, coef, relu, ys, mask, s);
+    }
+}
+
+int r48_bn_backward_apply(const void *dy, const uint8_t *mask, const void *x, int64_t rows, int32_t C, const float *coef,
+                          void *dx, void *stream)
+{
+    int rc = check_args(x, rows, C);
+    if (rc)
+        return rc;
+    if (!dy || !aligned16(dy) || !mask || !coef || !dx || !aligned16(dx))
+        return fail(R48_EINVAL, "r48_bn_backward_apply: null or misaligned argument");
+    const uint16_t *d = (const uint16_t *)dy, *xs = (const uint16_t *)x, *y = nullptr;
+    uint16_t *o = (uint16_t *)dx;
+    hipStream_t s = (hipStream_t)stream;
+    switch (C) {
+    case 32:
+        hipLaunchKernelGGL((k_bn_bwd_apply<32, true, false, true>), dim3(apply_blocks(rows, 32)), dim3(kBlock), 0, s, d,
+                           y, mask, xs, rows, coef, o, nullptr);
+        break;
+    case 64:
+        hipLaunchKernelGGL((k_bn_bwd_apply<64, true, false, true>), dim3(apply_blocks(rows, 64)), dim3(kBlock), 0, s, d,
+                           y, mask, xs, rows, coef, o, nullptr);
+        break;
+    default:
+        hipLaunchKernelGGL((k_bn_bwd_apply<128, true, false, true>), dim3(apply_blocks(rows, 128)), dim3(kBlock), 0, s,
+                           d, y, mask, xs, rows, coef, o, nullptr);
+    }
+    return launched("k_bn_bwd_apply");
 }
 
 int r48_bn_backward(const void *dy, const void *y, const uint8_t *mask, const void *x, int64_t rows, int32_t C,

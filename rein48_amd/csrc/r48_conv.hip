@@ -29,6 +29,7 @@
 #include <string>
 
 #include "../../include/rein48.h"
+#include "r48_bn_finish.h"
 
 namespace r48 {
 void set_last_error(const std::string &msg);
@@ -137,7 +138,8 @@ __global__ __launch_bounds__(64 * kConvWaves, 1) void k_conv3x3(const uint16_t *
                                                                const uint16_t *__restrict__ res = nullptr,
                                                                uint16_t *__restrict__ z_out = nullptr,
                                                                uint8_t *__restrict__ m_out = nullptr,
-                                                               const uint8_t *__restrict__ add_mask = nullptr)
+                                                               const uint8_t *__restrict__ add_mask = nullptr,
+                                                               const r48_bn_finish_args fin = r48_bn_finish_args{})
 {
     constexpr bool STATS = SM != 0;
     constexpr int PO = STATS ? 1 : 2;
@@ -379,7 +381,27 @@ __global__ __launch_bounds__(64 * kConvWaves, 1) void k_conv3x3(const uint16_t *
 #pragma unroll
             for (int w = 0; w < kConvWaves; w++)
                 t += st_lds[w][c >> 3][8 * v + (c & 7)];
-            stats[(int64_t)blockIdx.x * 2 * kCout + threadIdx.x] = t;
+            // device-coherent stores (agent scope: no L2 write-back fence needed before the ticket)
+            __hip_atomic_store(stats + (int64_t)blockIdx.x * 2 * kCout + threadIdx.x, t, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (fin.save) {
+            // the BN's finish in the workgroup whose record arrives last (r48_bn_finish_args): every
+            // record store is acknowledged at the device's coherence point before this workgroup
+            // takes a ticket, and the last one reads every record with device-coherent loads
+            __shared__ unsigned int ticket;
+            __shared__ double fin_lds[8 * kCout];
+            unsigned int *counter = reinterpret_cast<unsigned int *>(stats + (int64_t)kPersistentGroups * 2 * kCout);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (threadIdx.x == 0)
+                ticket = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __syncthreads();
+            if (ticket == kPersistentGroups - 1) {
+                r48bn::finish_records<kCout, kPersistentGroups, SM == 2>(stats, fin, fin_lds);
+                if (threadIdx.x == 0)   // ready for the next launch on this buffer
+                    __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
     }
 }
@@ -932,7 +954,32 @@ int r48_board_onehot32(const int8_t *boards, int64_t n, void *out, void *stream)
     return launched("k_onehot32");
 }
 
-int64_t r48_conv_stats_floats(void) { return (int64_t)cu_count() * 2 * kCout; }
+// the records, then one float holding the finishing forms' arrival counter (+ 3 to keep 16 B)
+int64_t r48_conv_stats_floats(void) { return (int64_t)cu_count() * 2 * kCout + 4; }
+
+int r48_conv3x3_stats_finish(const void *x, int64_t boards, int32_t cin, const void *wfrag, const float *bias, void *y,
+                             float *stats, const r48_bn_finish_args *fin, void *stream)
+{
+    if (!x || !wfrag || !y || !stats || !fin || !fin->gamma || !fin->beta || !fin->save || !fin->coef || boards < 1 ||
+        (cin != 32 && cin != 64) || fin->rows < 1)
+        return fail(R48_EINVAL, "r48_conv3x3_stats_finish: NULL argument, boards < 1, rows < 1 or cin not 32/64");
+    if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(wfrag) | reinterpret_cast<uintptr_t>(y) |
+         reinterpret_cast<uintptr_t>(bias)) & 15u)
+        return fail(R48_EINVAL, "r48_conv3x3_stats_finish: x, wfrag, bias and y must be 16-byte aligned");
+    if ((fin->running_mean == nullptr) != (fin->running_var == nullptr))
+        return fail(R48_EINVAL, "r48_conv3x3_stats_finish: running_mean and running_var go together");
+    const dim3 g(cu_count()), blk(64 * kConvWaves);
+    hipStream_t s = (hipStream_t)stream;
+    const uint16_t *xs = (const uint16_t *)x;
+    const uint4 *wf = (const uint4 *)wfrag;
+    if (cin == 64)
+        hipLaunchKernelGGL((k_conv3x3<2, 0, 1>), g, blk, 0, s, xs, boards, wf, bias, nullptr, (uint16_t *)y, stats,
+                           nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, *fin);
+    else
+        hipLaunchKernelGGL((k_conv3x3<1, 0, 1>), g, blk, 0, s, xs, boards, wf, bias, nullptr, (uint16_t *)y, stats,
+                           nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, *fin);
+    return launched("k_conv3x3 (stats + BN finish)");
+}
 
 int r48_conv3x3(const void *x, int64_t boards, int32_t cin, const void *wfrag, const float *bias, const void *add,
                 void *y, float *stats, void *stream)
@@ -969,8 +1016,13 @@ int r48_conv3x3(const void *x, int64_t boards, int32_t cin, const void *wfrag, c
 }
 
 int r48_conv3x3_bn_in(const void *x, int64_t boards, const void *wfrag, const float *bias, const float *coef,
-                      const void *residual, void *z_out, uint8_t *mask_out, void *y, float *stats, void *stream)
+                      const void *residual, void *z_out, uint8_t *mask_out, void *y, float *stats,
+                      const r48_bn_finish_args *fin, void *stream)
 {
+    if (fin && (!fin->gamma || !fin->beta || !fin->save || !fin->coef || fin->rows < 1 ||
+                (fin->running_mean == nullptr) != (fin->running_var == nullptr)))
+        return fail(R48_EINVAL, "r48_conv3x3_bn_in: incomplete BN finish arguments");
+    const r48_bn_finish_args f = fin ? *fin : r48_bn_finish_args{};
     if (!x || !wfrag || !coef || !z_out || !mask_out || !y || !stats || boards < 1)
         return fail(R48_EINVAL, "r48_conv3x3_bn_in: NULL argument or boards < 1");
     if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(wfrag) | reinterpret_cast<uintptr_t>(y) |
@@ -983,17 +1035,20 @@ int r48_conv3x3_bn_in(const void *x, int64_t boards, const void *wfrag, const fl
     const uint4 *wf = (const uint4 *)wfrag;
     if (residual)
         hipLaunchKernelGGL((k_conv3x3<2, 0, 1, 2>), g, blk, 0, s, xs, boards, wf, bias, nullptr, (uint16_t *)y, stats,
-                           nullptr, nullptr, nullptr, coef, rs, (uint16_t *)z_out, mask_out);
+                           nullptr, nullptr, nullptr, coef, rs, (uint16_t *)z_out, mask_out, nullptr, f);
     else
         hipLaunchKernelGGL((k_conv3x3<2, 0, 1, 1>), g, blk, 0, s, xs, boards, wf, bias, nullptr, (uint16_t *)y, stats,
-                           nullptr, nullptr, nullptr, coef, rs, (uint16_t *)z_out, mask_out);
+                           nullptr, nullptr, nullptr, coef, rs, (uint16_t *)z_out, mask_out, nullptr, f);
     return launched("k_conv3x3 (bn in)");
 }
 
 int r48_conv3x3_bn_grad(const void *dy, int64_t boards, const void *wfrag, const void *add, const uint8_t *add_mask,
                         void *dx, const void *bn_x, const uint8_t *bn_mask, const float *bn_save, float *bn_part,
-                        void *stream)
+                        const r48_bn_finish_args *fin, void *stream)
 {
+    if (fin && (!fin->gamma || !fin->coef || fin->save != bn_save || fin->rows < 1))
+        return fail(R48_EINVAL, "r48_conv3x3_bn_grad: incomplete BN finish arguments (fin->save must be bn_save)");
+    const r48_bn_finish_args f = fin ? *fin : r48_bn_finish_args{};
     if (add_mask && !add)
         return fail(R48_EINVAL, "r48_conv3x3_bn_grad: add_mask without add");
     if (!dy || !wfrag || !dx || !bn_x || !bn_mask || !bn_save || !bn_part || boards < 1)
@@ -1008,13 +1063,13 @@ int r48_conv3x3_bn_grad(const void *dy, int64_t boards, const void *wfrag, const
     const uint4 *wf = (const uint4 *)wfrag;
     if (add_mask)
         hipLaunchKernelGGL((k_conv3x3<2, 2, 2>), g, blk, 0, s, xs, boards, wf, nullptr, a, (uint16_t *)dx, bn_part,
-                           bx, bn_mask, bn_save, nullptr, nullptr, nullptr, nullptr, add_mask);
+                           bx, bn_mask, bn_save, nullptr, nullptr, nullptr, nullptr, add_mask, f);
     else if (add)
         hipLaunchKernelGGL((k_conv3x3<2, 1, 2>), g, blk, 0, s, xs, boards, wf, nullptr, a, (uint16_t *)dx, bn_part,
-                           bx, bn_mask, bn_save);
+                           bx, bn_mask, bn_save, nullptr, nullptr, nullptr, nullptr, nullptr, f);
     else
         hipLaunchKernelGGL((k_conv3x3<2, 0, 2>), g, blk, 0, s, xs, boards, wf, nullptr, a, (uint16_t *)dx,
-                           bn_part, bx, bn_mask, bn_save);
+                           bn_part, bx, bn_mask, bn_save, nullptr, nullptr, nullptr, nullptr, nullptr, f);
     return launched("k_conv3x3 (bn grad)");
 }
 

@@ -485,7 +485,7 @@ def test_conv3x3_stats_match_fp64_sums(ci, B):
     st = torch.empty(int(_lib.load().r48_conv_stats_floats()), dtype=torch.float32, device=DEV)
     y = conv3x3(x.contiguous(), pack_conv(w, x.shape[2]), bias, stats=st)
     assert torch.equal(y, conv3x3(x.contiguous(), pack_conv(w, x.shape[2]), bias))
-    rec = st.view(-1, 2, 64).double().sum(0)
+    rec = st[:-4].view(-1, 2, 64).double().sum(0)   # (the last 4 floats: the arrival counter)
     yd = y.reshape(-1, 64).double()
     for got, want in ((rec[0], yd.sum(0)), (rec[1], (yd * yd).sum(0))):
         assert float((got - want).abs().max()) <= 1e-5 * float(want.abs().max())
@@ -514,7 +514,7 @@ def test_conv3x3_bn_grad_reduction_matches_fp64(B, with_add):
     part = torch.full((int(L.r48_conv_stats_floats()),), float("nan"), dtype=torch.float32, device=DEV)
     out = torch.empty_like(dy)
     _lib.check(L.r48_conv3x3_bn_grad(_lib.ptr(dy), B, _lib.ptr(frags), _lib.ptr(add), _lib.ptr(add_mask), _lib.ptr(out),
-                                     _lib.ptr(bn_x), _lib.ptr(mask), _lib.ptr(save), _lib.ptr(part),
+                                     _lib.ptr(bn_x), _lib.ptr(mask), _lib.ptr(save), _lib.ptr(part), None,
                                      ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
     if add_mask is not None:
         abits = ((add_mask.long().unsqueeze(-1) >> torch.arange(8, device=DEV)) & 1).reshape(B, 16, 64).bool()
@@ -523,11 +523,122 @@ def test_conv3x3_bn_grad_reduction_matches_fp64(B, with_add):
     bits = ((mask.long().unsqueeze(-1) >> torch.arange(8, device=DEV)) & 1).reshape(B * 16, 64).bool()
     gd = torch.where(bits, out.reshape(-1, 64).double(), torch.zeros((), dtype=torch.float64, device=DEV))
     xd = bn_x.reshape(-1, 64).double() - save[:64].double()
-    rec = part.view(-1, 2, 64).double().sum(0)
+    rec = part[:-4].view(-1, 2, 64).double().sum(0)
     for got, terms in ((rec[0], gd), (rec[1], gd * xd)):
         err = (got - terms.sum(0)).abs()
         assert bool((err <= 1e-5 * terms.abs().sum(0) + 1e-30).all()), float(err.max())
 
+
+
+def _fin_args(L, gamma, beta, rm, rv, save, coef, dgamma, dbeta, rows, mom, eps):
+    from rein48_amd import _lib
+    p = lambda t: None if t is None else t.data_ptr()   # noqa: E731
+    return _lib.BnFinishArgs(p(gamma), p(beta), p(rm), p(rv), p(save), p(coef), p(dgamma), p(dbeta), rows, mom, eps)
+
+
+@pytest.mark.parametrize("B,cin", [(4099, 64), (1 << 16, 64), (1037, 32)])
+def test_conv_stats_finish_equals_conv_then_bn_finish(B, cin):
+    """r48_conv3x3_stats_finish (the BN finish in the workgroup whose statistics record arrives last,
+    r48_bn_finish_args) against r48_conv3x3 with stats + the standalone r48_bn_finish: the same conv
+    output bit for bit; save (mean, invstd), coef and the running statistics equal to fp32 rounding of
+    the same fp64 sums taken in another order (rel 1e-6); twice in a row (the arrival counter is reset)
+    with bit-identical results; then r48_bn_apply from that coef == r48_bn_forward_stats' output."""
+    import ctypes
+    from rein48_amd import _lib
+    from rein48_amd.dqn.conv import pack_conv
+    g = torch.Generator(device="cpu").manual_seed(B + cin)
+    L = _lib.load()
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    w = (torch.randn(64, cin, 3, 3, generator=g) * 0.1).to(DEV)
+    frags, bias = pack_conv(w, cin), (torch.randn(64, generator=g) * 0.3).to(DEV)
+    x = torch.randn(B, 16, cin, generator=g).to(DEV).to(torch.bfloat16)
+    gamma, beta = (torch.rand(64, generator=g) + 0.5).to(DEV), (torch.randn(64, generator=g) * 0.2).to(DEV)
+    rm0, rv0 = (torch.randn(64, generator=g) * 0.1).to(DEV), (torch.rand(64, generator=g) + 0.5).to(DEV)
+    n = int(L.r48_conv_stats_floats())
+    # reference: conv with statistics records, then the standalone finish
+    st = torch.zeros(n, dtype=torch.float32, device=DEV)
+    y_ref = torch.empty(B, 16, 64, dtype=torch.bfloat16, device=DEV)
+    _lib.check(L.r48_conv3x3(_lib.ptr(x), B, cin, _lib.ptr(frags), _lib.ptr(bias), None, _lib.ptr(y_ref), _lib.ptr(st), s))
+    save_r, coef_r = torch.empty(128, device=DEV), torch.empty(128, device=DEV)
+    rm_r, rv_r = rm0.clone(), rv0.clone()
+    _lib.check(L.r48_bn_finish(_lib.ptr(st), 256, B * 16, 64, _lib.ptr(gamma), _lib.ptr(beta), _lib.ptr(rm_r),
+                               _lib.ptr(rv_r), 0.1, 1e-5, _lib.ptr(save_r), _lib.ptr(coef_r), s))
+    outs = []
+    st2 = torch.zeros(n, dtype=torch.float32, device=DEV)
+    for _ in range(2):
+        y = torch.empty_like(y_ref)
+        save, coef = torch.empty(128, device=DEV), torch.empty(128, device=DEV)
+        rm, rv = rm0.clone(), rv0.clone()
+        fin = _fin_args(L, gamma, beta, rm, rv, save, coef, None, None, B * 16, 0.1, 1e-5)
+        _lib.check(L.r48_conv3x3_stats_finish(_lib.ptr(x), B, cin, _lib.ptr(frags), _lib.ptr(bias), _lib.ptr(y),
+                                              _lib.ptr(st2), ctypes.byref(fin), s))
+        torch.cuda.synchronize()
+        assert int(st2[-4:].view(torch.int32)[0]) == 0          # the arrival counter is back to 0
+        outs.append((y, save, coef, rm, rv))
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)
+    y, save, coef, rm, rv = outs[0]
+    assert torch.equal(y, y_ref)
+    for got, want in ((save, save_r), (coef, coef_r), (rm, rm_r), (rv, rv_r)):
+        torch.testing.assert_close(got, want, rtol=1e-6, atol=1e-7)
+    z, m = torch.empty_like(y), torch.empty(B * 16, 8, dtype=torch.uint8, device=DEV)
+    _lib.check(L.r48_bn_apply(_lib.ptr(y), None, B * 16, 64, _lib.ptr(coef_r), 1, _lib.ptr(z), _lib.ptr(m), s))
+    z_r, m_r = torch.empty_like(y), torch.empty_like(m)
+    ws = torch.empty(int(L.r48_bn_workspace_floats(B * 16, 64)), device=DEV)
+    _lib.check(L.r48_bn_forward_stats(_lib.ptr(st), 256, _lib.ptr(y), None, B * 16, 64, _lib.ptr(gamma), _lib.ptr(beta),
+                                      None, None, 0.1, 1e-5, 1, _lib.ptr(torch.empty(128, device=DEV)), _lib.ptr(ws),
+                                      _lib.ptr(z_r), _lib.ptr(m_r), s))
+    assert torch.equal(z, z_r) and torch.equal(m, m_r)
+
+
+@pytest.mark.parametrize("B,with_add", [(4099, "mask"), (1 << 16, False)])
+def test_conv_bn_grad_finish_equals_backward_part(B, with_add):
+    """r48_conv3x3_bn_grad with fin (the BN backward's finish in its last workgroup) against the same
+    conv without it + r48_bn_backward_part's finish: the same dx bit for bit; dgamma, dbeta and the
+    apply coefficients equal to fp32 rounding (rel 1e-6, other fp64 order); r48_bn_backward_apply
+    from the standalone finish's coefficients == r48_bn_backward_part's input gradient bit for bit."""
+    import ctypes
+    from rein48_amd import _lib
+    from rein48_amd.dqn.conv import pack_conv_dgrad
+    g = torch.Generator(device="cpu").manual_seed(B + 11)
+    L = _lib.load()
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    frags = pack_conv_dgrad((torch.randn(64, 64, 3, 3, generator=g) * 0.1).to(DEV))
+    dy = torch.randn(B, 16, 64, generator=g).to(DEV).to(torch.bfloat16)
+    add = torch.randn(B, 16, 64, generator=g).to(DEV).to(torch.bfloat16) if with_add else None
+    add_mask = torch.randint(0, 256, (B * 16, 8), generator=g, dtype=torch.uint8).to(DEV) if with_add == "mask" else None
+    bn_x = (torch.randn(B, 16, 64, generator=g) + 3.0).to(DEV).to(torch.bfloat16)
+    mask = torch.randint(0, 256, (B * 16, 8), generator=g, dtype=torch.uint8).to(DEV)
+    save = torch.cat([torch.randn(64, generator=g) + 3.0, torch.rand(64, generator=g) + 0.5]).to(DEV)
+    gamma = (torch.rand(64, generator=g) + 0.5).to(DEV)
+    n = int(L.r48_conv_stats_floats())
+    part = torch.zeros(n, dtype=torch.float32, device=DEV)
+    out_r = torch.empty_like(dy)
+    _lib.check(L.r48_conv3x3_bn_grad(_lib.ptr(dy), B, _lib.ptr(frags), _lib.ptr(add), _lib.ptr(add_mask), _lib.ptr(out_r),
+                                     _lib.ptr(bn_x), _lib.ptr(mask), _lib.ptr(save), _lib.ptr(part), None, s))
+    dz = torch.randn(B, 16, 64, generator=g).to(DEV).to(torch.bfloat16)    # the gradient the apply consumes
+    ws = torch.empty(int(L.r48_bn_workspace_floats(B * 16, 64)), device=DEV)
+    dx_r, dg_r, db_r = torch.empty_like(dz), torch.empty(64, device=DEV), torch.empty(64, device=DEV)
+    _lib.check(L.r48_bn_backward_part(_lib.ptr(part), 256, _lib.ptr(dz), _lib.ptr(mask), _lib.ptr(bn_x), B * 16, 64,
+                                      _lib.ptr(gamma), _lib.ptr(save), _lib.ptr(ws), _lib.ptr(dx_r), None, _lib.ptr(dg_r),
+                                      _lib.ptr(db_r), s))
+    coef_r = ws[-192:].clone()                               # the finish's coefficients (workspace tail)
+    part2 = torch.zeros(n, dtype=torch.float32, device=DEV)
+    out = torch.empty_like(dy)
+    coef, dg, db = torch.empty(192, device=DEV), torch.empty(64, device=DEV), torch.empty(64, device=DEV)
+    fin = _fin_args(L, gamma, None, None, None, save, coef, dg, db, B * 16, 0.0, 0.0)
+    _lib.check(L.r48_conv3x3_bn_grad(_lib.ptr(dy), B, _lib.ptr(frags), _lib.ptr(add), _lib.ptr(add_mask), _lib.ptr(out),
+                                     _lib.ptr(bn_x), _lib.ptr(mask), _lib.ptr(save), _lib.ptr(part2), ctypes.byref(fin), s))
+    torch.cuda.synchronize()
+    assert torch.equal(out, out_r)
+    assert int(part2[-4:].view(torch.int32)[0]) == 0
+    torch.testing.assert_close(dg, dg_r, rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(db, db_r, rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(coef, coef_r, rtol=1e-6, atol=1e-9)
+    dx = torch.empty_like(dz)
+    _lib.check(L.r48_bn_backward_apply(_lib.ptr(dz), _lib.ptr(mask), _lib.ptr(bn_x), B * 16, 64, _lib.ptr(coef_r),
+                                       _lib.ptr(dx), s))
+    assert torch.equal(dx, dx_r)
 
 # ---------------------------------------------------------------- steady-state sizes (the bench's)
 # The tests above run the conv kernels at <= 1 tile per wave and the wgrad ring at <= 3 steps per
@@ -591,7 +702,7 @@ def test_conv3x3_kernels_at_bench_size_match_fp64(B):
     y = conv3x3(x, pack_conv(w, 64), bias, stats=st)
     assert _rel(y, y_ref) < 1e-2
     assert torch.equal(y, conv3x3(x, pack_conv(w, 64), bias))
-    rec = st.view(-1, 2, 64).double().sum(0)
+    rec = st[:-4].view(-1, 2, 64).double().sum(0)   # (the last 4 floats: the arrival counter)
     yd = y.reshape(-1, 64).double()
     for got, want in ((rec[0], yd.sum(0)), (rec[1], (yd * yd).sum(0))):
         assert float((got - want).abs().max()) <= 1e-5 * float(want.abs().max())
@@ -629,13 +740,13 @@ def test_conv3x3_bn_grad_at_bench_size_matches_fp64(B, with_add):
     part = torch.full((int(L.r48_conv_stats_floats()),), float("nan"), dtype=torch.float32, device=DEV)
     out = torch.empty_like(dy)
     _lib.check(L.r48_conv3x3_bn_grad(_lib.ptr(dy), B, _lib.ptr(frags), _lib.ptr(add), None, _lib.ptr(out),
-                                     _lib.ptr(bn_x), _lib.ptr(mask), _lib.ptr(save), _lib.ptr(part),
+                                     _lib.ptr(bn_x), _lib.ptr(mask), _lib.ptr(save), _lib.ptr(part), None,
                                      ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
     assert torch.equal(out, conv3x3(dy, frags, add=add))
     bits = ((mask.long().unsqueeze(-1) >> torch.arange(8, device=DEV)) & 1).reshape(B * 16, 64).bool()
     gd = torch.where(bits, out.reshape(-1, 64).double(), torch.zeros((), dtype=torch.float64, device=DEV))
     xd = bn_x.reshape(-1, 64).double() - save[:64].double()
-    rec = part.view(-1, 2, 64).double().sum(0)
+    rec = part[:-4].view(-1, 2, 64).double().sum(0)
     for got, terms in ((rec[0], gd), (rec[1], gd * xd)):
         err = (got - terms.sum(0)).abs()
         assert bool((err <= 1e-5 * terms.abs().sum(0) + 1e-30).all()), float(err.max())

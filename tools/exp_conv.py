@@ -47,7 +47,7 @@ part = None
 def bn_grad(dy_, add_, bnx, mask, add_mask=None):
     out = torch.empty_like(dy_)
     C.check(_lib.load().r48_conv3x3_bn_grad(C.ptr(dy_), B, C.ptr(f64), C.ptr(add_), C.ptr(add_mask), C.ptr(out), C.ptr(bnx),
-                                            C.ptr(mask), C.ptr(save), C.ptr(part), C._stream(dy_)))
+                                            C.ptr(mask), C.ptr(save), C.ptr(part), None, C._stream(dy_)))
     return out
 
 
@@ -60,7 +60,7 @@ def bn_in(x_, res_):
     z_ = torch.empty_like(x_)
     m_ = torch.empty((B * 16, 8), dtype=torch.uint8, device=dev)
     C.check(_lib.load().r48_conv3x3_bn_in(C.ptr(x_), B, C.ptr(f64), C.ptr(bias), C.ptr(coef), C.ptr(res_), C.ptr(z_),
-                                          C.ptr(m_), C.ptr(y_), C.ptr(stats), C._stream(x_)))
+                                          C.ptr(m_), C.ptr(y_), C.ptr(stats), None, C._stream(x_)))
     return y_
 
 
