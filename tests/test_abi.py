@@ -43,6 +43,26 @@ def test_library_exports_every_declared_symbol():
     assert set(_lib.SIGNATURES) == declared()
 
 
+def prototypes():
+    """name -> parameter count of every r48_ prototype in the header (comments stripped)."""
+    text = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    out = {}
+    for m in re.finditer(r"(r48_\w+)\s*\(([^;{]*?)\)\s*;", text, re.S):
+        params = m.group(2).strip()
+        out[m.group(1)] = 0 if params in ("", "void") else params.count(",") + 1
+    return out
+
+
+def test_ctypes_signatures_match_the_header_arity():
+    """Every ctypes argtypes list has exactly as many entries as the header prototype has
+    parameters (an entry point that gained an argument in include/rein48.h but not in _lib.py would
+    otherwise shift every later argument silently)."""
+    protos = prototypes()
+    assert set(protos) == declared()
+    bad = {n: (len(_lib.SIGNATURES[n][1]), k) for n, k in protos.items() if len(_lib.SIGNATURES[n][1]) != k}
+    assert not bad, bad
+
+
 def test_library_is_gfx950_code_object():
     data = open(_lib.LIB_PATH, "rb").read()
     assert b"amdgcn-amd-amdhsa--gfx950" in data  # the embedded offload bundle's target triple
