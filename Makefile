@@ -4,7 +4,7 @@ ARCH ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -Wall -Wno-unused-function
 LIBDIR := rein48_amd/lib
 SRC := rein48_amd/csrc/r48_env.hip rein48_amd/csrc/r48_a3c.hip rein48_amd/csrc/r48_policy.hip rein48_amd/csrc/r48_replay.hip rein48_amd/csrc/r48_dqn.hip rein48_amd/csrc/r48_resnet.hip rein48_amd/csrc/r48_a3c_train.hip rein48_amd/csrc/r48_bn.hip rein48_amd/csrc/r48_conv.hip rein48_amd/csrc/r48_game.hip rein48_amd/csrc/r48_mlp.hip rein48_amd/csrc/r48_mlp_train.hip
-DEPS := rein48_amd/csrc/r48_host.h rein48_amd/csrc/r48_board.h rein48_amd/csrc/r48_cnn_common.h rein48_amd/csrc/r48_mlp_common.h include/rein48.h
+DEPS := rein48_amd/csrc/r48_host.h rein48_amd/csrc/r48_board.h rein48_amd/csrc/r48_cnn_common.h rein48_amd/csrc/r48_mlp_common.h rein48_amd/csrc/r48_bn_finish.h include/rein48.h
 
 all: $(LIBDIR)/librein48.so oracle
 
