@@ -414,7 +414,8 @@ int r48_adam(float *param, const float *grad, float *m, float *v, int64_t n, flo
  * beta, gamma as the BN's. Backward: save is read (the forward's), coef = float[3C] {a, cc, d} of
  * dx = a g + cc x + d, dgamma / dbeta (nullable) = invstd sum g (x - mean), sum g. The statistics
  * buffer's last float is the arrival counter: it must be 0 before the first such call (the finishing
- * workgroup resets it). C = 64 (the update's convs). */
+ * workgroup resets it), and one buffer serves one such launch at a time (launches on one stream). C = 64
+ * (the update's convs). */
 typedef struct r48_bn_finish_args {
     const float *gamma;
     const float *beta;
