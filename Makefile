@@ -11,8 +11,10 @@ all: $(LIBDIR)/librein48.so oracle
 OBJDIR := build/obj
 OBJ := $(patsubst rein48_amd/csrc/%.hip,$(OBJDIR)/%.o,$(SRC))
 # the fused A3C update keeps its loop-carried gradient slices in AGPRs and its MFMA results in
-# VGPRs (no accumulator round trips through v_accvgpr_read before each epilogue)
-FLAGS_r48_a3c_train := -mllvm -amdgpu-mfma-vgpr-form=1
+# VGPRs (no accumulator round trips through v_accvgpr_read before each epilogue); LLVM's
+# max-memory-clause machine scheduler: -1.5 % per 10^8 rows, bit-identical (four alternated rounds,
+# process per library, A/A control: profiles/r06/a3c/train/sched_strategy_ab.txt)
+FLAGS_r48_a3c_train := -mllvm -amdgpu-mfma-vgpr-form=1 -mllvm -amdgpu-sched-strategy=max-memory-clause
 # the CNN rollout megakernel: the max-ILP machine scheduler (rollout 7.82 -> 7.70 ms textbook, 7.46 -> 7.35 ms
 # reference over 4 alternated samples each, profiles/r04/a3c/rollout_sched_max_ilp_ab.txt)
 FLAGS_r48_policy ?= -mllvm -amdgpu-sched-strategy=max-ilp
