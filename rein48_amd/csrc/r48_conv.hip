@@ -444,10 +444,12 @@ __device__ __forceinline__ bf16x8 tr_pair(const uint16_t *p0, const uint16_t *p1
     return f;
 }
 
-// gradient accumulation in AGPRs; operands straight from LDS reads (no VALU wait states needed)
+// gradient accumulation (36 accumulators = 144 registers: more than the 128 AGPRs a wave gets at
+// two waves per SIMD, so the builtin, whose hazards hipcc pads, with the accumulators where it
+// places them)
 __device__ __forceinline__ void acc16(f32x4 &acc, const bf16x8 &a, const bf16x8 &b)
 {
-    asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
 }
 
 // One DMA of 64 x 16 bytes: rows [row0, row0 + 512 / COLS) of a [rows][COLS] bf16 tensor into the
@@ -473,9 +475,13 @@ __device__ __forceinline__ void dma_rows(const uint16_t *src, int64_t row0, int6
     static_assert(kRows * kChunks == 64, "one DMA = 64 chunks");
 }
 
-// partial record per workgroup: [9 taps][64 co][CIN ci] fp32. Eight waves (two per SIMD, so one
-// wave's DMA issue and barrier waits run under the other's MFMAs): wave w owns input-channel tile
-// w % (CIN / 16) and output tiles of its share, for every tap.
+// partial record per workgroup: [9 taps][64 co][CIN ci] fp32. Eight waves, two per SIMD (one wave's
+// DMA issue and barrier waits run under the other's MFMAs). Wave w owns input-channel tile w % NCT
+// and ALL four output tiles, for every tap, over its share of each step's k-steps: k-steps
+// kPer (w / NCT) .. kPer (w / NCT + 1) - 1 (split K). Its dy^T fragments then feed 9 MFMAs each and its
+// x^T fragments 4: 13 transposed fragment pairs per 36 MFMAs (the former split by output tile read
+// 11 per 18, and the CU's LDS read port, not the MFMA pipe, set the step time). The kSplit waves of
+// one channel tile add their accumulators in wave order through LDS at the end (deterministic).
 constexpr int kWgWaves = 8;
 
 template <int CIN>
@@ -485,112 +491,80 @@ __global__ __launch_bounds__(64 * kWgWaves, 1) void k_conv_wgrad(const uint16_t 
 {
     constexpr int kThr = 64 * kWgWaves;
     constexpr int NCT = CIN / 16;                                // input-channel tiles of 16
-    constexpr int kCoT = 4 * NCT / kWgWaves;                     // output tiles per wave (2 or 1)
-    static_assert(kCoT >= 1 && kCoT * kWgWaves == 4 * NCT, "wave split");
+    constexpr int kSplit = kWgWaves / NCT;                       // waves per channel tile (2 or 4)
+    constexpr int kPer = kKSteps / kSplit;                       // k-steps per wave and step (2 or 1)
+    static_assert(kSplit * NCT == kWgWaves && kPer * kSplit == kKSteps, "wave split");
     constexpr int kDyImg = kStepRows * kCout, kXImg = kXRows * CIN;
     constexpr int kBuf = kDyImg + kXImg;
     constexpr int kDyRowsPerDma = 512 / kCout, kXRowsPerDma = 512 / CIN;
     constexpr int kDyDmas = kStepRows / kDyRowsPerDma, kXDmas = kStepRows / kXRowsPerDma;   // per step
     constexpr int kDmas = kDyDmas + kXDmas;
+    constexpr int kMyDmas = kDmas / kWgWaves;                    // per wave and step (4 or 3)
     static_assert(kDyDmas * kDyRowsPerDma == kStepRows && kXDmas * kXRowsPerDma == kStepRows, "staging split");
+    static_assert(kMyDmas * kWgWaves == kDmas && kDyDmas % kWgWaves == 0, "the same DMA count for every wave");
+    // the end's partial sums (one tap at a time) reuse the ring
+    static_assert((kSplit - 1) * NCT * 4 * 64 * 8 <= kRing * kBuf, "partial sums fit the ring");
     __shared__ __attribute__((aligned(16))) uint16_t lds[kRing * kBuf];   // the only LDS object
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int i16 = lane & 15, g = lane >> 4;
-    const int ct = wave % NCT;                                   // input-channel tile of this wave
-    const int cot0 = (wave / NCT) * kCoT;                        // first output tile of this wave
-    // DMA d = wave, wave + 8, ... of a step (dy pieces first): this wave's count per step
-    const int my_dmas = (kDmas - wave + kWgWaves - 1) / kWgWaves;
+    const int ct = wave % NCT, kh = wave / NCT;                  // channel tile, k share of this wave
     for (int i = threadIdx.x; i < kRing * kKSteps * CIN; i += kThr) {   // zero bands (never overwritten)
         const int buf = i / (kKSteps * CIN), k = i % (kKSteps * CIN);
         lds[buf * kBuf + kDyImg + (kZeroRow + 32 * (k / CIN)) * CIN + k % CIN] = 0;
     }
-    // transposed-read addresses of k-step 0 (k-step ks adds 32 ks rows). A (dy^T, lanes = co):
-    // rows 8g + 4u + q, columns 16 cot + 4p (lane 4q + p of a 16-lane group addresses row q of the
-    // group's 4-row block). B (x^T shifted by tap t, lanes = ci): row + off(t) when that cell is in
-    // the grid, else the zero row.
+    // transposed-read addresses of this wave's first k-step (its k-step kk adds 32 kk rows). A (dy^T,
+    // lanes = co): rows 8g + 4u + q, columns 16 o + 4p (lane 4q + p of a 16-lane group addresses row q
+    // of the group's 4-row block). B (x^T shifted by tap t, lanes = ci): row + off(t) when that cell is
+    // in the grid, else the zero row (the zero band keeps both 32-row periodic, swz has period 16).
     const int q = i16 >> 2, p4 = i16 & 3;
-    int a_off[kCoT][2], b_off[9][2];
+    int a_off[4][2], b_off[9][2];
 #pragma unroll
     for (int u = 0; u < 2; u++) {
         const int row = 8 * g + 4 * u + q;
 #pragma unroll
-        for (int j = 0; j < kCoT; j++)
-            a_off[j][u] = wimg<kCout>(row, 16 * (cot0 + j) + 4 * p4);
+        for (int o = 0; o < 4; o++)
+            a_off[o][u] = wimg<kCout>(row + 32 * kPer * kh, 16 * o + 4 * p4);
 #pragma unroll
         for (int t = 0; t < 9; t++) {
             const int src = in_grid(row & 15, t) ? row + tap_off(t) : kZeroRow;
-            b_off[t][u] = kDyImg + wimg<CIN>(src, 16 * ct + 4 * p4);
+            b_off[t][u] = kDyImg + wimg<CIN>(src + 32 * kPer * kh, 16 * ct + 4 * p4);
         }
     }
-    f32x4 acc[9][kCoT];
+    f32x4 acc[9][4];
 #pragma unroll
     for (int t = 0; t < 9; t++)
 #pragma unroll
-        for (int j = 0; j < kCoT; j++)
-            acc[t][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int o = 0; o < 4; o++)
+            acc[t][o] = f32x4{0.f, 0.f, 0.f, 0.f};
     // this workgroup's steps: blockIdx.x + i * gridDim.x (the grid sweeps the tensors in order)
     const int64_t rows_total = boards * 16, last = rows_total - 1;
     const int64_t steps_total = (rows_total + kStepRows - 1) / kStepRows;
     const int64_t n_my = blockIdx.x < steps_total ? (steps_total - blockIdx.x + gridDim.x - 1) / gridDim.x : 0;
-    // stage this workgroup's step i into ring buffer `buf`: this wave issues its my_dmas DMAs.
-    // Steps past the end are staged too (clamped rows, a buffer nobody reads), so every step
-    // issues the same count and the counted wait below stays exact.
-    auto stage = [&](int64_t i, int buf) {
-        uint16_t *dimg = lds + buf * kBuf, *ximg = dimg + kDyImg;
-        const int64_t row0 = ((int64_t)blockIdx.x + i * gridDim.x) * kStepRows;
-#pragma unroll
-        for (int k = 0; k < (kDmas + kWgWaves - 1) / kWgWaves; k++) {
-            const int d = wave + k * kWgWaves;
-            if (d < kDyDmas)
-                dma_rows<kCout>(dy, row0 + d * kDyRowsPerDma, last, dimg, d * kDyRowsPerDma, lane);
-            else if (d < kDmas)
-                dma_rows<CIN>(x, row0 + (d - kDyDmas) * kXRowsPerDma, last, ximg, (d - kDyDmas) * kXRowsPerDma,
-                              lane);
-        }
-    };
-    // one DMA of this wave (its k-th of the step) for step i into ring buffer `buf`
+    // one DMA of this wave (its k-th of the step) for step i into ring buffer `buf`. Steps past the
+    // end are staged too (clamped rows, a buffer nobody reads), so every step issues the same count
+    // and the counted wait below stays exact.
     auto stage_one = [&](int64_t i, int buf, int k) {
         uint16_t *dimg = lds + buf * kBuf, *ximg = dimg + kDyImg;
         const int64_t row0 = ((int64_t)blockIdx.x + i * gridDim.x) * kStepRows;
-        const int d = wave + k * kWgWaves;
-        if (d < kDyDmas)
+        const int d = wave + k * kWgWaves;                       // dy pieces first: d < kDyDmas iff k < 2
+        if (k < kDyDmas / kWgWaves)
             dma_rows<kCout>(dy, row0 + d * kDyRowsPerDma, last, dimg, d * kDyRowsPerDma, lane);
-        else if (d < kDmas)
+        else
             dma_rows<CIN>(x, row0 + (d - kDyDmas) * kXRowsPerDma, last, ximg, (d - kDyDmas) * kXRowsPerDma, lane);
-    };
-    static_assert(kKSteps == 4 && kDmas <= kKSteps * kWgWaves, "one DMA per wave and k-step");
-    auto compute = [&](int buf, int ks0, int ks1) {
-        const uint16_t *img = lds + buf * kBuf;
-#pragma unroll
-        for (int ks = ks0; ks < ks1; ks++) {
-            bf16x8 A[kCoT];
-#pragma unroll
-            for (int j = 0; j < kCoT; j++)
-                A[j] = tr_pair(img + a_off[j][0] + 32 * ks * kCout, img + a_off[j][1] + 32 * ks * kCout);
-#pragma unroll
-            for (int t = 0; t < 9; t++) {
-                const bf16x8 B = tr_pair(img + b_off[t][0] + 32 * ks * CIN, img + b_off[t][1] + 32 * ks * CIN);
-#pragma unroll
-                for (int j = 0; j < kCoT; j++)
-                    acc16(acc[t][j], A[j], B);
-            }
-        }
     };
     __syncthreads();                                              // zero bands written
 #pragma unroll
     for (int i = 0; i < kRing - 1; i++)
-        stage(i, i);
+#pragma unroll
+        for (int k = 0; k < kMyDmas; k++)
+            stage_one(i, i, k);
     for (int64_t i = 0; i < n_my; i++) {
         const int64_t s = (int64_t)blockIdx.x + i * gridDim.x;
         const int buf = (int)(i % kRing);
-        // this wave's DMAs of step s done (steps s + 1, s + 2 may stay in flight), then the barrier
-        // that orders them for every reader -- and that every wave passes only after its reads of
-        // step s - 1, whose buffer is restaged below
-        if (my_dmas == 4)
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"((kRing - 2) * 4) : "memory");
-        else
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"((kRing - 2) * 3) : "memory");
-        static_assert(kDmas <= 4 * kWgWaves && kDmas > 2 * kWgWaves && kDmas % kWgWaves == 0, "3 or 4 DMAs a step");
+        // this wave's DMAs of step s done (step s + 1's may stay in flight), then the barrier that
+        // orders them for every reader -- and that every wave passes only after its reads of step
+        // s - 1, whose buffer is restaged below
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"((kRing - 2) * kMyDmas) : "memory");
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         if (s == steps_total - 1 && rows_total - s * kStepRows < kStepRows) {
@@ -604,39 +578,57 @@ __global__ __launch_bounds__(64 * kWgWaves, 1) void k_conv_wgrad(const uint16_t 
                 ximg[real * CIN + i] = 0;
             __syncthreads();
         }
-        if constexpr (kDmas == kKSteps * kWgWaves) {
-            // one DMA of step i + kRing - 1 (into the buffer of step i - 1) per k-step and wave: the
-            // CU's 32 DMAs of a step issue in four bursts of 8 instead of one burst right after the
-            // barrier, which queued each wave's issue behind the others' (tools/exp_conv.py, inputs
-            // past the Infinity Cache: 92-95 -> 85-87 us; inside the update, with dy just written and
-            // cache-resident: 77 us either way)
+        const uint16_t *img = lds + buf * kBuf;
+        const int nbuf = (buf + kRing - 1) % kRing;
+        // this wave's DMAs of step i + kRing - 1 (into the buffer of step i - 1) spread over its
+        // (k-step, tap) items, so that the CU's DMAs issue in bursts of 8 under the MFMAs
+        constexpr int kItems = kPer * 9;
 #pragma unroll
-            for (int ks = 0; ks < kKSteps; ks++) {
-                stage_one(i + kRing - 1, (buf + kRing - 1) % kRing, ks);
-                compute(buf, ks, ks + 1);
+        for (int kk = 0; kk < kPer; kk++) {
+            bf16x8 A[4];
+#pragma unroll
+            for (int o = 0; o < 4; o++)
+                A[o] = tr_pair(img + a_off[o][0] + 32 * kk * kCout, img + a_off[o][1] + 32 * kk * kCout);
+#pragma unroll
+            for (int t = 0; t < 9; t++) {
+#pragma unroll
+                for (int k = 0; k < kMyDmas; k++)
+                    if ((k * kItems) / kMyDmas == kk * 9 + t)
+                        stage_one(i + kRing - 1, nbuf, k);
+                const bf16x8 B = tr_pair(img + b_off[t][0] + 32 * kk * CIN, img + b_off[t][1] + 32 * kk * CIN);
+#pragma unroll
+                for (int o = 0; o < 4; o++)
+                    acc16(acc[t][o], A[o], B);
             }
-        } else {
-            // 3 DMAs per wave (32 input channels): issued between the two k-step halves, under the
-            // first one's MFMAs (measured faster here than one per k-step)
-            compute(buf, 0, 2);
-            __builtin_amdgcn_sched_barrier(0);
-            stage(i + kRing - 1, (buf + kRing - 1) % kRing);
-            __builtin_amdgcn_sched_barrier(0);
-            compute(buf, 2, 4);
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");              // no DMA outlives the kernel
-    // record: D[m = co 16][n = ci 16], lane l: column i16 (ci), rows 4g + i (co). 24 wait states
-    // between the last accumulating MFMA and the AGPR reads
-    asm volatile("s_nop 15\n\ts_nop 7" ::: "memory");
+    __syncthreads();                                              // every read of the ring done
+    // record: D[m = co 16][n = ci 16], lane l: column i16 (ci), rows 4g + i (co) of output tile o.
+    // Waves kh > 0 park a tap's accumulators in the ring, wave kh = 0 of the tile adds them in order.
+    f32x4 *part = reinterpret_cast<f32x4 *>(lds);
     float *rec = partials + (int64_t)blockIdx.x * 9 * kCout * CIN;
 #pragma unroll
-    for (int t = 0; t < 9; t++)
+    for (int t = 0; t < 9; t++) {
+        if (kh > 0)
 #pragma unroll
-        for (int j = 0; j < kCoT; j++)
+            for (int o = 0; o < 4; o++)
+                part[(((kh - 1) * NCT + ct) * 4 + o) * 64 + lane] = acc[t][o];
+        __syncthreads();
+        if (kh == 0) {
 #pragma unroll
-            for (int i = 0; i < 4; i++)
-                rec[(t * kCout + 16 * (cot0 + j) + 4 * g + i) * CIN + 16 * ct + i16] = acc[t][j][i];
+            for (int o = 0; o < 4; o++) {
+                f32x4 v = acc[t][o];
+#pragma unroll
+                for (int h = 1; h < kSplit; h++)
+                    v += part[(((h - 1) * NCT + ct) * 4 + o) * 64 + lane];
+#pragma unroll
+                for (int i = 0; i < 4; i++)
+                    rec[(t * kCout + 16 * o + 4 * g + i) * CIN + 16 * ct + i16] = v[i];
+            }
+        }
+        __syncthreads();
+    }
 }
 
 // Fixed-order sum of n_rec <= kRedGroup^2 records of len4 float4 entries in ONE pass: a block of

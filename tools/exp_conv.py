@@ -4,7 +4,7 @@ reduction epilogue with and without the residual add (dg64bn, add64bn), r48_conv
 32) for the product library and variant libraries
 (tools/build_variant.sh), at `boards` boards, with a bit-level digest of every output.
 
-    python tools/exp_conv.py [boards] [lib.so ...]
+    python tools/exp_conv.py [boards] [lib.so ...]      (CASES=a,b: only those cases)
 """
 import os
 import sys
@@ -100,8 +100,11 @@ for path in libs:
             "add64bn": lambda: bn_grad(rot(dys), rot(x64s), rot(x64s), rot(masks)),
             "addm64bn": lambda: bn_grad(rot(dys), rot(x64s), rot(x64s), rot(masks), rot(masks)),
             "wgrad64": lambda: C.conv3x3_wgrad(rot(dys), rot(x64s)), "wgrad32": lambda: C.conv3x3_wgrad(rot(dys), rot(x32s))}
+    only = os.environ.get("CASES")                     # e.g. CASES=wgrad64,wgrad32
     line = []
     for k, fn in runs.items():
+        if only and k not in only.split(","):
+            continue
         _rot[0] = -1
         out = fn()
         torch.cuda.synchronize()
